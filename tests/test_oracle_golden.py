@@ -1,0 +1,146 @@
+"""Pin the CPU oracle (oracle/facevae_cpu.py) against fixtures produced by the reference.
+
+CPU only.  The fixtures come from tests/golden/make_golden.py (reference classes imported
+from /root/reference in the build container).
+"""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import facevae_cpu as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    return torch.load(os.path.join(GOLD, name), weights_only=True)
+
+
+def rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+
+def dead_bias_keys(cfg):
+    """Conv biases that feed a training-mode BN: their gradient is rounding noise (SURVEY.md
+    Appendix A.6), so Adam moves them by ~±lr in a noise-determined direction.  They cannot
+    change any output; compared with an absolute tolerance of 2*lr per step."""
+    keys = set()
+    for s in O.conv_specs(cfg):
+        if s.block == "cna" or (s.block == "nac" and ".layers.0.layers.2" in s.prefix):
+            keys.add(s.prefix + ".bias")
+    return keys
+
+
+def check_state(sd, ref, cfg, steps, tol):
+    dead = dead_bias_keys(cfg)
+    for k, v in ref.items():
+        a = sd[k].detach()
+        if not v.is_floating_point():
+            assert torch.equal(a, v), k
+        elif k in dead:
+            assert (a - v).abs().max().item() <= 2 * cfg.lr * steps + 1e-7, k
+        else:
+            assert rel(a, v) < tol, k
+
+
+def test_init_matches_reference_construction():
+    g = load("toy_step.pt")
+    sd = O.init_state(O.OracleConfig.toy(), seed=0)
+    assert set(sd) == set(g["init"])
+    for k in sd:
+        assert torch.equal(sd[k], g["init"][k]), k
+
+
+def test_full_init_checksums():
+    g = load("full256.pt")
+    sd = O.init_state(O.OracleConfig(), seed=0)
+    assert set(sd) == set(g["init_checksums"])
+    for k, v in sd.items():
+        s = torch.tensor([v.double().sum().item(), v.double().abs().sum().item()], dtype=torch.float64)
+        assert torch.allclose(s, g["init_checksums"][k].double(), rtol=1e-12, atol=1e-9), k
+
+
+def test_toy_step_matches_reference():
+    g = load("toy_step.pt")
+    cfg = O.OracleConfig.toy()
+    sd = O.prepare_state(g["init"])
+    opt = O.adam_init(sd)
+    out, grads = O.train_step(sd, opt, g["x"], g["eps"], cfg)
+    s1 = g["step1"]
+    assert rel(out["y"], s1["y"]) < 1e-6
+    assert rel(out["mu"], s1["mu"]) < 1e-6
+    assert abs(out["R"].item() - s1["R"].item()) <= 1e-6 * abs(s1["R"].item())
+    assert abs(out["K"].item() - s1["K"].item()) <= 1e-6 * abs(s1["K"].item())
+    dead = dead_bias_keys(cfg)
+    for k, gr in s1["grads"].items():
+        if k in dead:
+            assert (grads[k] - gr).abs().max().item() < 1e-6, k
+        else:
+            assert rel(grads[k], gr) < 1e-5, k
+    check_state(sd, s1["state"], cfg, 1, 1e-6)
+    # steps 2, 3
+    Rs, Ks = [out["R"].item()], [out["K"].item()]
+    for _ in range(2):
+        o, _ = O.train_step(sd, opt, g["x"], g["eps"], cfg)
+        Rs.append(o["R"].item())
+        Ks.append(o["K"].item())
+    assert torch.allclose(torch.tensor(Rs, dtype=torch.float64), g["step3"]["R"].double(), rtol=1e-5)
+    assert torch.allclose(torch.tensor(Ks, dtype=torch.float64), g["step3"]["K"].double(), rtol=1e-5)
+    assert rel(o["y"], g["step3"]["y"]) < 1e-5
+    check_state(sd, g["step3"]["state"], cfg, 3, 1e-5)
+
+
+def test_full256_two_steps_match_reference():
+    g = load("full256.pt")
+    cfg = O.OracleConfig()
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    sd = O.prepare_state(O.init_state(cfg, 0))
+    opt = O.adam_init(sd)
+    B = 2
+    x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1234))
+    eps = torch.randn(B, 256, 64, 64, generator=torch.Generator().manual_seed(1235))
+    o1, _ = O.train_step(sd, opt, x, eps, cfg)
+    o2, _ = O.train_step(sd, opt, x, eps, cfg)
+    assert torch.allclose(torch.stack([o1["R"], o2["R"]]).double(), g["R"].double(), rtol=1e-5)
+    assert torch.allclose(torch.stack([o1["K"], o2["K"]]).double(), g["K"].double(), rtol=1e-5)
+    assert rel(o1["y"][:, :, ::17, ::13], g["y1_samples"]) < 1e-5
+
+
+BLOCKS = ["cna_relu", "cna_leaky_sn", "cna_7x7", "down", "up_sn", "res_sn", "same"]
+
+
+def oracle_block(name, sd, x):
+    """Each reference block restated with the oracle primitives (prefix '' -> 'layers')."""
+    sd = {"m." + k: v for k, v in sd.items()}
+    if name == "cna_relu" or name == "cna_7x7":
+        return O.conv_block(sd, "m", x, "CNA", True), sd
+    if name == "same":                                   # SameBlock2D.layers is the ConvBlock2D
+        return O.conv_block(sd, "m.layers", x, "CNA", True), sd
+    if name == "cna_leaky_sn":
+        return O.conv_block(sd, "m", x, "CNA", True, "leakyrelu"), sd
+    if name == "down":
+        return F.avg_pool2d(O.conv_block(sd, "m.layers.0", x, "CNA", True), 2), sd
+    if name == "up_sn":
+        return O.conv_block(sd, "m.layers.1", F.interpolate(x, scale_factor=2.0), "CNA", True), sd
+    if name == "res_sn":
+        t = O.conv_block(sd, "m.layers.0", x, "NAC", True)
+        return x + O.conv_block(sd, "m.layers.1", t, "NAC", True), sd
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", BLOCKS)
+def test_block_cases(name):
+    c = load("blocks.pt")[name]
+    sd = O.prepare_state(c["init"])
+    x = c["x"].clone().requires_grad_(True)
+    y, sdp = oracle_block(name, sd, x)
+    assert rel(y, c["y"]) < 1e-6
+    (y * c["gy"]).sum().backward()
+    assert rel(x.grad, c["gx"]) < 1e-5
+    for k, gr in c["grads"].items():
+        assert rel(sdp["m." + k].grad, gr) < 1e-5, k
+    for k, v in c["state"].items():
+        if v.is_floating_point():
+            assert rel(sdp["m." + k].detach(), v) < 1e-6, k
