@@ -1,0 +1,177 @@
+"""FaceVAE training-step benchmark (BASELINE.json metric: training images/sec of the
+256x256 face-VAE step; MFMA utilisation).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--res 256] [--dtype bf16]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = zero_grad -> forward (AFE trunk, reparam, Generator trunk) -> MSE + KL ->
+backward (+ RCCL gradient all-reduce, SyncBN collectives when N > 1) -> Adam, on synthetic
+VoxCeleb-shaped frames x ~ U[0,1) [B,3,H,H] and eps ~ N(0,1), resident in HBM before the
+timed region.  Weak scaling: B images per GPU.  Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import fvamd  # noqa: E402,F401
+import facevae_amd as fv  # noqa: E402
+from facevae_amd import ops  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 2.4 GHz x 4096 FLOP/clk (dense), MI355X_MICROARCH.md
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU")
+    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-syncbn", action="store_true", help="per-rank BN statistics (labelled)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def conv_launch_flops(d):
+    """Algorithmic FLOPs of one conv launch (reference formulation)."""
+    return 2.0 * d.n * d.h * d.w * d.cout * d.cin_valid * d.ksize * d.ksize
+
+
+def cpu_baseline(args, cfg):
+    """The oracle (fp32 torch-CPU restatement of the reference step) on a bounded sample."""
+    from oracle import facevae_cpu as O   # checker / baseline only
+    torch.set_num_threads(args.cpu_threads)
+    ocfg = O.OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent, n_res=cfg.n_res,
+                          up_seq=cfg.up_seq)
+    B = 2
+    sd = O.prepare_state(O.init_state(ocfg, 0))
+    opt = O.adam_init(sd)
+    x = torch.rand(B, 3, cfg.H, cfg.H, generator=torch.Generator().manual_seed(1234))
+    eps = torch.randn(B, cfg.latent, cfg.latent_hw, cfg.latent_hw, generator=torch.Generator().manual_seed(1235))
+    O.train_step(sd, opt, x, eps, ocfg)                          # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.train_step(sd, opt, x, eps, ocfg)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds or n >= 50:
+            break
+    return {"value": round(n * B / dt, 4), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle fp32 step at {cfg.H}x{cfg.H}, batch {B}, {n} timed steps ({dt:.1f} s) after 1 warm-up"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        fv.distributed.init_dist(local, world, syncbn=not args.no_syncbn)
+    torch.cuda.set_device(local)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    cfg = fv.FaceVAEConfig(H=args.res)
+    torch.manual_seed(0)
+    model = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(dtype)
+    net = fv.distributed.DataParallel(model) if world > 1 else model
+    opt = fv.Adam(model.parameters(), lr=cfg.lr, betas=cfg.betas)
+    rec, kl = fv.ReconLoss(), fv.KLDivergenceLoss()
+    B = args.batch
+    g = torch.Generator().manual_seed(1234 + rank)
+    x = torch.rand(B, 3, cfg.H, cfg.H, generator=g).cuda()
+    eps = torch.randn(B, cfg.latent, cfg.latent_hw, cfg.latent_hw,
+                      generator=torch.Generator().manual_seed(1235 + rank)).cuda()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        y, mu, logstd = net(x, eps)
+        loss = cfg.w_R * rec((x, y)) + cfg.w_K * kl((mu, logstd))
+        loss.backward()
+        opt.step()
+        return loss
+
+    # dominant kernel family: the ResBlock 3x3 256->256 convs at the latent resolution
+    res_c = cfg.up_seq[0]
+
+    def is_res(kind, d):
+        return d.ksize == 3 and d.pro_act == 1 and d.cin_valid == res_c and d.cout == res_c
+
+    timer = ops.KernelTimer(is_res)
+    ops.TIMER = timer
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.enabled = True
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = tt.item()
+    assert torch.isfinite(loss).item()
+
+    ms = t / args.steps * 1e3
+    ips = world * B * args.steps / t
+    ev = timer.summary()
+    # algorithmic FLOPs of one res-conv launch (fwd, dgrad and wgrad have equal work)
+    P = B * cfg.latent_hw * cfg.latent_hw
+    f_launch = 2.0 * P * res_c * res_c * 9
+    fam = {k: sum(v) / len(v) for k, v in ev.items() if v}
+    dom = max(fam, key=lambda k: fam[k] * len(ev[k])) if fam else None
+    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+    roof = None
+    if dom is not None:
+        ach = f_launch / (fam[dom] * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": f"conv3x3 {res_c}->{res_c} {dom} @{cfg.latent_hw}x{cfg.latent_hw} B={B}",
+                "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                "avg_ms": round(fam[dom], 4), "flop_per_launch": f_launch, "traffic": None,
+                "families_avg_ms": {k: round(v, 4) for k, v in fam.items()}}
+    from oracle.facevae_cpu import OracleConfig, flops_per_image
+    _, f_img = flops_per_image(OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent,
+                                            n_res=cfg.n_res, up_seq=cfg.up_seq))
+    step_util = ips / world * f_img / (peak * 1e12)
+    out = {
+        "metric": "training images/sec (256x256 face-VAE step)" if cfg.H == 256 else
+                  f"training images/sec ({cfg.H}x{cfg.H} face-VAE step)",
+        "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (x~U[0,1), eps~N(0,1); seed-0 random init)",
+        "config": {"workload": f"FaceVAE step {cfg.H}x{cfg.H} (AFE trunk + reparam + Generator trunk, MSE+KL, Adam)",
+                   "global_batch": B * world, "per_gpu_batch": B, "resolution": cfg.H,
+                   "parallelism": f"dp{world}" + ("" if world == 1 else (" syncbn" if not args.no_syncbn else " local-bn"))},
+        "mfma_util_step": round(step_util, 4),
+        "step_flop_per_image": f_img,
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(args, cfg)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,27 @@
+"""facevae_amd — MI355X-native (gfx950) FaceVAE training step.
+
+Import as `facevae_amd` (see `load_package()` in the repo root's __graft_entry__.py, or
+`import fvamd` which registers the package under that name).
+
+Hot path: AFE 2-D trunk -> latent split/reparam -> Generator 2-D trunk,
+MSE + KL, Adam; every compute op is a hand-written HIP kernel in libfacevae.so called
+through the C-ABI in include/facevae.h.
+"""
+from . import _lib
+from .config import FaceVAEConfig, compute_dtype, set_compute_dtype
+from .losses import KLDivergenceLoss, L1Loss, ReconLoss
+from .models import AFE, FaceVAE, Generator
+from .modules import Conv2d, ConvBlock2D, DownBlock2D, ResBlock2D, SameBlock2D, UpBlock2D
+from .optim import Adam
+from . import distributed, ops
+
+__all__ = ["FaceVAEConfig", "compute_dtype", "set_compute_dtype", "KLDivergenceLoss", "L1Loss", "ReconLoss",
+           "AFE", "FaceVAE", "Generator", "Conv2d", "ConvBlock2D", "DownBlock2D", "ResBlock2D", "SameBlock2D",
+           "UpBlock2D", "Adam", "distributed", "ops", "FaceVAETrainer"]
+
+
+def __getattr__(name):
+    if name == "FaceVAETrainer":
+        from .trainer import FaceVAETrainer
+        return FaceVAETrainer
+    raise AttributeError(name)

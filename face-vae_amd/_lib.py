@@ -1,0 +1,150 @@
+"""ctypes binding of libfacevae.so (the C-ABI declared in include/facevae.h).
+
+The library is built in-tree (face-vae_amd/csrc/build.py -> face-vae_amd/libfacevae.so).
+There is no fallback: if the library is missing or a call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int, c_long, c_size_t, c_void_p
+
+import torch  # noqa: F401  (must be imported first: the HIP runtime is shared with torch)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfacevae.so")
+
+FV_F32, FV_BF16, FV_F64 = 0, 1, 2
+ADAM_CHUNK = 4096
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [
+        ("dtype", c_int), ("n", c_int), ("h", c_int), ("w", c_int),
+        ("cin", c_int), ("cin_valid", c_int), ("cout", c_int), ("ldy", c_int),
+        ("ksize", c_int), ("upsample", c_int), ("pro_act", c_int), ("pro_slope", c_float),
+        ("epi_sigmoid", c_int), ("out_nchw_f32", c_int),
+    ]
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p),
+                ("exp_avg_sq", c_void_p), ("numel", c_long)]
+
+
+P = c_void_p
+D = POINTER(ConvDesc)
+# name -> (restype, argtypes)
+_SIGS = {
+    "fv_abi_version": (c_int, []),
+    "fv_last_error": (ctypes.c_char_p, []),
+    "fv_conv_wk_elems": (c_size_t, [D]),
+    "fv_conv_wt_elems": (c_size_t, [D]),
+    "fv_conv2d_stats_blocks": (c_int, [D]),
+    "fv_conv2d_stats_block_pixels": (c_int, [D]),
+    "fv_conv_weight_prep": (c_int, [D, P, P, P, P, P]),
+    "fv_conv2d_fwd": (c_int, [D, P, P, P, P, P, P, P, P, P]),
+    "fv_conv2d_bwd_data": (c_int, [D, P, c_int, P, P, P]),
+    "fv_conv2d_wgrad_nsplit": (c_int, [D]),
+    "fv_conv2d_wgrad_slab_elems": (c_size_t, [D]),
+    "fv_conv2d_bwd_weight": (c_int, [D, P, P, P, P, c_int, P, P, P]),
+    "fv_conv2d_wgrad_reduce": (c_int, [D, P, P, P, P, P]),
+    "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),
+    "fv_spectral_norm_fwd": (c_int, [P, c_int, c_int, P, P, P, c_int, P, P]),
+    "fv_spectral_norm_bwd": (c_int, [P, P, c_int, c_int, P, P, P, P, P, P]),
+    "fv_bn_ws_bytes": (c_size_t, [c_int]),
+    "fv_bn_stats_from_partials": (c_int, [P, c_int, c_int, c_long, c_int, P, P, P]),
+    "fv_bn_stats_tensor": (c_int, [c_int, P, c_long, c_int, c_int, P, P, P]),
+    "fv_bn_finalize": (c_int, [P, c_int, P, P, c_float, c_float, c_int, P, P, P, P, P, P, P]),
+    "fv_bn_act_fwd": (c_int, [c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, c_float, c_int, P, P]),
+    "fv_bn_act_bwd_reduce": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_float,
+                                     c_int, P, P, P]),
+    "fv_bn_bwd_finalize": (c_int, [P, c_int, c_long, P, P, P, P]),
+    "fv_bn_act_bwd_apply": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_float,
+                                    c_int, P, P, P, P]),
+    "fv_nchw_to_nhwc": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "fv_nhwc_to_nchw": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "fv_cast": (c_int, [c_int, P, c_int, P, c_long, P]),
+    "fv_upsample2x_bwd": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "fv_sigmoid_bwd_to_nhwc": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, P, P]),
+    "fv_loss_ws_bytes": (c_size_t, []),
+    "fv_reparam_fwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P]),
+    "fv_reparam_bwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P, P]),
+    "fv_kl_fwd": (c_int, [c_int, P, P, c_long, P, P, P]),
+    "fv_kl_bwd": (c_int, [c_int, P, P, c_long, P, P, P, P]),
+    "fv_mse_fwd": (c_int, [P, P, c_long, P, P, P]),
+    "fv_mse_bwd": (c_int, [P, P, c_long, P, P, P, P]),
+    "fv_l1_fwd": (c_int, [P, P, c_long, P, P, P]),
+    "fv_l1_bwd": (c_int, [P, P, c_long, P, P, P, P]),
+    "fv_adam_step": (c_int, [P, P, c_int, c_float, c_float, c_float, c_float, c_long, P]),
+    "fv_comm_unique_id": (c_int, [P]),
+    "fv_comm_init": (c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "fv_comm_allreduce": (c_int, [c_void_p, P, c_size_t, c_int, c_int, P]),
+    "fv_comm_allgather": (c_int, [c_void_p, P, P, c_size_t, c_int, P]),
+    "fv_comm_broadcast": (c_int, [c_void_p, P, c_size_t, c_int, c_int, P]),
+    "fv_comm_destroy": (c_int, [c_void_p]),
+}
+
+_lib = None
+
+
+class FaceVAELibError(RuntimeError):
+    pass
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def load():
+    """Load libfacevae.so (idempotent).  Raises if it is missing — there is no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `python face-vae_amd/csrc/build.py` "
+                          "(or __graft_entry__.build()); the FaceVAE path has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.fv_abi_version() != 1:
+        raise ImportError("libfacevae ABI mismatch")
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Call an fv_* entry; raise FaceVAELibError with fv_last_error() on failure."""
+    lib = load()
+    st = getattr(lib, name)(*args)
+    if st != 0:
+        msg = lib.fv_last_error().decode(errors="replace")
+        raise FaceVAELibError(f"{name} failed ({st}): {msg}")
+    return st
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)
+
+
+def ptr(t):
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return FV_F32
+    if dt == torch.bfloat16:
+        return FV_BF16
+    if dt == torch.float64:
+        return FV_F64
+    raise TypeError(f"unsupported dtype {dt}")

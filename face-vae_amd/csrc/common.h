@@ -1,0 +1,98 @@
+// Shared device/host helpers for libfacevae (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/facevae.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define FV_LDS __attribute__((address_space(3)))
+
+// ------------------------------------------------------------------------------------
+// host-side error plumbing (thread-local message, never abort)
+// ------------------------------------------------------------------------------------
+void fv_set_error(const char* fmt, ...);
+int fv_check_launch(const char* what);
+
+#define FV_REQUIRE(cond, ...)                  \
+  do {                                         \
+    if (!(cond)) {                             \
+      fv_set_error(__VA_ARGS__);               \
+      return FV_E_BADARG;                      \
+    }                                          \
+  } while (0)
+
+static inline int fv_ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return ((1 << l) == v) ? l : -1;
+}
+static inline int fv_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// ------------------------------------------------------------------------------------
+// element helpers: T is float (fp32 parity mode) or bf16 (fast mode)
+// ------------------------------------------------------------------------------------
+template <typename T> struct Elt;
+template <> struct Elt<float> {
+  static __device__ __forceinline__ float to_f(float v) { return v; }
+  static __device__ __forceinline__ float from_f(float v) { return v; }
+};
+template <> struct Elt<bf16> {
+  static __device__ __forceinline__ float to_f(bf16 v) { return (float)v; }
+  static __device__ __forceinline__ bf16 from_f(float v) { return (bf16)v; }
+};
+
+// 8 consecutive elements moved as raw bits (16 B for bf16, 32 B for f32)
+template <typename T> struct Chunk8;
+template <> struct Chunk8<bf16> {
+  uint4 raw;
+  __device__ __forceinline__ void load(const bf16* p) { raw = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void store(bf16* p) const { *reinterpret_cast<uint4*>(p) = raw; }
+  __device__ __forceinline__ void zero() { raw = make_uint4(0, 0, 0, 0); }
+  __device__ __forceinline__ float get(int j) const {
+    const uint32_t w = (&raw.x)[j >> 1];
+    const uint32_t b = (j & 1) ? (w & 0xffff0000u) : (w << 16);
+    return __uint_as_float(b);
+  }
+  __device__ __forceinline__ void set8(const float* f) {
+    bf16 t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = (bf16)f[j];
+    raw = *reinterpret_cast<const uint4*>(t);
+  }
+};
+template <> struct Chunk8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = reinterpret_cast<const float4*>(p)[0];
+    b = reinterpret_cast<const float4*>(p)[1];
+  }
+  __device__ __forceinline__ void store(float* p) const {
+    reinterpret_cast<float4*>(p)[0] = a;
+    reinterpret_cast<float4*>(p)[1] = b;
+  }
+  __device__ __forceinline__ void zero() { a = b = make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ __forceinline__ float get(int j) const { return j < 4 ? (&a.x)[j] : (&b.x)[j - 4]; }
+  __device__ __forceinline__ void set8(const float* f) {
+    a = make_float4(f[0], f[1], f[2], f[3]);
+    b = make_float4(f[4], f[5], f[6], f[7]);
+  }
+};
+
+__device__ __forceinline__ float fv_act(float v, float slope) { return v > 0.f ? v : v * slope; }
+
+// wave-level reductions (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

@@ -1,0 +1,977 @@
+// Implicit-GEMM convolution for gfx950 (CDNA4): forward (+ backward-data via transposed
+// weights) and backward-weight.  NHWC activations, MFMA 16x16x32 bf16 (fast mode) or
+// 16x16x4 f32 (exact fp32 parity mode), fp32 accumulation.
+//
+// Reference behaviour replaced: F.conv2d as called by _ConvBlock / nn.Conv2d
+// (modules.py:32-42; models.py:932-934, 1095-1099) in the FaceVAE path, plus the fused
+// pieces around it (nearest x2 upsample modules.py:81, NAC BN-apply+act modules.py:13,
+// residual add modules.py:125, sigmoid models.py:1110, BN statistics modules.py:19).
+//
+// Forward GEMM orientation:  D[co][pixel] = W[co][k] * im2col(x)[k][pixel]
+//   MFMA A operand = weight tile (rows = output channels), B operand = activation tile
+//   (cols = pixels).  The accumulator layout then gives each lane 4 consecutive output
+//   channels of one pixel -> contiguous NHWC stores.  K = (tap, ci), ci fastest, chunks
+//   of 8 k never straddle a tap (cin is a power of two >= 8).
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 32;  // k per main-loop step (one bf16 MFMA K, eight f32 MFMA K=4)
+
+struct ConvArgs {
+  const void* x;
+  const void* w;
+  const float* bias;
+  const float* psc;
+  const float* psh;
+  float slope;
+  const void* res;
+  void* y;
+  float* stats;
+  int N, H, W, Hin, Win, P;
+  int lgCin, Cin;
+  int Cout, ldy;
+  int K, Kpad, nks;
+  int sigmoid, nchw;
+  int ntn;
+};
+
+// 16-B chunk swizzle of a 64-B bf16 LDS row (4 chunks): conflict-free ds_read_b128 for the
+// MFMA fragment read (16 consecutive rows, chunk = lane>>4).  f(row) = [0,2,3,1][(row>>2)&3].
+template <typename T>
+__device__ __forceinline__ int rswz(int row) {
+  if constexpr (sizeof(T) == 2) return (0x1320 >> (((row >> 2) & 3) * 4)) & 3;
+  else return 0;
+}
+
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float* f);
+template <>
+__device__ __forceinline__ void load4<float>(const float* p, float* f) {
+  float4 v = *reinterpret_cast<const float4*>(p);
+  f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+}
+template <>
+__device__ __forceinline__ void load4<bf16>(const bf16* p, float* f) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const float* f);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, const float* f) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+}
+template <>
+__device__ __forceinline__ void store4<bf16>(bf16* p, const float* f) {
+  bf16 t[4] = {(bf16)f[0], (bf16)f[1], (bf16)f[2], (bf16)f[3]};
+  *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(t);
+}
+
+// one MFMA step over a 32-deep k slice for a 16x16 tile
+template <typename T>
+struct Frag;
+template <>
+struct Frag<bf16> {
+  bf16x8 v;
+  __device__ __forceinline__ void lds(const char* p) { v = *reinterpret_cast<const bf16x8*>(p); }
+};
+template <>
+struct Frag<float> {
+  float v[8];
+  __device__ __forceinline__ void lds(const char* p) {
+    float4 a = reinterpret_cast<const float4*>(p)[0];
+    float4 b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+};
+__device__ __forceinline__ f32x4 mma(const Frag<bf16>& a, const Frag<bf16>& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b, f32x4 c) {
+  // k-slot h (= lane>>4) of MFMA j carries k = 8h + j: same map for A and B.
+#pragma unroll
+  for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], c, 0, 0, 0);
+  return c;
+}
+
+template <typename T, int KS, int WN, int WM, int RN, int RM, bool PRO, bool UPS>
+__global__ void __launch_bounds__(64 * WN * WM)
+conv_fwd_kernel(ConvArgs a) {
+  constexpr int NT = 64 * WN * WM;
+  constexpr int BN = WN * RN * 16;   // output channels per block
+  constexpr int BM = WM * RM * 16;   // pixels per block
+  constexpr int PAD = KS / 2;
+  constexpr int ES = sizeof(T);
+  constexpr int ROWB = BK * ES;
+  constexpr int CA = BM * 4 / NT;
+  constexpr int NBCH = BN * 4;
+  constexpr int CB = (NBCH + NT - 1) / NT;
+  static_assert((BM * 4) % NT == 0, "A staging");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * ROWB];
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ wk = reinterpret_cast<const T*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % WN, wm = wave / WN;
+  const int tn = blockIdx.x % a.ntn, tm = blockIdx.x / a.ntn;
+  const int co0 = tn * BN, p0 = tm * BM;
+  const int kc = tid & 3;
+  const int HW = a.H * a.W;
+
+  int rh[CA], rw[CA], rb[CA];
+  bool rv[CA];
+#pragma unroll
+  for (int i = 0; i < CA; ++i) {
+    const int pix = p0 + (tid >> 2) + i * (NT / 4);
+    rv[i] = pix < a.P;
+    const int n = pix / HW;
+    const int rem = pix - n * HW;
+    rh[i] = rem / a.W;
+    rw[i] = rem - rh[i] * a.W;
+    rb[i] = n * a.Hin * a.Win;
+  }
+
+  Chunk8<T> ra[CA], rbw[CB];
+  unsigned okm = 0;
+  int cur_ci = 0;
+
+  auto gload = [&](int ks) {
+    const int k = ks * BK + kc * 8;
+    const bool kin = k < a.K;
+    const int tap = k >> a.lgCin;
+    const int ci = k & (a.Cin - 1);
+    const int r = tap / KS, s = tap - (tap / KS) * KS;
+    cur_ci = ci;
+    okm = 0;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int hh = rh[i] + r - PAD, ww = rw[i] + s - PAD;
+      bool ok = kin && rv[i];
+      int hs, ws;
+      if constexpr (UPS) {
+        ok = ok && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+        hs = hh >> 1;
+        ws = ww >> 1;
+      } else {
+        ok = ok && hh >= 0 && hh < a.Hin && ww >= 0 && ww < a.Win;
+        hs = hh;
+        ws = ww;
+      }
+      if (ok) {
+        ra[i].load(x + ((long)(rb[i] + hs * a.Win + ws) << a.lgCin) + ci);
+        okm |= 1u << i;
+      } else {
+        ra[i].zero();
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const int q = tid + j * NT;
+      if (q < NBCH) rbw[j].load(wk + (long)(co0 + (q >> 2)) * a.Kpad + ks * BK + kc * 8);
+    }
+  };
+
+  auto lstore = [&](int buf) {
+    char* As = smem + buf * (BM + BN) * ROWB;
+    char* Bs = As + BM * ROWB;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int row = (tid >> 2) + i * (NT / 4);
+      Chunk8<T> c = ra[i];
+      if constexpr (PRO) {
+        if (okm & (1u << i)) {
+          float f[8];
+          const float4 s0 = *reinterpret_cast<const float4*>(a.psc + cur_ci);
+          const float4 s1 = *reinterpret_cast<const float4*>(a.psc + cur_ci + 4);
+          const float4 h0 = *reinterpret_cast<const float4*>(a.psh + cur_ci);
+          const float4 h1 = *reinterpret_cast<const float4*>(a.psh + cur_ci + 4);
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fv_act(c.get(j) * sc[j] + sh[j], a.slope);
+          c.set8(f);
+        }
+      }
+      c.store(reinterpret_cast<T*>(As + row * ROWB + ((kc ^ rswz<T>(row)) * 8 * ES)));
+    }
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const int q = tid + j * NT;
+      if (q < NBCH) {
+        const int row = q >> 2;
+        rbw[j].store(reinterpret_cast<T*>(Bs + row * ROWB + ((kc ^ rswz<T>(row)) * 8 * ES)));
+      }
+    }
+  };
+
+  f32x4 acc[RN][RM];
+#pragma unroll
+  for (int n = 0; n < RN; ++n)
+#pragma unroll
+    for (int m = 0; m < RM; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lh = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * (BM + BN) * ROWB;
+    const char* Bs = As + BM * ROWB;
+    Frag<T> af[RN], bfm[RM];
+#pragma unroll
+    for (int n = 0; n < RN; ++n) {
+      const int row = wn * RN * 16 + n * 16 + lr;
+      af[n].lds(Bs + row * ROWB + ((lh ^ rswz<T>(row)) * 8 * ES));
+    }
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int row = wm * RM * 16 + m * 16 + lr;
+      bfm[m].lds(As + row * ROWB + ((lh ^ rswz<T>(row)) * 8 * ES));
+    }
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[n][m] = mma(af[n], bfm[m], acc[n][m]);
+  };
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < a.nks; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < a.nks) gload(ks + 1);
+    compute(cur);
+    if (ks + 1 < a.nks) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  float bv[RN][4];
+#pragma unroll
+  for (int n = 0; n < RN; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wn * RN * 16 + n * 16 + lh * 4 + i;
+      bv[n][i] = (a.bias && co < a.Cout) ? a.bias[co] : 0.f;
+    }
+  bool pv[RM];
+  int pix_of[RM];
+#pragma unroll
+  for (int m = 0; m < RM; ++m) {
+    pix_of[m] = p0 + wm * RM * 16 + m * 16 + lr;
+    pv[m] = pix_of[m] < a.P;
+  }
+#pragma unroll
+  for (int n = 0; n < RN; ++n) {
+    const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[n][m][i] += bv[n][i];
+      if (a.res && pv[m]) {
+        const T* rp = reinterpret_cast<const T*>(a.res) + (long)pix_of[m] * a.ldy + cb;
+        if (cb + 3 < a.Cout) {
+          float f[4];
+          load4<T>(rp, f);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[n][m][i] += f[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (cb + i < a.Cout) acc[n][m][i] += Elt<T>::to_f(rp[i]);
+        }
+      }
+    }
+  }
+
+  if (a.stats) {
+    // per-block (sum, centred M2) per output channel; rows of this block = valid pixels
+    float* red = reinterpret_cast<float*>(smem);        // [WM][BN]
+    float* meanv = red + WM * BN;                         // [BN]
+    const int cnt = min(BM, a.P - p0);
+    float s[RN][4];
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < RM; ++m) t += pv[m] ? acc[n][m][i] : 0.f;
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        s[n][i] = t;
+      }
+    if (lr == 0) {
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float S = 0.f;
+#pragma unroll
+      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
+      meanv[c] = S / (float)cnt;
+      if (co0 + c < a.Cout) a.stats[(long)(tm * 2) * a.Cout + co0 + c] = S;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float mu = meanv[wn * RN * 16 + n * 16 + lh * 4 + i];
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < RM; ++m) {
+          const float d = acc[n][m][i] - mu;
+          t += pv[m] ? d * d : 0.f;
+        }
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        s[n][i] = t;
+      }
+    __syncthreads();
+    if (lr == 0) {
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float S = 0.f;
+#pragma unroll
+      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
+      if (co0 + c < a.Cout) a.stats[(long)(tm * 2 + 1) * a.Cout + co0 + c] = S;
+    }
+  }
+
+#pragma unroll
+  for (int n = 0; n < RN; ++n) {
+    const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      if (!pv[m]) continue;
+      float f[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[i] = acc[n][m][i];
+        if (a.sigmoid) f[i] = 1.f / (1.f + __expf(-f[i]));
+      }
+      if (a.nchw) {
+        float* yp = reinterpret_cast<float*>(a.y);
+        const int img = pix_of[m] / HW, hw = pix_of[m] - img * HW;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (cb + i < a.Cout) yp[((long)img * a.Cout + cb + i) * HW + hw] = f[i];
+      } else {
+        T* yp = reinterpret_cast<T*>(a.y) + (long)pix_of[m] * a.ldy + cb;
+        if (cb + 3 < a.Cout) {
+          store4<T>(yp, f);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (cb + i < a.Cout) yp[i] = Elt<T>::from_f(f[i]);
+        }
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// backward-weight:  D[k][co] = sum_p im2col(x)[p][k] * dy[p][co], split over pixels
+// MFMA A operand = im2col^T (rows = k), B operand = dy (cols = co); both are k-slot =
+// pixel, i.e. COLUMN reads of the [pixel][channel] LDS images -> ds_read_b64_tr_b16.
+// ----------------------------------------------------------------------------------------
+struct WgArgs {
+  const void* x;
+  const float* psc;
+  const float* psh;
+  float slope;
+  const void* dy;
+  float* slab;
+  float* bslab;
+  int N, H, W, Hin, Win, P;
+  int lgCin, Cin;
+  int K, KW;          // KW = slab row stride (>= Kpad, multiple of the k tile)
+  int Cout, ldd;      // valid output channels, channel stride of dy
+  int CW;             // slab co rows
+  int ntk, ntc, steps_per_split, nsteps;
+};
+
+// 8-B granule swizzle for the transposed-read images (cols >= 64): conflict-free
+// ds_read_b64_tr_b16 over rows {8g+q} (wgrad).
+__device__ __forceinline__ int gswz(int row) { return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 2; }
+
+template <int COLS>
+__device__ __forceinline__ int tr_off(int row, int col) {  // byte offset of (row, col) bf16
+  if constexpr (COLS >= 64) return row * COLS * 2 + (((col >> 2) ^ gswz(row)) << 3) + (col & 3) * 2;
+  else return row * COLS * 2 + col * 2;
+}
+
+template <typename T, int COLS>
+__device__ __forceinline__ void colfrag(const char* base, int cbase, int lane, Frag<T>& f) {
+  const int g = lane >> 4, li = lane & 15;
+  if constexpr (sizeof(T) == 2) {
+    const int q = li >> 2, pp = li & 3;
+    const int c = cbase + 4 * pp;
+    FV_LDS char* lb = (FV_LDS char*)(base);   // generic -> LDS address-space cast
+    s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + tr_off<COLS>(8 * g + q, c)));
+    s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + tr_off<COLS>(8 * g + 4 + q, c)));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    f.v = __builtin_bit_cast(bf16x8, v);
+  } else {
+    const float* fb = reinterpret_cast<const float*>(base);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.v[j] = fb[(8 * g + j) * COLS + cbase + li];
+  }
+}
+
+template <typename T, int KS, int WK, int WC, int RK, int RC, bool PRO, bool UPS>
+__global__ void __launch_bounds__(64 * WK * WC)
+conv_wgrad_kernel(WgArgs a) {
+  constexpr int NT = 64 * WK * WC;
+  constexpr int BKT = WK * RK * 16;  // k columns per block
+  constexpr int BC = WC * RC * 16;   // output channels per block
+  constexpr int PAD = KS / 2;
+  constexpr int ES = sizeof(T);
+  constexpr int PX = 32;             // pixels per step
+  constexpr int ABYTES = PX * BKT * ES, DBYTES = PX * BC * ES;
+  constexpr int KCH = BKT / 8, CCH = BC / 8;     // 8-element chunks per row
+  constexpr int CA = (PX * KCH + NT - 1) / NT;
+  constexpr int CD = (PX * CCH + NT - 1) / NT;
+  static_assert(NT % KCH == 0 && NT % CCH == 0, "chunk map");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (ABYTES + DBYTES)];
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wk = wave % WK, wc = wave / WK;
+  const int per = a.ntk * a.ntc;
+  const int split = blockIdx.x / per;
+  const int rem = blockIdx.x - split * per;
+  const int tc = rem % a.ntc, tk = rem / a.ntc;
+  const int k0 = tk * BKT, c0 = tc * BC;
+  const int s_begin = split * a.steps_per_split;
+  const int s_end = min(a.nsteps, s_begin + a.steps_per_split);
+  const int HW = a.H * a.W;
+
+  // fixed per-thread k chunk (gather) and co chunk (dy)
+  const int kq = tid % KCH;
+  const int kk = k0 + kq * 8;
+  const bool kin = kk < a.K;
+  const int tap = kk >> a.lgCin, ci = kk & (a.Cin - 1);
+  const int rr = tap / KS, ss = tap - (tap / KS) * KS;
+  const int cq = tid % CCH;
+  const int cc = c0 + cq * 8;
+  const bool cin_ok = cc < a.ldd;
+
+  Chunk8<T> ra[CA], rd[CD];
+  unsigned okm = 0;
+
+  auto gload = [&](int st) {
+    const int pbase = st * PX;
+    okm = 0;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int q = tid + i * NT;
+      const int prow = q / KCH;
+      const int pix = pbase + prow;
+      bool ok = kin && (q < PX * KCH) && pix < a.P;
+      int n = pix / HW, r2 = pix - n * HW;
+      int h = r2 / a.W, w = r2 - h * a.W;
+      int hh = h + rr - PAD, ww = w + ss - PAD;
+      int hs, ws;
+      if constexpr (UPS) {
+        ok = ok && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+        hs = hh >> 1;
+        ws = ww >> 1;
+      } else {
+        ok = ok && hh >= 0 && hh < a.Hin && ww >= 0 && ww < a.Win;
+        hs = hh;
+        ws = ww;
+      }
+      if (ok) {
+        ra[i].load(x + ((long)(n * a.Hin * a.Win + hs * a.Win + ws) << a.lgCin) + ci);
+        okm |= 1u << i;
+      } else {
+        ra[i].zero();
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < CD; ++i) {
+      const int q = tid + i * NT;
+      const int pix = pbase + q / CCH;
+      if (cin_ok && q < PX * CCH && pix < a.P) rd[i].load(dy + (long)pix * a.ldd + cc);
+      else rd[i].zero();
+    }
+  };
+
+  auto chunk_off = [&](int row, int col, int cols) -> int {  // byte offset of an 8-elt chunk
+    if constexpr (ES == 2) {
+      if (cols >= 64) return row * cols * 2 + (((col >> 2) ^ gswz(row)) << 3);
+      return row * cols * 2 + col * 2;
+    } else {
+      return (row * cols + col) * 4;
+    }
+  };
+
+  auto lstore = [&](int buf) {
+    char* As = smem + buf * (ABYTES + DBYTES);
+    char* Ds = As + ABYTES;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int q = tid + i * NT;
+      if (q < PX * KCH) {
+        Chunk8<T> c = ra[i];
+        if constexpr (PRO) {
+          if (okm & (1u << i)) {
+            float f[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fv_act(c.get(j) * a.psc[ci + j] + a.psh[ci + j], a.slope);
+            c.set8(f);
+          }
+        }
+        c.store(reinterpret_cast<T*>(As + chunk_off(q / KCH, kq * 8, BKT)));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < CD; ++i) {
+      const int q = tid + i * NT;
+      if (q < PX * CCH) rd[i].store(reinterpret_cast<T*>(Ds + chunk_off(q / CCH, cq * 8, BC)));
+    }
+  };
+
+  f32x4 acc[RK][RC];
+#pragma unroll
+  for (int i = 0; i < RK; ++i)
+#pragma unroll
+    for (int j = 0; j < RC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // bias-gradient partial (only the k-tile-0 blocks): thread -> column tid % BC
+  const bool do_bias = (tk == 0) && a.bslab;
+  constexpr int BROWS = NT / BC > 0 ? NT / BC : 1;
+  float bsum = 0.f;
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * (ABYTES + DBYTES);
+    const char* Ds = As + ABYTES;
+    Frag<T> af[RK], bfr[RC];
+#pragma unroll
+    for (int i = 0; i < RK; ++i) colfrag<T, BKT>(As, wk * RK * 16 + i * 16, lane, af[i]);
+#pragma unroll
+    for (int j = 0; j < RC; ++j) colfrag<T, BC>(Ds, wc * RC * 16 + j * 16, lane, bfr[j]);
+#pragma unroll
+    for (int i = 0; i < RK; ++i)
+#pragma unroll
+      for (int j = 0; j < RC; ++j) acc[i][j] = mma(af[i], bfr[j], acc[i][j]);
+    if (do_bias && tid < BROWS * BC) {
+      const int col = tid % BC, part = tid / BC;
+      for (int r = part; r < PX; r += BROWS) {
+        if constexpr (ES == 2) bsum += (float)*reinterpret_cast<const bf16*>(Ds + tr_off<BC>(r, col));
+        else bsum += reinterpret_cast<const float*>(Ds)[r * BC + col];
+      }
+    }
+  };
+
+  if (s_begin < s_end) {
+    gload(s_begin);
+    lstore(0);
+    __syncthreads();
+    for (int st = s_begin; st < s_end; ++st) {
+      const int cur = (st - s_begin) & 1;
+      if (st + 1 < s_end) gload(st + 1);
+      compute(cur);
+      if (st + 1 < s_end) lstore(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // D[k][co]: lane holds k = kb + 4*(lane>>4) + i for co = cb + (lane & 15)
+  const int lr = lane & 15, lh = lane >> 4;
+  float* slab = a.slab + (long)split * a.CW * a.KW;
+#pragma unroll
+  for (int i = 0; i < RK; ++i) {
+    const int kb = k0 + wk * RK * 16 + i * 16 + lh * 4;
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+      const int co = c0 + wc * RC * 16 + j * 16 + lr;
+      *reinterpret_cast<float4*>(slab + (long)co * a.KW + kb) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(smem);
+    if (tid < BROWS * BC) red[tid] = bsum;
+    __syncthreads();
+    if (tid < BC) {
+      float t = 0.f;
+      for (int p = 0; p < BROWS; ++p) t += red[p * BC + tid];
+      a.bslab[(long)split * a.CW + c0 + tid] = t;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// weight re-layout (+ 1/sigma) and slab reduction
+// ----------------------------------------------------------------------------------------
+template <typename T>
+__global__ void weight_prep_kernel(const float* __restrict__ wp, const float* sigma, T* wk,
+                                   int rows, int Kpad, int cout, int cin_valid, int lgCin, int KS,
+                                   int K, int transposed) {
+  const long total = (long)rows * Kpad;
+  const float inv = sigma ? 1.f / sigma[0] : 1.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(e / Kpad), k = (int)(e - (long)row * Kpad);
+    float v = 0.f;
+    if (k < K) {
+      const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
+      const int r = tap / KS, s = tap - (tap / KS) * KS;
+      if (!transposed) {        // wk[co][(r,s,ci)] = W[co][ci][r][s]
+        if (row < cout && c < cin_valid) v = wp[(((long)row * cin_valid + c) * KS + r) * KS + s];
+      } else {                  // wt[ci][(r',s',co)] = W[co][ci][KS-1-r'][KS-1-s']
+        if (row < cin_valid && c < cout)
+          v = wp[(((long)c * cin_valid + row) * KS + (KS - 1 - r)) * KS + (KS - 1 - s)];
+      }
+    }
+    wk[e] = Elt<T>::from_f(v * inv);
+  }
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
+                                    float* dw, float* db, int nsplit, int CW, int KW, int K,
+                                    int cout, int cin_valid, int lgCin, int KS) {
+  const long total = (long)cout * K;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(e / K), k = (int)(e - (long)co * K);
+    const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
+    if (c >= cin_valid) continue;
+    float g = 0.f;
+    for (int s = 0; s < nsplit; ++s) g += slab[((long)s * CW + co) * KW + k];
+    const int r = tap / KS, sx = tap - (tap / KS) * KS;
+    dw[(((long)co * cin_valid + c) * KS + r) * KS + sx] = g;
+  }
+  if (db && blockIdx.x == 0) {
+    for (int co = threadIdx.x; co < cout; co += blockDim.x) {
+      float g = 0.f;
+      for (int s = 0; s < nsplit; ++s) g += bslab[(long)s * CW + co];
+      db[co] = g;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// host dispatch
+// ----------------------------------------------------------------------------------------
+struct FwdTile { int bn, bm; };
+
+FwdTile fwd_tile(int rows_needed) {
+  if (rows_needed > 64) return {128, 128};
+  if (rows_needed > 32) return {64, 128};
+  if (rows_needed > 16) return {32, 128};
+  return {16, 128};
+}
+
+int pad_pow2_8(int c) {
+  int p = 8;
+  while (p < c) p <<= 1;
+  return p;
+}
+
+template <typename T, int KS, int WN, int WM, int RN, int RM>
+int launch_fwd_t(const ConvArgs& a, int pro, int ups, int nblk, hipStream_t s) {
+  dim3 g(nblk), b(64 * WN * WM);
+  if (pro && ups) {
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_kernel<T, KS, WN, WM, RN, RM, true, true>), g, b, 0, s, a);
+    else return FV_E_UNSUPPORTED;
+  } else if (pro) {
+    if constexpr (KS != 7) hipLaunchKernelGGL((conv_fwd_kernel<T, KS, WN, WM, RN, RM, true, false>), g, b, 0, s, a);
+    else return FV_E_UNSUPPORTED;
+  } else if (ups) {
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_kernel<T, KS, WN, WM, RN, RM, false, true>), g, b, 0, s, a);
+    else return FV_E_UNSUPPORTED;
+  } else {
+    hipLaunchKernelGGL((conv_fwd_kernel<T, KS, WN, WM, RN, RM, false, false>), g, b, 0, s, a);
+  }
+  return FV_OK;
+}
+
+template <typename T, int KS>
+int launch_fwd_ks(const ConvArgs& a, FwdTile t, int pro, int ups, int nblk, hipStream_t s) {
+  if (t.bn == 128) return launch_fwd_t<T, KS, 2, 2, 4, 4>(a, pro, ups, nblk, s);
+  if (t.bn == 64) return launch_fwd_t<T, KS, 2, 2, 2, 4>(a, pro, ups, nblk, s);
+  if (t.bn == 32) return launch_fwd_t<T, KS, 2, 2, 1, 4>(a, pro, ups, nblk, s);
+  return launch_fwd_t<T, KS, 1, 4, 1, 2>(a, pro, ups, nblk, s);
+}
+
+template <typename T>
+int launch_fwd(const ConvArgs& a, int ks, FwdTile t, int pro, int ups, int nblk, hipStream_t s) {
+  switch (ks) {
+    case 1: return launch_fwd_ks<T, 1>(a, t, pro, ups, nblk, s);
+    case 3: return launch_fwd_ks<T, 3>(a, t, pro, ups, nblk, s);
+    case 7: return launch_fwd_ks<T, 7>(a, t, pro, ups, nblk, s);
+  }
+  return FV_E_UNSUPPORTED;
+}
+
+int check_desc(const fv_conv_desc* d) {
+  FV_REQUIRE(d, "null conv descriptor");
+  FV_REQUIRE(d->dtype == FV_F32 || d->dtype == FV_BF16, "conv dtype must be f32 or bf16");
+  FV_REQUIRE(d->ksize == 1 || d->ksize == 3 || d->ksize == 7, "ksize must be 1, 3 or 7");
+  FV_REQUIRE(d->n > 0 && d->h > 0 && d->w > 0, "bad spatial size");
+  FV_REQUIRE(fv_ilog2(d->cin) >= 3, "cin must be a power of two >= 8 (got %d)", d->cin);
+  FV_REQUIRE(d->cin_valid > 0 && d->cin_valid <= d->cin, "bad cin_valid");
+  FV_REQUIRE(d->cout > 0, "bad cout");
+  FV_REQUIRE(!d->upsample || (d->h % 2 == 0 && d->w % 2 == 0), "upsample needs even h, w");
+  FV_REQUIRE(!d->upsample || d->ksize == 3, "upsample only with 3x3");
+  FV_REQUIRE(!d->pro_act || d->ksize != 7, "BN prologue not supported for 7x7");
+  return FV_OK;
+}
+
+int kpad_of(int ks, int cin) { return fv_cdiv((long)ks * ks * cin, BK) * BK; }
+
+struct WgTile { int bkt, bc; };
+WgTile wg_tile(const fv_conv_desc* d) {
+  WgTile t;
+  t.bc = d->cout > 64 ? 128 : (d->cout > 16 ? 64 : 16);
+  t.bkt = 128;
+  return t;
+}
+
+int wg_nsplit(const fv_conv_desc* d) {
+  const WgTile t = wg_tile(d);
+  const int K = d->ksize * d->ksize * d->cin;
+  const int ntk = fv_cdiv(K, t.bkt), ntc = fv_cdiv(d->cout, t.bc);
+  const long P = (long)d->n * d->h * d->w;
+  const int nsteps = fv_cdiv(P, 32);
+  int ns = 2048 / (ntk * ntc);
+  if (ns < 1) ns = 1;
+  if (ns > nsteps) ns = nsteps;
+  const int per = fv_cdiv(nsteps, ns);
+  return fv_cdiv(nsteps, per);
+}
+
+template <typename T, int KS, int WK, int WC, int RK, int RC>
+int launch_wg_t(const WgArgs& a, int pro, int ups, int nblk, hipStream_t s) {
+  dim3 g(nblk), b(64 * WK * WC);
+  if (pro && ups) {
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, WK, WC, RK, RC, true, true>), g, b, 0, s, a);
+    else return FV_E_UNSUPPORTED;
+  } else if (pro) {
+    if constexpr (KS != 7) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, WK, WC, RK, RC, true, false>), g, b, 0, s, a);
+    else return FV_E_UNSUPPORTED;
+  } else if (ups) {
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, WK, WC, RK, RC, false, true>), g, b, 0, s, a);
+    else return FV_E_UNSUPPORTED;
+  } else {
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, WK, WC, RK, RC, false, false>), g, b, 0, s, a);
+  }
+  return FV_OK;
+}
+
+template <typename T, int KS>
+int launch_wg_ks(const WgArgs& a, WgTile t, int pro, int ups, int nblk, hipStream_t s) {
+  if (t.bc == 128) return launch_wg_t<T, KS, 2, 2, 4, 4>(a, pro, ups, nblk, s);
+  if (t.bc == 64) return launch_wg_t<T, KS, 2, 2, 4, 2>(a, pro, ups, nblk, s);
+  return launch_wg_t<T, KS, 4, 1, 2, 1>(a, pro, ups, nblk, s);
+}
+
+template <typename T>
+int launch_wg(const WgArgs& a, int ks, WgTile t, int pro, int ups, int nblk, hipStream_t s) {
+  switch (ks) {
+    case 1: return launch_wg_ks<T, 1>(a, t, pro, ups, nblk, s);
+    case 3: return launch_wg_ks<T, 3>(a, t, pro, ups, nblk, s);
+    case 7: return launch_wg_ks<T, 7>(a, t, pro, ups, nblk, s);
+  }
+  return FV_E_UNSUPPORTED;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t fv_conv_wk_elems(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  const FwdTile t = fwd_tile(d->cout);
+  return (size_t)fv_cdiv(d->cout, t.bn) * t.bn * kpad_of(d->ksize, d->cin);
+}
+
+size_t fv_conv_wt_elems(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  const int cin_t = pad_pow2_8(d->cout);
+  const FwdTile t = fwd_tile(d->cin);
+  return (size_t)fv_cdiv(d->cin, t.bn) * t.bn * kpad_of(d->ksize, cin_t);
+}
+
+int fv_conv2d_stats_block_pixels(const fv_conv_desc* d) { return fwd_tile(d->cout).bm; }
+
+int fv_conv2d_stats_blocks(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  return fv_cdiv((long)d->n * d->h * d->w, fwd_tile(d->cout).bm);
+}
+
+int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma, void* wk,
+                        void* wt, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const int ks = d->ksize;
+  if (wk) {
+    const FwdTile t = fwd_tile(d->cout);
+    const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_of(ks, d->cin);
+    const long tot = (long)rows * Kp;
+    const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
+    if (d->dtype == FV_BF16)
+      hipLaunchKernelGGL(weight_prep_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wk,
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0);
+    else
+      hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(nb), dim3(256), 0, s, w_param, sigma, (float*)wk,
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0);
+    if ((st = fv_check_launch("weight_prep"))) return st;
+  }
+  if (wt) {
+    const int cin_t = pad_pow2_8(d->cout);
+    const FwdTile t = fwd_tile(d->cin);
+    const int rows = fv_cdiv(d->cin, t.bn) * t.bn, Kp = kpad_of(ks, cin_t);
+    const long tot = (long)rows * Kp;
+    const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
+    if (d->dtype == FV_BF16)
+      hipLaunchKernelGGL(weight_prep_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wt,
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(cin_t), ks, ks * ks * cin_t, 1);
+    else
+      hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(nb), dim3(256), 0, s, w_param, sigma, (float*)wt,
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(cin_t), ks, ks * ks * cin_t, 1);
+    if ((st = fv_check_launch("weight_prep_t"))) return st;
+  }
+  return FV_OK;
+}
+
+static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
+                    const float* psc, const float* psh, const void* res, void* y, float* stats,
+                    hipStream_t s) {
+  ConvArgs a{};
+  const FwdTile t = fwd_tile(d->cout);
+  a.x = x; a.w = wk; a.bias = bias; a.psc = psc; a.psh = psh; a.slope = d->pro_slope;
+  a.res = res; a.y = y; a.stats = stats;
+  a.N = d->n; a.H = d->h; a.W = d->w;
+  a.Hin = d->upsample ? d->h / 2 : d->h;
+  a.Win = d->upsample ? d->w / 2 : d->w;
+  a.P = d->n * d->h * d->w;
+  a.Cin = d->cin; a.lgCin = fv_ilog2(d->cin);
+  a.Cout = d->cout; a.ldy = d->ldy;
+  a.K = d->ksize * d->ksize * d->cin; a.Kpad = kpad_of(d->ksize, d->cin); a.nks = a.Kpad / BK;
+  a.sigmoid = d->epi_sigmoid; a.nchw = d->out_nchw_f32;
+  a.ntn = fv_cdiv(d->cout, t.bn);
+  const int nblk = a.ntn * fv_cdiv(a.P, t.bm);
+  int st = d->dtype == FV_BF16 ? launch_fwd<bf16>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s)
+                               : launch_fwd<float>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s);
+  if (st) {
+    fv_set_error("conv variant unsupported (k=%d pro=%d ups=%d)", d->ksize, d->pro_act, d->upsample);
+    return st;
+  }
+  return fv_check_launch("conv2d_fwd");
+}
+
+int fv_conv2d_fwd(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
+                  const float* pro_scale, const float* pro_shift, const void* res, void* y,
+                  float* stats, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(x && wk && y, "null pointer");
+  FV_REQUIRE(!d->pro_act || (pro_scale && pro_shift), "prologue needs scale/shift");
+  FV_REQUIRE(d->out_nchw_f32 || d->ldy >= d->cout, "ldy < cout");
+  FV_REQUIRE(!res || d->ldy % 4 == 0, "residual needs ldy % 4 == 0");
+  FV_REQUIRE(d->out_nchw_f32 || d->cout % 4 == 0 || d->ldy >= d->cout, "bad ldy");
+  return conv_run(d, x, wk, bias, pro_scale, pro_shift, res, y, stats, (hipStream_t)stream);
+}
+
+int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,
+                       void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  fv_conv_desc t{};
+  t.dtype = d->dtype;
+  t.n = d->n; t.h = d->h; t.w = d->w;
+  t.cin = pad_pow2_8(d->cout);
+  t.cin_valid = d->cout;
+  FV_REQUIRE(ldy_dy == t.cin, "bwd_data: dy channel stride must be %d (got %d)", t.cin, ldy_dy);
+  t.cout = d->cin;   // every (padded) input channel; padded ones come out 0
+  t.ldy = d->cin;
+  t.ksize = d->ksize;
+  return conv_run(&t, dy, wt, nullptr, nullptr, nullptr, nullptr, dx, nullptr, (hipStream_t)stream);
+}
+
+int fv_conv2d_wgrad_nsplit(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  return wg_nsplit(d);
+}
+
+size_t fv_conv2d_wgrad_slab_elems(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  const WgTile t = wg_tile(d);
+  const int K = d->ksize * d->ksize * d->cin;
+  const size_t CW = (size_t)fv_cdiv(d->cout, t.bc) * t.bc;
+  const size_t KW = (size_t)fv_cdiv(K, t.bkt) * t.bkt;
+  return (size_t)wg_nsplit(d) * CW * KW;
+}
+
+int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_scale,
+                         const float* pro_shift, const void* dy, int ldy_dy, float* slab,
+                         float* bias_slab, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(x && dy && slab, "null pointer");
+  FV_REQUIRE(ldy_dy % 8 == 0 && ldy_dy >= d->cout, "wgrad: dy channel stride must be a multiple of 8 >= cout");
+  FV_REQUIRE(!d->pro_act || (pro_scale && pro_shift), "prologue needs scale/shift");
+  const WgTile t = wg_tile(d);
+  WgArgs a{};
+  a.x = x; a.psc = pro_scale; a.psh = pro_shift; a.slope = d->pro_slope;
+  a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+  a.N = d->n; a.H = d->h; a.W = d->w;
+  a.Hin = d->upsample ? d->h / 2 : d->h;
+  a.Win = d->upsample ? d->w / 2 : d->w;
+  a.P = d->n * d->h * d->w;
+  a.Cin = d->cin; a.lgCin = fv_ilog2(d->cin);
+  a.K = d->ksize * d->ksize * d->cin;
+  a.ntk = fv_cdiv(a.K, t.bkt); a.KW = a.ntk * t.bkt;
+  a.Cout = d->cout; a.ldd = ldy_dy;
+  a.ntc = fv_cdiv(d->cout, t.bc); a.CW = a.ntc * t.bc;
+  a.nsteps = fv_cdiv(a.P, 32);
+  const int ns = wg_nsplit(d);
+  a.steps_per_split = fv_cdiv(a.nsteps, ns);
+  const int nblk = a.ntk * a.ntc * ns;
+  st = d->dtype == FV_BF16 ? launch_wg<bf16>(a, d->ksize, t, d->pro_act, d->upsample, nblk, (hipStream_t)stream)
+                           : launch_wg<float>(a, d->ksize, t, d->pro_act, d->upsample, nblk, (hipStream_t)stream);
+  if (st) {
+    fv_set_error("wgrad variant unsupported (k=%d pro=%d ups=%d)", d->ksize, d->pro_act, d->upsample);
+    return st;
+  }
+  return fv_check_launch("conv2d_bwd_weight");
+}
+
+int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab,
+                           float* dw_param, float* db, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(slab && dw_param, "null pointer");
+  FV_REQUIRE(!db || bias_slab, "db needs the bias slab");
+  const WgTile t = wg_tile(d);
+  const int K = d->ksize * d->ksize * d->cin;
+  const int KW = fv_cdiv(K, t.bkt) * t.bkt, CW = fv_cdiv(d->cout, t.bc) * t.bc;
+  const long tot = (long)d->cout * K;
+  const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 8192);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, slab, bias_slab,
+                     dw_param, db, wg_nsplit(d), CW, KW, K, d->cout, d->cin_valid, fv_ilog2(d->cin),
+                     d->ksize);
+  return fv_check_launch("wgrad_reduce");
+}
+
+}  // extern "C"

@@ -1,0 +1,563 @@
+// HBM-streaming kernels around the convs: layout changes, upsample backward, latent
+// reparameterisation, KL / MSE / L1 reductions, spectral norm and multi-tensor Adam.
+//
+//   reparam : flatten_vae_nl convention (models.py:559-561), eps supplied by the caller
+//   KL      : KLDivergenceLoss (losses.py:392)
+//   MSE     : ReconLoss = nn.MSELoss (losses.py:396-403)
+//   L1      : PerceptualLoss pixel term (losses.py:128,135)
+//   SN      : torch/nn/utils/spectral_norm.py:62-113 (one power iteration per training fwd)
+//   Adam    : torch.optim.Adam (logger.py:60)
+#include <math.h>
+
+#include "common.h"
+
+namespace {
+
+constexpr int NTH = 256;
+constexpr int RED_BLOCKS = 1024;   // first-stage blocks of the scalar loss reductions
+
+int grid_for(long work, int cap = 8192) {
+  long g = (work + NTH - 1) / NTH;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, long i) { return Elt<T>::to_f(p[i]); }
+
+// -------------------------------------------------------------------------- layout
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int N, int C, int HW, int ldc, T* out) {
+  const int cg_n = (ldc + 7) / 8;
+  const long total = (long)N * cg_n * HW;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int hw = (int)(e % HW);
+    const long r = e / HW;
+    const int cg = (int)(r % cg_n), n = (int)(r / cg_n);
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      f[j] = c < C ? x[((long)n * C + c) * HW + hw] : 0.f;
+    }
+    T* o = out + ((long)n * HW + hw) * ldc + cg * 8;
+    if (cg * 8 + 8 <= ldc) {
+      Chunk8<T> ch;
+      ch.set8(f);
+      ch.store(o);
+    } else {
+      for (int j = 0; j < 8 && cg * 8 + j < ldc; ++j) o[j] = Elt<T>::from_f(f[j]);
+    }
+  }
+}
+
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(const T* __restrict__ x, int N, int C, int HW, int ldc, float* out) {
+  const int cg_n = (C + 7) / 8;
+  const long total = (long)N * cg_n * HW;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int hw = (int)(e % HW);
+    const long r = e / HW;
+    const int cg = (int)(r % cg_n), n = (int)(r / cg_n);
+    const T* ip = x + ((long)n * HW + hw) * ldc + cg * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      if (c < C) out[((long)n * C + c) * HW + hw] = Elt<T>::to_f(ip[j]);
+    }
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = Elt<TO>::from_f(Elt<TI>::to_f(x[i]));
+}
+
+template <typename T>
+__global__ void upsample_bwd_kernel(const T* __restrict__ g, int N, int h, int w, int C, T* out) {
+  const int cpc = C / 8;
+  const long total = (long)N * h * w * cpc;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(e % cpc);
+    const long p = e / cpc;
+    const int n = (int)(p / ((long)h * w));
+    const int rem = (int)(p - (long)n * h * w);
+    const int i = rem / w, j = rem - i * w;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        Chunk8<T> c;
+        c.load(g + ((long)(n * 2 * h + 2 * i + a) * (2 * w) + 2 * j + b) * C + cg * 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += c.get(k);
+      }
+    Chunk8<T> o;
+    o.set8(acc);
+    o.store(out + p * C + cg * 8);
+  }
+}
+
+template <typename T>
+__global__ void sigmoid_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y, int N, int C,
+                                   int HW, int ldc, T* dpre) {
+  const long total = (long)N * HW;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(e / HW), hw = (int)(e - (long)n * HW);
+    T* o = dpre + e * ldc;
+    for (int c = 0; c < ldc; ++c) {
+      float v = 0.f;
+      if (c < C) {
+        const long i = ((long)n * C + c) * HW + hw;
+        const float yy = y[i];
+        v = dy[i] * yy * (1.f - yy);
+      }
+      o[c] = Elt<T>::from_f(v);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- latent / losses
+// thread per (n, 8-channel group, hw) with hw fastest: eps (NCHW) reads coalesce
+template <typename T>
+__global__ void reparam_fwd_kernel(const T* __restrict__ h, const float* __restrict__ eps, int N, int L,
+                                   int HW, T* mu, T* ls, T* z) {
+  const int cpc = L / 8;
+  const long total = (long)N * cpc * HW;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int hw = (int)(e % HW);
+    const long r = e / HW;
+    const int cg = (int)(r % cpc), n = (int)(r / cpc);
+    const long p = (long)n * HW + hw;
+    Chunk8<T> m, s;
+    m.load(h + p * 2 * L + cg * 8);
+    s.load(h + p * 2 * L + L + cg * 8);
+    float fz[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      fz[j] = m.get(j) + __expf(s.get(j)) * eps[((long)n * L + cg * 8 + j) * HW + hw];
+    m.store(mu + p * L + cg * 8);
+    s.store(ls + p * L + cg * 8);
+    Chunk8<T> o;
+    o.set8(fz);
+    o.store(z + p * L + cg * 8);
+  }
+}
+
+template <typename T>
+__global__ void reparam_bwd_kernel(const T* __restrict__ h, const float* __restrict__ eps, int N, int L,
+                                   int HW, const T* dz, const T* dmu, const T* dls, T* dh) {
+  const int cpc = L / 8;
+  const long total = (long)N * cpc * HW;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int hw = (int)(e % HW);
+    const long r = e / HW;
+    const int cg = (int)(r % cpc), n = (int)(r / cpc);
+    const long p = (long)n * HW + hw;
+    Chunk8<T> s, gz, gm, gs;
+    s.load(h + p * 2 * L + L + cg * 8);
+    if (dz) gz.load(dz + p * L + cg * 8); else gz.zero();
+    if (dmu) gm.load(dmu + p * L + cg * 8); else gm.zero();
+    if (dls) gs.load(dls + p * L + cg * 8); else gs.zero();
+    float om[8], os[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float ep = eps[((long)n * L + cg * 8 + j) * HW + hw];
+      om[j] = gz.get(j) + gm.get(j);
+      os[j] = gz.get(j) * __expf(s.get(j)) * ep + gs.get(j);
+    }
+    Chunk8<T> a, b;
+    a.set8(om);
+    b.set8(os);
+    a.store(dh + p * 2 * L + cg * 8);
+    b.store(dh + p * 2 * L + L + cg * 8);
+  }
+}
+
+// generic two-stage scalar mean: kind 0 = KL(mu, logstd), 1 = (a-b)^2, 2 = |a-b|
+template <int KIND, typename T>
+__global__ void loss_partial_kernel(const T* __restrict__ a, const T* __restrict__ b, long n, double* part) {
+  double acc = 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float x = ldf(a, i), y = ldf(b, i);
+    float v;
+    if constexpr (KIND == 0) v = -0.5f - y + 0.5f * x * x + 0.5f * __expf(2.f * y);
+    else if constexpr (KIND == 1) v = (x - y) * (x - y);
+    else v = fabsf(x - y);
+    acc += v;
+  }
+  acc = wave_sum_d(acc);
+  __shared__ double sh[NTH / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0;
+    for (int i = 0; i < NTH / 64; ++i) t += sh[i];
+    part[blockIdx.x] = t;
+  }
+}
+
+__global__ void loss_final_kernel(const double* part, int nparts, double count, float* out) {
+  double acc = 0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  acc = wave_sum_d(acc);
+  __shared__ double sh[NTH / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0;
+    for (int i = 0; i < NTH / 64; ++i) t += sh[i];
+    out[0] = (float)(t / count);
+  }
+}
+
+template <typename T>
+__global__ void kl_bwd_kernel(const T* __restrict__ mu, const T* __restrict__ ls, long n, const float* gout,
+                              T* dmu, T* dls) {
+  const float g = gout[0] / (float)n;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float m = ldf(mu, i), s = ldf(ls, i);
+    if (dmu) dmu[i] = Elt<T>::from_f(g * m);
+    if (dls) dls[i] = Elt<T>::from_f(g * (__expf(2.f * s) - 1.f));
+  }
+}
+
+template <int KIND>
+__global__ void pair_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b, long n,
+                                const float* gout, float* da, float* db) {
+  const float g = gout[0] / (float)n;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float d = a[i] - b[i];
+    float v;
+    if constexpr (KIND == 1) v = 2.f * g * d;
+    else v = d > 0.f ? g : (d < 0.f ? -g : 0.f);
+    if (da) da[i] = v;
+    if (db) db[i] = -v;
+  }
+}
+
+// --------------------------------------------------------------------- spectral norm
+// t = W^T u (cols), per-block partial of |t|^2
+__global__ void sn_wtu_kernel(const float* __restrict__ w, int rows, int cols, const float* __restrict__ u,
+                              float* t, float* part) {
+  const int j = blockIdx.x * NTH + threadIdx.x;
+  float acc = 0.f;
+  if (j < cols) {
+    for (int i = 0; i < rows; ++i) acc += w[(long)i * cols + j] * u[i];
+    t[j] = acc;
+  }
+  float sq = wave_sum(acc * acc);
+  __shared__ float sh[NTH / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// s = W v  (one wave per row), v = t / max(|t|, eps) when normalize (written out too)
+__global__ void sn_wv_kernel(const float* __restrict__ w, int rows, int cols, const float* t,
+                             const float* part, int nparts, int normalize, float* v, float* s) {
+  float inv = 1.f;
+  if (normalize) {
+    float n2 = 0.f;
+    for (int i = 0; i < nparts; ++i) n2 += part[i];
+    inv = 1.f / fmaxf(sqrtf(n2), 1e-12f);
+    for (int j = blockIdx.x * NTH + threadIdx.x; j < cols; j += gridDim.x * NTH) v[j] = t[j] * inv;
+  }
+  const float* vv = normalize ? t : v;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (NTH / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float acc = 0.f;
+  for (int j = lane; j < cols; j += 64) acc += w[(long)row * cols + j] * vv[j];
+  acc = wave_sum(acc) * inv;
+  if (lane == 0) s[row] = acc;
+}
+
+// u = s / max(|s|, eps) (power iteration) ; sigma = u . s
+__global__ void sn_fin_kernel(const float* s, int rows, int update_u, float* u, float* sigma) {
+  __shared__ float sh[NTH / 64];
+  __shared__ float bc;
+  float n2 = 0.f;
+  for (int i = threadIdx.x; i < rows; i += NTH) n2 += s[i] * s[i];
+  n2 = wave_sum(n2);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = n2;
+  __syncthreads();
+  if (threadIdx.x == 0) bc = 1.f / fmaxf(sqrtf(sh[0] + sh[1] + sh[2] + sh[3]), 1e-12f);
+  __syncthreads();
+  const float inv = bc;
+  float d = 0.f;
+  for (int i = threadIdx.x; i < rows; i += NTH) {
+    float uu;
+    if (update_u) {
+      uu = s[i] * inv;
+      u[i] = uu;
+    } else {
+      uu = u[i];
+    }
+    d += uu * s[i];
+  }
+  __syncthreads();
+  d = wave_sum(d);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) sigma[0] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void dot_partial_kernel(const float* __restrict__ a, const float* __restrict__ b, long n, float* part) {
+  float acc = 0.f;
+  for (long i = blockIdx.x * (long)NTH + threadIdx.x; i < n; i += (long)gridDim.x * NTH) acc += a[i] * b[i];
+  acc = wave_sum(acc);
+  __shared__ float sh[NTH / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void sn_bwd_apply_kernel(const float* __restrict__ g, int rows, int cols, const float* u,
+                                    const float* v, const float* sigma, const float* part, int nparts,
+                                    float* out) {
+  __shared__ float dot_s;
+  if (threadIdx.x == 0) {
+    float d = 0.f;
+    for (int i = 0; i < nparts; ++i) d += part[i];
+    dot_s = d;
+  }
+  __syncthreads();
+  const float sg = sigma[0];
+  const float c1 = 1.f / sg, c2 = dot_s / (sg * sg);
+  const long n = (long)rows * cols;
+  for (long e = blockIdx.x * (long)NTH + threadIdx.x; e < n; e += (long)gridDim.x * NTH) {
+    const int i = (int)(e / cols), j = (int)(e - (long)i * cols);
+    out[e] = g[e] * c1 - c2 * u[i] * v[j];
+  }
+}
+
+// ------------------------------------------------------------------------------ Adam
+__global__ void adam_kernel(const fv_adam_tensor* __restrict__ ts, const int* __restrict__ blocks, float lr,
+                            float b1, float b2, float eps, float step_size, float bc2_sqrt) {
+  const int t = blocks[2 * blockIdx.x], ch = blocks[2 * blockIdx.x + 1];
+  const fv_adam_tensor d = ts[t];
+  const long base = (long)ch * FV_ADAM_CHUNK;
+  const long end = min(d.numel, base + FV_ADAM_CHUNK);
+  for (long i = base + threadIdx.x; i < end; i += NTH) {
+    const float g = d.grad[i];
+    float m = d.exp_avg[i], v = d.exp_avg_sq[i];
+    m = m + (1.f - b1) * (g - m);
+    v = v * b2 + (1.f - b2) * g * g;
+    d.exp_avg[i] = m;
+    d.exp_avg_sq[i] = v;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    d.param[i] = d.param[i] - step_size * (m / denom);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int fv_nchw_to_nhwc(int dtype_out, const float* x, int n, int c, int hw, int ldc, void* out, void* stream) {
+  FV_REQUIRE(x && out && ldc >= c, "bad args");
+  const long work = (long)n * ((ldc + 7) / 8) * hw;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_out == FV_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, x, n, c, hw, ldc, (bf16*)out);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, x, n, c, hw, ldc, (float*)out);
+  return fv_check_launch("nchw_to_nhwc");
+}
+
+int fv_nhwc_to_nchw(int dtype_in, const void* x, int n, int c, int hw, int ldc, float* out, void* stream) {
+  FV_REQUIRE(x && out && ldc >= c, "bad args");
+  const long work = (long)n * ((c + 7) / 8) * hw;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype_in == FV_BF16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)x, n, c, hw, ldc, out);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)x, n, c, hw, ldc, out);
+  return fv_check_launch("nhwc_to_nchw");
+}
+
+int fv_cast(int dtype_in, const void* x, int dtype_out, void* y, long count, void* stream) {
+  FV_REQUIRE(x && y, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int g = grid_for(count);
+  if (dtype_in == FV_F32 && dtype_out == FV_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(g), dim3(NTH), 0, s, (const float*)x, (bf16*)y, count);
+  else if (dtype_in == FV_BF16 && dtype_out == FV_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(g), dim3(NTH), 0, s, (const bf16*)x, (float*)y, count);
+  else if (dtype_in == FV_F32 && dtype_out == FV_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(NTH), 0, s, (const float*)x, (float*)y, count);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(g), dim3(NTH), 0, s, (const bf16*)x, (bf16*)y, count);
+  return fv_check_launch("cast");
+}
+
+int fv_upsample2x_bwd(int dtype, const void* g, int n, int h_src, int w_src, int c, void* out, void* stream) {
+  FV_REQUIRE(g && out && c % 8 == 0, "upsample bwd: channels must be a multiple of 8");
+  const long work = (long)n * h_src * w_src * (c / 8);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(upsample_bwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)g, n, h_src,
+                       w_src, c, (bf16*)out);
+  else
+    hipLaunchKernelGGL(upsample_bwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)g, n, h_src,
+                       w_src, c, (float*)out);
+  return fv_check_launch("upsample2x_bwd");
+}
+
+int fv_sigmoid_bwd_to_nhwc(int dtype_out, const float* dy, const float* y, int n, int c, int hw, int ldc,
+                           void* dpre, void* stream) {
+  FV_REQUIRE(dy && y && dpre && ldc >= c, "bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const long work = (long)n * hw;
+  if (dtype_out == FV_BF16)
+    hipLaunchKernelGGL(sigmoid_bwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, dy, y, n, c, hw, ldc,
+                       (bf16*)dpre);
+  else
+    hipLaunchKernelGGL(sigmoid_bwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, dy, y, n, c, hw, ldc,
+                       (float*)dpre);
+  return fv_check_launch("sigmoid_bwd");
+}
+
+size_t fv_loss_ws_bytes(void) { return RED_BLOCKS * sizeof(double); }
+
+int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu, void* logstd,
+                   void* z, void* stream) {
+  FV_REQUIRE(h && eps && mu && logstd && z && L % 8 == 0, "reparam: bad args (L %% 8 == 0)");
+  const long work = (long)n * (L / 8) * hw;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(reparam_fwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)h, eps, n, L, hw,
+                       (bf16*)mu, (bf16*)logstd, (bf16*)z);
+  else
+    hipLaunchKernelGGL(reparam_fwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)h, eps, n, L,
+                       hw, (float*)mu, (float*)logstd, (float*)z);
+  return fv_check_launch("reparam_fwd");
+}
+
+int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw, const void* dz,
+                   const void* dmu, const void* dlogstd, void* dh, void* stream) {
+  FV_REQUIRE(h && eps && dh && L % 8 == 0, "reparam bwd: bad args");
+  const long work = (long)n * (L / 8) * hw;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(reparam_bwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)h, eps, n, L, hw,
+                       (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, (bf16*)dh);
+  else
+    hipLaunchKernelGGL(reparam_bwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)h, eps, n, L,
+                       hw, (const float*)dz, (const float*)dmu, (const float*)dlogstd, (float*)dh);
+  return fv_check_launch("reparam_bwd");
+}
+
+static int reduce_scalar(int kind, int dtype, const void* a, const void* b, long count, float* loss, void* ws,
+                         hipStream_t s) {
+  FV_REQUIRE(a && b && loss && ws && count > 0, "loss: bad args");
+  const int g = grid_for(count, RED_BLOCKS);
+  double* part = (double*)ws;
+  if (kind == 0) {
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL((loss_partial_kernel<0, bf16>), dim3(g), dim3(NTH), 0, s, (const bf16*)a, (const bf16*)b, count, part);
+    else
+      hipLaunchKernelGGL((loss_partial_kernel<0, float>), dim3(g), dim3(NTH), 0, s, (const float*)a, (const float*)b, count, part);
+  } else if (kind == 1) {
+    hipLaunchKernelGGL((loss_partial_kernel<1, float>), dim3(g), dim3(NTH), 0, s, (const float*)a, (const float*)b, count, part);
+  } else {
+    hipLaunchKernelGGL((loss_partial_kernel<2, float>), dim3(g), dim3(NTH), 0, s, (const float*)a, (const float*)b, count, part);
+  }
+  int st = fv_check_launch("loss_partial");
+  if (st) return st;
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(NTH), 0, s, part, g, (double)count, loss);
+  return fv_check_launch("loss_final");
+}
+
+int fv_kl_fwd(int dtype, const void* mu, const void* logstd, long count, float* loss, void* ws, void* stream) {
+  return reduce_scalar(0, dtype, mu, logstd, count, loss, ws, (hipStream_t)stream);
+}
+
+int fv_kl_bwd(int dtype, const void* mu, const void* logstd, long count, const float* gout, void* dmu,
+              void* dlogstd, void* stream) {
+  FV_REQUIRE(mu && logstd && gout, "kl bwd: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(kl_bwd_kernel<bf16>, dim3(grid_for(count)), dim3(NTH), 0, s, (const bf16*)mu, (const bf16*)logstd,
+                       count, gout, (bf16*)dmu, (bf16*)dlogstd);
+  else
+    hipLaunchKernelGGL(kl_bwd_kernel<float>, dim3(grid_for(count)), dim3(NTH), 0, s, (const float*)mu,
+                       (const float*)logstd, count, gout, (float*)dmu, (float*)dlogstd);
+  return fv_check_launch("kl_bwd");
+}
+
+int fv_mse_fwd(const float* a, const float* b, long count, float* loss, void* ws, void* stream) {
+  return reduce_scalar(1, FV_F32, a, b, count, loss, ws, (hipStream_t)stream);
+}
+int fv_l1_fwd(const float* a, const float* b, long count, float* loss, void* ws, void* stream) {
+  return reduce_scalar(2, FV_F32, a, b, count, loss, ws, (hipStream_t)stream);
+}
+int fv_mse_bwd(const float* a, const float* b, long count, const float* gout, float* da, float* db, void* stream) {
+  FV_REQUIRE(a && b && gout, "mse bwd: bad args");
+  hipLaunchKernelGGL(pair_bwd_kernel<1>, dim3(grid_for(count)), dim3(NTH), 0, (hipStream_t)stream, a, b, count, gout,
+                     da, db);
+  return fv_check_launch("mse_bwd");
+}
+int fv_l1_bwd(const float* a, const float* b, long count, const float* gout, float* da, float* db, void* stream) {
+  FV_REQUIRE(a && b && gout, "l1 bwd: bad args");
+  hipLaunchKernelGGL(pair_bwd_kernel<2>, dim3(grid_for(count)), dim3(NTH), 0, (hipStream_t)stream, a, b, count, gout,
+                     da, db);
+  return fv_check_launch("l1_bwd");
+}
+
+size_t fv_spectral_norm_ws_bytes(int rows, int cols) {
+  return ((size_t)cols + rows + 2 * NTH + 64) * sizeof(float);
+}
+
+int fv_spectral_norm_fwd(const float* w, int rows, int cols, float* u, float* v, float* sigma, int power_iter,
+                         void* ws, void* stream) {
+  FV_REQUIRE(w && u && v && sigma && ws && rows > 0 && cols > 0, "spectral norm: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  float* t = (float*)ws;
+  float* sv = t + cols;
+  float* part = sv + rows;
+  const int nparts = fv_cdiv(cols, NTH);
+  FV_REQUIRE(nparts <= 2 * NTH, "spectral norm: too many columns");
+  if (power_iter) {
+    hipLaunchKernelGGL(sn_wtu_kernel, dim3(nparts), dim3(NTH), 0, s, w, rows, cols, u, t, part);
+    int st = fv_check_launch("sn_wtu");
+    if (st) return st;
+  }
+  hipLaunchKernelGGL(sn_wv_kernel, dim3(fv_cdiv(rows, NTH / 64)), dim3(NTH), 0, s, w, rows, cols, t, part, nparts,
+                     power_iter, v, sv);
+  int st = fv_check_launch("sn_wv");
+  if (st) return st;
+  hipLaunchKernelGGL(sn_fin_kernel, dim3(1), dim3(NTH), 0, s, sv, rows, power_iter, u, sigma);
+  return fv_check_launch("sn_fin");
+}
+
+int fv_spectral_norm_bwd(const float* w, const float* g_sn, int rows, int cols, const float* u, const float* v,
+                         const float* sigma, float* g_orig, void* ws, void* stream) {
+  FV_REQUIRE(w && g_sn && u && v && sigma && g_orig && ws, "spectral norm bwd: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)ws;
+  const long n = (long)rows * cols;
+  const int nb = (int)std::min<long>(fv_cdiv(n, NTH), 256);
+  hipLaunchKernelGGL(dot_partial_kernel, dim3(nb), dim3(NTH), 0, s, g_sn, w, n, part);
+  int st = fv_check_launch("sn_dot");
+  if (st) return st;
+  hipLaunchKernelGGL(sn_bwd_apply_kernel, dim3(grid_for(n, 2048)), dim3(NTH), 0, s, g_sn, rows, cols, u, v, sigma,
+                     part, nb, g_orig);
+  return fv_check_launch("sn_bwd");
+}
+
+int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, float lr, float beta1, float beta2,
+                 float eps, long step, void* stream) {
+  FV_REQUIRE(tensors && blocks && nblocks > 0 && step > 0, "adam: bad args");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel, dim3(nblocks), dim3(NTH), 0, (hipStream_t)stream, tensors, blocks, lr, beta1, beta2,
+                     eps, (float)(lr / bc1), (float)sqrt(bc2));
+  return fv_check_launch("adam");
+}
+
+}  // extern "C"

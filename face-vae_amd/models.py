@@ -1,0 +1,88 @@
+"""Encoder (AFE 2-D trunk), decoder (Generator 2-D trunk) and the FaceVAE composition
+ with the reference constructor signatures and state-dict keys
+(models.py:922-945 AFE, 1085-1111 Generator of Luh1124/face-vae)."""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import config as _config
+from . import ops
+from .modules import Conv2d, ConvBlock2D, DownBlock2D, ResBlock2D, UpBlock2D, _Block
+
+
+class AFE(_Block):
+    """Appearance-feature extractor (models.py:922-945).  The 2-D trunk (in_conv 7x7 CNA,
+    DownBlock2D chain, 1x1 mid_conv) is the FaceVAE encoder.  Its 3-D ResBlock3D trunk is
+    SURVEY.md §8(f) "next #1" and not built yet: n_res must be 0."""
+
+    def __init__(self, use_weight_norm=False, down_seq=(64, 128, 256), n_res=6, C=32, D=16):
+        super().__init__()
+        if n_res != 0:
+            raise NotImplementedError("AFE ResBlock3D trunk (SURVEY.md §8(f) next #1): use n_res=0")
+        down_seq = list(down_seq)
+        self.in_conv = ConvBlock2D("CNA", 3, down_seq[0], 7, 1, 3, use_weight_norm)
+        self.down = nn.Sequential(*[DownBlock2D(down_seq[i], down_seq[i + 1], use_weight_norm)
+                                    for i in range(len(down_seq) - 1)])
+        self.mid_conv = Conv2d(down_seq[-1], C * D, 1, 1, 0)
+        self.res = nn.Sequential()
+        self.C, self.D = C, D
+
+    def forward_2d(self, x):
+        return self.mid_conv(self.down(self.in_conv(x)))
+
+    def forward(self, x):
+        h = self.forward_2d(x)
+        N, _, H, W = h.shape
+        return h.reshape(N, self.C, self.D, H, W)
+
+
+class Generator(_Block):
+    """Decoder (models.py:1085-1111).  The grid_sample warp (1103) and occlusion multiply
+    (1106) are SURVEY.md §8(f) "next #2": forward() accepts them only as identity (None)."""
+
+    def __init__(self, use_weight_norm=True, n_res=6, up_seq=(256, 128, 64), D=16, C=32):
+        super().__init__()
+        up_seq = list(up_seq)
+        self.in_conv = ConvBlock2D("CNA", C * D, up_seq[0], 3, 1, 1, use_weight_norm, nonlinearity_type="leakyrelu")
+        self.mid_conv = Conv2d(up_seq[0], up_seq[0], 1, 1, 0)
+        self.res = nn.Sequential(*[ResBlock2D(up_seq[0], use_weight_norm) for _ in range(n_res)])
+        self.up = nn.Sequential(*[UpBlock2D(up_seq[i], up_seq[i + 1], use_weight_norm)
+                                  for i in range(len(up_seq) - 1)])
+        self.out_conv = Conv2d(up_seq[-1], 3, 7, 1, 3)
+
+    def forward_2d(self, fs):
+        fs = self.in_conv(fs)
+        fs = self.mid_conv(fs)
+        fs = self.res(fs)
+        fs = self.up(fs)
+        return self.out_conv(fs, sigmoid=True)       # conv + bias + sigmoid, NCHW fp32 out
+
+    def forward(self, fs, deformation=None, occlusion=None):
+        if deformation is not None or occlusion is not None:
+            raise NotImplementedError("Generator warp path (grid_sample/occlusion): SURVEY.md §8(f) next #2")
+        if fs.dim() == 5:
+            N, C, D, H, W = fs.shape
+            fs = fs.reshape(N, C * D, H, W)
+        return self.forward_2d(fs)
+
+
+class FaceVAE(_Block):
+    """AFE 2-D trunk -> [mu | logstd] split + reparameterisation -> Generator 2-D trunk.
+
+    forward(x, eps) -> (y, mu, logstd).  x: [B,3,H,H] fp32 in [0,1]; eps: [B,L,H/4,H/4]
+    standard-normal noise (the reference draws it with torch.randn inside
+    flatten_vae_nl, models.py:561; here it is an input so runs are reproducible)."""
+
+    def __init__(self, cfg: _config.FaceVAEConfig = None):
+        super().__init__()
+        cfg = cfg or _config.FaceVAEConfig()
+        self.cfg = cfg
+        self.afe = AFE(False, list(cfg.down_seq), 0, C=2 * cfg.latent, D=1)
+        self.generator = Generator(True, cfg.n_res, list(cfg.up_seq), D=1, C=cfg.latent)
+
+    def forward(self, x, eps):
+        h = self.afe.forward_2d(x)
+        mu, logstd, z = ops.reparameterise(h, eps, self.compute_dtype())
+        y = self.generator.forward_2d(z)
+        return y, mu, logstd

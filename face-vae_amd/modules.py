@@ -1,0 +1,219 @@
+"""Drop-in building blocks with the reference constructor signatures and state-dict keys
+(modules.py:8-130 of Luh1124/face-vae), computed by the HIP kernels in ops.py.
+
+Parameter / buffer layout is identical to the reference (e.g. `layers.0.weight_orig`,
+`layers.0.weight_u`, `layers.1.running_mean`), and construction draws the same RNG
+sequence as the reference constructors (nn.Conv2d.reset_parameters, then spectral_norm's
+u/v), so `torch.manual_seed(s)` gives bit-identical initial weights.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import config
+from . import ops
+
+
+class _Conv(nn.Module):
+    """Parameter holder of one conv: `weight` + `bias` or, with spectral norm,
+    `bias` + `weight_orig` + buffers `weight_u`/`weight_v` (torch/nn/utils/spectral_norm.py:163-181)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, use_sn=False, bias=True):
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = in_channels, out_channels, kernel_size
+        self.sn = use_sn
+        w = torch.empty(out_channels, in_channels, kernel_size, kernel_size)
+        b = torch.empty(out_channels) if bias else None
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))           # nn.Conv2d.reset_parameters
+        if b is not None:
+            bound = 1.0 / math.sqrt(in_channels * kernel_size * kernel_size)
+            nn.init.uniform_(b, -bound, bound)
+        if use_sn:
+            with torch.no_grad():
+                u = F.normalize(w.new_empty(out_channels).normal_(0, 1), dim=0, eps=1e-12)
+                v = F.normalize(w.new_empty(w[0].numel()).normal_(0, 1), dim=0, eps=1e-12)
+            self.bias = nn.Parameter(b) if b is not None else None
+            self.weight_orig = nn.Parameter(w)
+            self.register_buffer("weight_u", u)
+            self.register_buffer("weight_v", v)
+        else:
+            self.weight = nn.Parameter(w)
+            self.bias = nn.Parameter(b) if b is not None else None
+
+    def weight_param(self):
+        return self.weight_orig if self.sn else self.weight
+
+    def extra_repr(self):
+        return f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, sn={self.sn}"
+
+
+class _BatchNorm(nn.Module):
+    """SyncBatchNorm parameter/buffer holder (modules.py:19); statistics are synchronised
+    across ranks when a communicator is installed (distributed.py)."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = num_features, eps, momentum
+        self.track_running_stats = True
+        self.weight = nn.Parameter(torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def extra_repr(self):
+        return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}"
+
+
+class _Act(nn.Module):
+    def __init__(self, kind):
+        super().__init__()
+        self.kind = kind
+        self.slope = 0.0 if kind == "relu" else 0.2
+
+    def extra_repr(self):
+        return self.kind
+
+
+class _Upsample(nn.Module):
+    def extra_repr(self):
+        return "scale_factor=2, mode=nearest (folded into the conv addressing)"
+
+
+class _AvgPool(nn.Module):
+    def extra_repr(self):
+        return "kernel_size=2 (fused into the BN/act pass)"
+
+
+def _ref(owner, name, module):
+    """Keep a plain (unregistered) reference to a submodule: no duplicate state-dict keys."""
+    object.__setattr__(owner, name, module)
+
+
+class _Block(nn.Module):
+    """Common plumbing: compute dtype and the SyncBN communicator."""
+
+    _dtype = None
+
+    def compute_dtype(self):
+        return self._dtype or config.compute_dtype()
+
+    def set_compute_dtype(self, dtype):
+        for m in self.modules():
+            if hasattr(m, "_dtype"):
+                m._dtype = dtype
+        return self
+
+    def bn_comm(self):
+        from . import distributed
+        return distributed.syncbn_comm() if self.training else None
+
+
+class ConvBlock2D(_Block):
+    """_ConvBlock (modules.py:8-49).  Patterns "CNA" (BN on the output) and "NAC" (BN on the
+    input) are fused into one kernel chain; stride must be 1 and padding kernel_size // 2."""
+
+    def __init__(self, pattern, in_channels, out_channels, kernel_size, stride, padding, use_weight_norm,
+                 activation_type="batch", nonlinearity_type="relu"):
+        super().__init__()
+        if stride != 1 or padding != kernel_size // 2:
+            raise NotImplementedError("facevae_amd ConvBlock2D: stride 1, 'same' padding only")
+        if activation_type != "batch":
+            raise NotImplementedError("facevae_amd ConvBlock2D: activation_type='batch' only")
+        if pattern not in ("CNA", "NAC"):
+            raise NotImplementedError(f"pattern {pattern}")
+        self.pattern = pattern
+        norm_channels = out_channels if pattern.find("C") < pattern.find("N") else in_channels
+        mappings = {"C": _Conv(in_channels, out_channels, kernel_size, use_weight_norm),
+                    "N": _BatchNorm(norm_channels),
+                    "A": _Act(nonlinearity_type)}
+        self.layers = nn.Sequential(*[mappings[c] for c in pattern])
+        _ref(self, "conv", mappings["C"])
+        _ref(self, "bn", mappings["N"])
+        _ref(self, "act", mappings["A"])
+        self.slope = self.act.slope
+        self.upsample = False
+        self.pool = False
+
+    def forward(self, x):
+        fn = ops.ConvBNActFn if self.pattern == "CNA" else ops.NACFn
+        return fn.apply(x, self.conv.weight_param(), self.conv.bias, self.bn.weight, self.bn.bias, self)
+
+
+class DownBlock2D(_Block):
+    """CNA 3x3 then AvgPool2d(2) (modules.py:59-70); pool fused into the BN/act pass."""
+
+    def __init__(self, in_channels, out_channels, use_weight_norm):
+        super().__init__()
+        cb = ConvBlock2D("CNA", in_channels, out_channels, 3, 1, 1, use_weight_norm)
+        cb.pool = True
+        self.layers = nn.Sequential(cb, _AvgPool())
+
+    def forward(self, x):
+        return self.layers[0](x)
+
+
+class UpBlock2D(_Block):
+    """Upsample(x2, nearest) then CNA 3x3 (modules.py:78-89); the upsample is folded into the
+    conv's input addressing, never materialised."""
+
+    def __init__(self, in_channels, out_channels, use_weight_norm):
+        super().__init__()
+        cb = ConvBlock2D("CNA", in_channels, out_channels, 3, 1, 1, use_weight_norm)
+        cb.upsample = True
+        self.layers = nn.Sequential(_Upsample(), cb)
+
+    def forward(self, x):
+        return self.layers[1](x)
+
+
+class SameBlock2D(_Block):
+    """CNA 1x1 (modules.py:97-108)."""
+
+    def __init__(self, in_channels, out_channels, use_weight_norm):
+        super().__init__()
+        self.layers = ConvBlock2D("CNA", in_channels, out_channels, 1, 1, 0, use_weight_norm)
+
+    def forward(self, x):
+        return self.layers(x)
+
+
+class ResBlock2D(_Block):
+    """x + NAC(NAC(x)) (modules.py:116-130); BN-apply+ReLU run in each conv's prologue and
+    the residual add in the second conv's epilogue."""
+
+    def __init__(self, in_channels, use_weight_norm):
+        super().__init__()
+        self.layers = nn.Sequential(
+            ConvBlock2D("NAC", in_channels, in_channels, 3, 1, 1, use_weight_norm),
+            ConvBlock2D("NAC", in_channels, in_channels, 3, 1, 1, use_weight_norm),
+        )
+        _ref(self, "bn1", self.layers[0].bn)
+        _ref(self, "conv1", self.layers[0].conv)
+        _ref(self, "bn2", self.layers[1].bn)
+        _ref(self, "conv2", self.layers[1].conv)
+
+    def forward(self, x):
+        c1, c2 = self.conv1, self.conv2
+        return ops.ResBlockFn.apply(x, c1.weight_param(), c1.bias, self.bn1.weight, self.bn1.bias,
+                                    c2.weight_param(), c2.bias, self.bn2.weight, self.bn2.bias, self)
+
+
+class Conv2d(_Conv):
+    """nn.Conv2d drop-in (stride 1, 'same' padding) with state-dict keys weight / bias."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
+        if stride != 1 or padding != kernel_size // 2:
+            raise NotImplementedError("facevae_amd Conv2d: stride 1, 'same' padding only")
+        super().__init__(in_channels, out_channels, kernel_size, False, bias)
+        self._dtype = None
+
+    def compute_dtype(self):
+        return self._dtype or config.compute_dtype()
+
+    def forward(self, x, sigmoid=False):
+        return ops.ConvFn.apply(x, self.weight, self.bias, self, self.compute_dtype(), int(sigmoid))

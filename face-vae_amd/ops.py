@@ -1,0 +1,565 @@
+"""torch.autograd.Functions over libfacevae (the HIP C-ABI).  No CPU fallback: every
+compute call goes through `_lib.call`, which raises if the library is missing or fails.
+
+Activations between blocks are NHWC: torch tensors of logical shape [N, C, H, W] in
+`torch.channels_last` memory format, dtype = the compute dtype (fp32 parity mode or bf16).
+Parameters stay fp32 in the reference layout / state-dict keys.
+
+Reference semantics restated here (file:line in Luh1124/face-vae):
+  _ConvBlock "CNA"/"NAC" (modules.py:8-42), DownBlock2D (:59-70), UpBlock2D (:78-89),
+  ResBlock2D (:116-130), SameBlock2D (:97-108), nn.Conv2d (models.py:934,1096,1099),
+  spectral_norm (modules.py:14,32), SyncBatchNorm (modules.py:19), flatten_vae_nl
+  reparameterisation (models.py:559-561), KLDivergenceLoss (losses.py:385-393),
+  ReconLoss (losses.py:396-403), pixel L1 (losses.py:128,135).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr, query, stream
+
+CL = torch.channels_last
+F32 = torch.float32
+F64 = torch.float64
+
+
+def pad_pow2(c: int) -> int:
+    p = 8
+    while p < c:
+        p *= 2
+    return p
+
+
+def is_pow2_8(c: int) -> bool:
+    return c >= 8 and (c & (c - 1)) == 0
+
+
+def _empty(n, dtype, device):
+    return torch.empty(int(n), dtype=dtype, device=device)
+
+
+def nhwc_view(t: torch.Tensor) -> bool:
+    """True if t is a dense NHWC (channels_last) tensor."""
+    return t.dim() == 4 and t.is_contiguous(memory_format=CL)
+
+
+def to_nhwc(x: torch.Tensor, dtype: torch.dtype):
+    """x -> (buffer, channel stride): a dense NHWC tensor of `dtype` whose channel count is
+    a power of two >= 8 (zero padded), as the conv kernels require."""
+    if not x.is_cuda:
+        raise RuntimeError("facevae_amd ops run on the GPU only (HIP); got a CPU tensor")
+    N, C, H, W = x.shape
+    if is_pow2_8(C):
+        if x.dtype == dtype and nhwc_view(x):
+            return x, C
+        return x.to(dtype).contiguous(memory_format=CL), C
+    cp = pad_pow2(C)
+    buf = torch.empty((N, cp, H, W), dtype=dtype, device=x.device, memory_format=CL)
+    x32 = x.float().contiguous()
+    call("fv_nchw_to_nhwc", L.dtype_code(dtype), ptr(x32), N, C, H * W, cp, ptr(buf), stream())
+    return buf, cp
+
+
+def from_nhwc(buf: torch.Tensor, ref: torch.Tensor) -> torch.Tensor:
+    """Gradient buffer (NHWC, possibly channel padded) -> tensor shaped/typed like ref."""
+    N, C, H, W = ref.shape
+    if buf.shape[1] == C:
+        return buf.to(ref.dtype)
+    out = torch.empty((N, C, H, W), dtype=F32, device=buf.device)
+    call("fv_nhwc_to_nchw", L.dtype_code(buf.dtype), ptr(buf), N, C, H * W, buf.shape[1], ptr(out), stream())
+    return out.to(ref.dtype)
+
+
+class KernelTimer:
+    """Optional HIP-event bracketing of selected conv launches (bench.py measures the dominant
+    kernel's average duration live, on the stream it is launched on)."""
+
+    def __init__(self, match):
+        self.match = match          # (kind, ConvDesc) -> bool ; kind in {"fwd", "dgrad", "wgrad"}
+        self.events = {}
+        self.enabled = False
+
+    def wrap(self, kind, d, fn):
+        if not (self.enabled and self.match(kind, d)):
+            return fn()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn()
+        e1.record()
+        self.events.setdefault(kind, []).append((e0, e1))
+        return r
+
+    def summary(self):
+        torch.cuda.synchronize()
+        return {k: [a.elapsed_time(b) for a, b in v] for k, v in self.events.items()}
+
+
+TIMER: Optional[KernelTimer] = None
+
+
+def _timed(kind, d, fn):
+    return fn() if TIMER is None else TIMER.wrap(kind, d, fn)
+
+
+def desc(dtype, n, h, w, cin, cin_valid, cout, ldy, k, ups=0, pro=0, slope=0.0, sig=0, nchw=0):
+    return L.ConvDesc(L.dtype_code(dtype), n, h, w, cin, cin_valid, cout, ldy, k, int(ups), int(pro),
+                      float(slope), int(sig), int(nchw))
+
+
+# ----------------------------------------------------------------------------------------
+# spectral norm / weights
+# ----------------------------------------------------------------------------------------
+
+def spectral_norm_fwd(w, u, v, power_iter: bool):
+    rows = w.shape[0]
+    cols = w.numel() // rows
+    ws = _empty(query("fv_spectral_norm_ws_bytes", rows, cols) // 4 + 1, F32, w.device)
+    sigma = torch.empty(1, dtype=F32, device=w.device)
+    call("fv_spectral_norm_fwd", ptr(w), rows, cols, ptr(u), ptr(v), ptr(sigma), int(power_iter), ptr(ws),
+         stream())
+    return sigma
+
+
+def spectral_norm_bwd(w, g, u, v, sigma):
+    rows = w.shape[0]
+    cols = w.numel() // rows
+    ws = _empty(1024, F32, w.device)
+    call("fv_spectral_norm_bwd", ptr(w), ptr(g), rows, cols, ptr(u), ptr(v), ptr(sigma), ptr(g), ptr(ws),
+         stream())
+    return g
+
+
+class ConvState:
+    """Per-forward state of one conv: descriptor, prepared weights, SN snapshot."""
+
+    def __init__(self, conv, d, dtype, device, training, need_wt):
+        self.conv = conv
+        self.d = d
+        w = conv.weight_param()
+        if w.dtype != F32 or not w.is_contiguous():
+            raise RuntimeError("conv weights must be contiguous fp32")
+        self.w = w
+        self.sigma = None
+        if conv.sn:
+            self.sigma = spectral_norm_fwd(w, conv.weight_u, conv.weight_v, training)
+            self.u = conv.weight_u.clone()
+            self.v = conv.weight_v.clone()
+        self.wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
+        self.wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if need_wt else None
+        call("fv_conv_weight_prep", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
+             stream())
+
+    def release(self):
+        self.wk = None
+
+
+def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False):
+    d = cs.d
+    part = None
+    if stats:
+        nb = query("fv_conv2d_stats_blocks", ctypes.byref(d))
+        part = _empty(nb * 2 * d.cout, F32, x.device)
+    psc, psh = (pro if pro is not None else (None, None))
+    _timed("fwd", d, lambda: call("fv_conv2d_fwd", ctypes.byref(d), ptr(x), ptr(cs.wk), ptr(bias), ptr(psc),
+                                  ptr(psh), ptr(res), ptr(y), ptr(part), stream()))
+    return part
+
+
+def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=True):
+    """-> (dx at the conv input resolution (upsample folded back), dW (param layout), db)."""
+    d = cs.d
+    dev = dy.device
+    slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
+    ns = query("fv_conv2d_wgrad_nsplit", ctypes.byref(d))
+    bslab = _empty(ns * ((d.cout + 127) // 128) * 128, F32, dev) if need_db else None
+    psc, psh = (pro if pro is not None else (None, None))
+    _timed("wgrad", d, lambda: call("fv_conv2d_bwd_weight", ctypes.byref(d), ptr(x), ptr(psc), ptr(psh), ptr(dy),
+                                    ldd, ptr(slab), ptr(bslab), stream()))
+    dw = torch.empty_like(cs.w)
+    db = torch.empty(d.cout, dtype=F32, device=dev) if need_db else None
+    call("fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(dw), ptr(db), stream())
+    if cs.conv.sn:
+        spectral_norm_bwd(cs.w, dw, cs.u, cs.v, cs.sigma)
+    dx = None
+    if need_dx:
+        dx = torch.empty((d.n, d.cin, d.h, d.w), dtype=dy.dtype, device=dev, memory_format=CL)
+        _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data", ctypes.byref(d), ptr(dy), ldd, ptr(cs.wt), ptr(dx),
+                                        stream()))
+        if d.upsample:
+            src = torch.empty((d.n, d.cin, d.h // 2, d.w // 2), dtype=dy.dtype, device=dev, memory_format=CL)
+            call("fv_upsample2x_bwd", L.dtype_code(dy.dtype), ptr(dx), d.n, d.h // 2, d.w // 2, d.cin, ptr(src),
+                 stream())
+            dx = src
+    return dx, dw, db
+
+
+# ----------------------------------------------------------------------------------------
+# batch norm
+# ----------------------------------------------------------------------------------------
+
+class BNResult:
+    __slots__ = ("mean", "invstd", "scale", "shift", "count")
+
+
+def bn_finalize(bn, stats, count, training):
+    """stats [3][C] fp64 (already all-reduced for SyncBN) -> BNResult; updates running stats."""
+    C = bn.num_features
+    dev = bn.weight.device
+    r = BNResult()
+    r.mean = torch.empty(C, dtype=F32, device=dev)
+    r.invstd = torch.empty(C, dtype=F32, device=dev)
+    r.scale = torch.empty(C, dtype=F32, device=dev)
+    r.shift = torch.empty(C, dtype=F32, device=dev)
+    r.count = count
+    upd = training and bn.track_running_stats
+    call("fv_bn_finalize", ptr(stats), C, ptr(bn.weight), ptr(bn.bias), float(bn.eps), float(bn.momentum),
+         int(training), ptr(bn.running_mean if (upd or not training) else None),
+         ptr(bn.running_var if (upd or not training) else None), ptr(r.mean), ptr(r.invstd), ptr(r.scale),
+         ptr(r.shift), stream())
+    if upd:
+        bn.num_batches_tracked.add_(1)
+    return r
+
+
+def _sync(stats, comm, dtype_code=L.FV_F64):
+    if comm is not None:
+        comm.allreduce_(stats, op="sum")
+
+
+def bn_from_partials(bn, part, d, training, comm):
+    C = d.cout
+    dev = part.device
+    P = d.n * d.h * d.w
+    nb = query("fv_conv2d_stats_blocks", ctypes.byref(d))
+    bp = query("fv_conv2d_stats_block_pixels", ctypes.byref(d))
+    stats = torch.empty(3 * C, dtype=F64, device=dev)
+    ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, dev)
+    call("fv_bn_stats_from_partials", ptr(part), nb, bp, P, C, ptr(stats), ptr(ws), stream())
+    _sync(stats, comm)
+    world = comm.world_size if comm is not None else 1
+    return bn_finalize(bn, stats, P * world, training)
+
+
+def bn_from_tensor(bn, x, training, comm):
+    N, C, H, W = x.shape
+    if not training:
+        return bn_finalize(bn, None, 0, False)
+    stats = torch.empty(3 * C, dtype=F64, device=x.device)
+    ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, x.device)
+    call("fv_bn_stats_tensor", L.dtype_code(x.dtype), ptr(x), N * H * W, C, C, ptr(stats), ptr(ws), stream())
+    _sync(stats, comm)
+    world = comm.world_size if comm is not None else 1
+    return bn_finalize(bn, stats, N * H * W * world, True)
+
+
+def bn_act_forward(y, r: BNResult, slope, pool):
+    N, C, H, W = y.shape
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    out = torch.empty((N, C, Ho, Wo), dtype=y.dtype, device=y.device, memory_format=CL)
+    call("fv_bn_act_fwd", L.dtype_code(y.dtype), ptr(y), N, H, W, C, C, ptr(r.scale), ptr(r.shift), float(slope),
+         int(pool), ptr(out), stream())
+    return out
+
+
+def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True):
+    """-> (dx of the BN input, dgamma, dbeta)."""
+    N, C, H, W = y.shape
+    dev = y.device
+    dc = L.dtype_code(y.dtype)
+    red = torch.empty(2 * C, dtype=F64, device=dev)
+    ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, dev)
+    call("fv_bn_act_bwd_reduce", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd), ptr(bn.weight),
+         ptr(bn.bias), float(slope), int(pool), ptr(red), ptr(ws), stream())
+    _sync(red, comm)
+    dg = torch.empty(C, dtype=F32, device=dev)
+    dbt = torch.empty(C, dtype=F32, device=dev)
+    k = torch.empty(2 * C, dtype=F32, device=dev)
+    call("fv_bn_bwd_finalize", ptr(red), C, int(r.count), ptr(dg), ptr(dbt), ptr(k), stream())
+    dx = None
+    if need_dx:
+        dx = torch.empty((N, C, H, W), dtype=y.dtype, device=dev, memory_format=CL)
+        call("fv_bn_act_bwd_apply", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
+             ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), ptr(k), ptr(addend), ptr(dx), stream())
+    return dx, dg, dbt
+
+
+def grad_in(g: torch.Tensor, dtype) -> torch.Tensor:
+    return g.to(dtype).contiguous(memory_format=CL)
+
+
+# ----------------------------------------------------------------------------------------
+# autograd Functions
+# ----------------------------------------------------------------------------------------
+
+class ConvBNActFn(torch.autograd.Function):
+    """CNA block: conv -> BN -> act [-> AvgPool2d(2)], optional nearest-x2 upsample in front
+    (ConvBlock2D "CNA", DownBlock2D, UpBlock2D, SameBlock2D)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, blk):
+        dtype = blk.compute_dtype()
+        conv, bn = blk.conv, blk.bn
+        xb, cin_pad = to_nhwc(x, dtype)
+        N, _, Hi, Wi = x.shape
+        H, W = (2 * Hi, 2 * Wi) if blk.upsample else (Hi, Wi)
+        cout = conv.out_channels
+        if cout % 8:
+            raise RuntimeError("CNA block output channels must be a multiple of 8")
+        training = blk.training
+        d = desc(dtype, N, H, W, cin_pad, conv.in_channels, cout, cout, conv.kernel_size, ups=blk.upsample)
+        cs = ConvState(conv, d, dtype, x.device, training, need_wt=ctx.needs_input_grad[0])
+        y = torch.empty((N, cout, H, W), dtype=dtype, device=x.device, memory_format=CL)
+        part = conv_forward(cs, xb, bias, y=y, stats=training)
+        comm = blk.bn_comm()
+        r = bn_from_partials(bn, part, d, True, comm) if training else bn_finalize(bn, None, 0, False)
+        z = bn_act_forward(y, r, blk.slope, blk.pool)
+        cs.release()
+        ctx.blk, ctx.cs, ctx.r, ctx.comm = blk, cs, r, comm
+        ctx.save_for_backward(x, xb, y)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, xb, y = ctx.saved_tensors
+        blk, cs, r = ctx.blk, ctx.cs, ctx.r
+        dz = grad_in(dz, y.dtype)
+        dy, dg, dbt = bn_act_backward(dz, y, blk.bn, r, blk.slope, blk.pool, ctx.comm)
+        dxb, dw, db = conv_backward(cs, xb, dy, y.shape[1], need_dx=ctx.needs_input_grad[0])
+        dx = from_nhwc(dxb, x) if dxb is not None else None
+        return dx, dw, db, dg, dbt, None
+
+
+class ResBlockFn(torch.autograd.Function):
+    """ResBlock2D: x + NAC(NAC(x)), NAC = BN -> ReLU -> conv3x3 (modules.py:116-130)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, blk):
+        dtype = blk.compute_dtype()
+        xb, C = to_nhwc(x, dtype)
+        if C != x.shape[1]:
+            raise RuntimeError("ResBlock2D channels must be a power of two >= 8")
+        N, _, H, W = x.shape
+        training = blk.training
+        comm = blk.bn_comm()
+        c1, c2 = blk.conv1, blk.conv2
+        need_wt = any(ctx.needs_input_grad[:9])
+        r1 = bn_from_tensor(blk.bn1, xb, training, comm)
+        d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size, pro=1, slope=0.0)
+        cs1 = ConvState(c1, d1, dtype, x.device, training, need_wt)
+        t1 = torch.empty_like(xb)
+        part = conv_forward(cs1, xb, b1, pro=(r1.scale, r1.shift), y=t1, stats=training)
+        r2 = bn_from_partials(blk.bn2, part, d1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
+        d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size, pro=1, slope=0.0)
+        cs2 = ConvState(c2, d2, dtype, x.device, training, need_wt)
+        out = torch.empty_like(xb)
+        conv_forward(cs2, t1, b2, pro=(r2.scale, r2.shift), res=xb, y=out)
+        cs1.release()
+        cs2.release()
+        ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm = blk, cs1, cs2, r1, r2, comm
+        ctx.save_for_backward(x, xb, t1)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, xb, t1 = ctx.saved_tensors
+        blk, cs1, cs2, r1, r2, comm = ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm
+        C = xb.shape[1]
+        dout = grad_in(dout, xb.dtype)
+        da2, dw2, db2 = conv_backward(cs2, t1, dout, C, pro=(r2.scale, r2.shift))
+        dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm)
+        da1, dw1, db1 = conv_backward(cs1, xb, dt1, C, pro=(r1.scale, r1.shift))
+        dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout)
+        dx = from_nhwc(dxb, x)
+        return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None
+
+
+class NACFn(torch.autograd.Function):
+    """Standalone "NAC" ConvBlock2D: conv(act(BN(x))) with BN-apply + act in the conv prologue."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, blk):
+        dtype = blk.compute_dtype()
+        xb, C = to_nhwc(x, dtype)
+        if C != x.shape[1]:
+            raise RuntimeError("NAC block input channels must be a power of two >= 8")
+        N, _, H, W = x.shape
+        conv = blk.conv
+        cout = conv.out_channels
+        if cout % 8:
+            raise RuntimeError("NAC block output channels must be a multiple of 8")
+        comm = blk.bn_comm()
+        r = bn_from_tensor(blk.bn, xb, blk.training, comm)
+        d = desc(dtype, N, H, W, C, C, cout, cout, conv.kernel_size, pro=1, slope=blk.slope)
+        cs = ConvState(conv, d, dtype, x.device, blk.training, need_wt=True)
+        y = torch.empty((N, cout, H, W), dtype=dtype, device=x.device, memory_format=CL)
+        conv_forward(cs, xb, bias, pro=(r.scale, r.shift), y=y)
+        cs.release()
+        ctx.blk, ctx.cs, ctx.r, ctx.comm = blk, cs, r, comm
+        ctx.save_for_backward(x, xb)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xb = ctx.saved_tensors
+        blk, cs, r = ctx.blk, ctx.cs, ctx.r
+        dy = grad_in(dy, xb.dtype)
+        da, dw, db = conv_backward(cs, xb, dy, dy.shape[1], pro=(r.scale, r.shift))
+        dxb, dg, dbt = bn_act_backward(da, xb, blk.bn, r, blk.slope, False, ctx.comm,
+                                       need_dx=ctx.needs_input_grad[0])
+        return (from_nhwc(dxb, x) if dxb is not None else None), dw, db, dg, dbt, None
+
+
+class ConvFn(torch.autograd.Function):
+    """Plain nn.Conv2d (+ optional fused sigmoid with NCHW fp32 output: models.py:1099,1110)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, conv, dtype, sigmoid):
+        xb, cin_pad = to_nhwc(x, dtype)
+        N, _, H, W = x.shape
+        cout = conv.out_channels
+        nchw = bool(sigmoid) or (cout % 8 != 0)
+        d = desc(dtype, N, H, W, cin_pad, conv.in_channels, cout, cout, conv.kernel_size, sig=sigmoid, nchw=nchw)
+        cs = ConvState(conv, d, dtype, x.device, conv.training, need_wt=ctx.needs_input_grad[0])
+        if nchw:
+            y = torch.empty((N, cout, H, W), dtype=F32, device=x.device)
+        else:
+            y = torch.empty((N, cout, H, W), dtype=dtype, device=x.device, memory_format=CL)
+        conv_forward(cs, xb, bias, y=y)
+        cs.release()
+        ctx.cs, ctx.sigmoid, ctx.nchw, ctx.dtype = cs, sigmoid, nchw, dtype
+        ctx.save_for_backward(x, xb, y if sigmoid else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xb, y = ctx.saved_tensors
+        cs = ctx.cs
+        d = cs.d
+        dtype = ctx.dtype
+        if ctx.nchw:
+            ldd = pad_pow2(d.cout)
+            dpre = torch.empty((d.n, ldd, d.h, d.w), dtype=dtype, device=dy.device, memory_format=CL)
+            dy32 = dy.float().contiguous()
+            if ctx.sigmoid:
+                call("fv_sigmoid_bwd_to_nhwc", L.dtype_code(dtype), ptr(dy32), ptr(y), d.n, d.cout, d.h * d.w, ldd,
+                     ptr(dpre), stream())
+            else:
+                call("fv_nchw_to_nhwc", L.dtype_code(dtype), ptr(dy32), d.n, d.cout, d.h * d.w, ldd, ptr(dpre),
+                     stream())
+        else:
+            ldd = d.cout
+            dpre = grad_in(dy, dtype)
+        dxb, dw, db = conv_backward(cs, xb, dpre, ldd, need_dx=ctx.needs_input_grad[0])
+        dx = from_nhwc(dxb, x) if dxb is not None else None
+        return dx, dw, db, None, None, None
+
+
+class ReparamFn(torch.autograd.Function):
+    """mu = h[:, :L], logstd = h[:, L:], z = mu + exp(logstd) * eps (models.py:559-561)."""
+
+    @staticmethod
+    def forward(ctx, h, eps, dtype):
+        hb, C2 = to_nhwc(h, dtype)
+        N, _, H, W = h.shape
+        Lc = C2 // 2
+        e32 = eps.float().contiguous()
+        if tuple(e32.shape) != (N, Lc, H, W):
+            raise RuntimeError(f"eps must be [N, {Lc}, {H}, {W}]")
+        mu = torch.empty((N, Lc, H, W), dtype=dtype, device=h.device, memory_format=CL)
+        ls = torch.empty_like(mu)
+        z = torch.empty_like(mu)
+        call("fv_reparam_fwd", L.dtype_code(dtype), ptr(hb), ptr(e32), N, Lc, H * W, ptr(mu), ptr(ls), ptr(z),
+             stream())
+        ctx.save_for_backward(h, hb, e32)
+        ctx.dtype = dtype
+        return mu, ls, z
+
+    @staticmethod
+    def backward(ctx, dmu, dls, dz):
+        h, hb, e32 = ctx.saved_tensors
+        N, C2, H, W = hb.shape
+        dt = ctx.dtype
+        dh = torch.empty_like(hb)
+        call("fv_reparam_bwd", L.dtype_code(dt), ptr(hb), ptr(e32), N, C2 // 2, H * W,
+             ptr(grad_in(dz, dt) if dz is not None else None),
+             ptr(grad_in(dmu, dt) if dmu is not None else None),
+             ptr(grad_in(dls, dt) if dls is not None else None), ptr(dh), stream())
+        return from_nhwc(dh, h), None, None
+
+
+def _same_layout(a, b):
+    if a.shape == b.shape and a.stride() == b.stride() and a.dtype == b.dtype and (
+            a.is_contiguous() or nhwc_view(a)):
+        return a, b
+    return a.contiguous(), b.to(a.dtype).contiguous()
+
+
+class KLFn(torch.autograd.Function):
+    """mean(-0.5 - logstd + 0.5 mu^2 + 0.5 exp(2 logstd)) (losses.py:392)."""
+
+    @staticmethod
+    def forward(ctx, mu, logstd):
+        if mu.dtype not in (F32, torch.bfloat16):
+            mu, logstd = mu.float(), logstd.float()
+        mu, logstd = _same_layout(mu, logstd)
+        out = torch.empty((), dtype=F32, device=mu.device)
+        ws = _empty(query("fv_loss_ws_bytes") // 8, F64, mu.device)
+        call("fv_kl_fwd", L.dtype_code(mu.dtype), ptr(mu), ptr(logstd), mu.numel(), ptr(out), ptr(ws), stream())
+        ctx.save_for_backward(mu, logstd)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        mu, ls = ctx.saved_tensors
+        g = g.float().contiguous()
+        dmu = torch.empty_like(mu) if ctx.needs_input_grad[0] else None
+        dls = torch.empty_like(ls) if ctx.needs_input_grad[1] else None
+        call("fv_kl_bwd", L.dtype_code(mu.dtype), ptr(mu), ptr(ls), mu.numel(), ptr(g), ptr(dmu), ptr(dls), stream())
+        return dmu, dls
+
+
+class _PairLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, kind):
+        a32 = a.float()
+        b32 = b.float()
+        a32, b32 = _same_layout(a32, b32)
+        out = torch.empty((), dtype=F32, device=a.device)
+        ws = _empty(query("fv_loss_ws_bytes") // 8, F64, a.device)
+        call("fv_mse_fwd" if kind == "mse" else "fv_l1_fwd", ptr(a32), ptr(b32), a32.numel(), ptr(out), ptr(ws),
+             stream())
+        ctx.save_for_backward(a32, b32)
+        ctx.kind = kind
+        ctx.dt = (a.dtype, b.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.float().contiguous()
+        da = torch.empty_like(a) if ctx.needs_input_grad[0] else None
+        db = torch.empty_like(b) if ctx.needs_input_grad[1] else None
+        call("fv_mse_bwd" if ctx.kind == "mse" else "fv_l1_bwd", ptr(a), ptr(b), a.numel(), ptr(g), ptr(da),
+             ptr(db), stream())
+        return (da.to(ctx.dt[0]) if da is not None else None, db.to(ctx.dt[1]) if db is not None else None, None)
+
+
+def mse_loss(a, b):
+    return _PairLossFn.apply(a, b, "mse")
+
+
+def l1_loss(a, b):
+    return _PairLossFn.apply(a, b, "l1")
+
+
+def kl_loss(mu, logstd):
+    return KLFn.apply(mu, logstd)
+
+
+def reparameterise(h, eps, dtype):
+    return ReparamFn.apply(h, eps, dtype)

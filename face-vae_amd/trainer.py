@@ -1,0 +1,130 @@
+"""Logger-compatible FaceVAE trainer (logger.py:24-184 of Luh1124/face-vae, restricted to the
+FaceVAE hot path).
+
+`FaceVAETrainer(ckp_dir, vis_dir, dataloader, lr, ...)` keeps the reference constructor and
+the `.step()` / `.save_cpk()` / `.load_cpk(epoch)` surface.  One `train_step` is the
+Logger.step iteration (logger.py:150-164): zero_grad -> forward -> loss = sum of weighted
+losses -> backward (gradient all-reduce overlapped) -> Adam.step.  The batch element used
+as the VAE input is `driving`.
+"""
+from __future__ import annotations
+
+import collections
+import os
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import config as _config
+from . import distributed
+from .losses import KLDivergenceLoss, ReconLoss
+from .models import FaceVAE
+from .optim import Adam
+
+
+class FaceVAETrainer:
+    def __init__(self, ckp_dir, vis_dir, dataloader, lr, checkpoint_freq=1, visualizer_params=None, zfill_num=8,
+                 log_file_name="log_facevae.txt", cfg: Optional[_config.FaceVAEConfig] = None,
+                 compute_dtype: Optional[torch.dtype] = None, seed: Optional[int] = 0):
+        self.cfg = cfg or _config.FaceVAEConfig(lr=lr)
+        self.ckp_dir, self.vis_dir = ckp_dir, vis_dir
+        self.dataloader = dataloader
+        self.checkpoint_freq, self.zfill_num = checkpoint_freq, zfill_num
+        self.epoch = 0
+        self.g_losses = []
+        self.loss_names = None
+        self.log_file = None
+        if distributed.is_master() and ckp_dir is not None:
+            os.makedirs(ckp_dir, exist_ok=True)
+            if vis_dir:
+                os.makedirs(vis_dir, exist_ok=True)
+            self.log_file = open(log_file_name, "a")
+        if seed is not None:
+            torch.manual_seed(seed)
+        self.model = FaceVAE(self.cfg).cuda()
+        if compute_dtype is not None:
+            self.model.set_compute_dtype(compute_dtype)
+        self.comm = distributed.get_comm()
+        self.ddp = distributed.DataParallel(self.model, self.comm) if self.comm is not None else None
+        self.net = self.ddp if self.ddp is not None else self.model
+        # one Adam per model as logger.py:60 (elementwise: identical to one over all params)
+        self.g_models = {"afe": self.model.afe, "generator": self.model.generator}
+        self.g_optimizers = {k: Adam(m.parameters(), lr=lr, betas=self.cfg.betas) for k, m in self.g_models.items()}
+        self.kl, self.recon = KLDivergenceLoss(), ReconLoss()
+        self.weights = {"R": self.cfg.w_R, "K": self.cfg.w_K}
+        self._eps_gen = None
+
+    # ---------------------------------------------------------------- one iteration
+    def train_step(self, x: torch.Tensor, eps: torch.Tensor) -> Dict[str, torch.Tensor]:
+        for opt in self.g_optimizers.values():
+            opt.zero_grad(set_to_none=True)
+        y, mu, logstd = self.net(x, eps)
+        losses = {"R": self.weights["R"] * self.recon((x, y)),
+                  "K": self.weights["K"] * self.kl((mu, logstd))}
+        loss = sum(losses.values())
+        loss.backward()
+        for opt in self.g_optimizers.values():
+            opt.step()
+        losses["y"] = y
+        return losses
+
+    def sample_eps(self, x: torch.Tensor) -> torch.Tensor:
+        B = x.shape[0]
+        h = self.cfg.latent_hw
+        if self._eps_gen is None:
+            self._eps_gen = torch.Generator(device=x.device)
+            self._eps_gen.manual_seed(1 + distributed.get_rank())
+        return torch.randn(B, self.cfg.latent, h, h, device=x.device, generator=self._eps_gen)
+
+    # ---------------------------------------------------------------- Logger surface
+    def step(self):
+        """One epoch over the dataloader (logger.py:135-184)."""
+        for idx, batch in enumerate(self.dataloader):
+            s, d, s_a, d_a = batch
+            d = d.cuda(non_blocking=True)
+            out = self.train_step(d, self.sample_eps(d))
+            self.log_iter({k: v.detach().float().cpu().numpy() for k, v in out.items() if k != "y"})
+        self.log_epoch()
+        self.epoch += 1
+
+    def log_iter(self, losses):
+        if not distributed.is_master():
+            return
+        losses = collections.OrderedDict(losses.items())
+        if self.loss_names is None:
+            self.loss_names = list(losses.keys())
+        self.g_losses.append(list(losses.values()))
+
+    def log_scores(self):
+        if not distributed.is_master() or self.log_file is None or not self.g_losses:
+            return
+        loss_mean = np.array(self.g_losses).mean(axis=0)
+        s = "; ".join("%s - %.5f" % (n, v) for n, v in zip(self.loss_names, loss_mean))
+        print("G" + str(self.epoch).zfill(self.zfill_num) + ") " + s, file=self.log_file)
+        self.log_file.flush()
+        self.g_losses = []
+
+    def log_epoch(self):
+        if (self.epoch + 1) % self.checkpoint_freq == 0:
+            self.save_cpk()
+        self.log_scores()
+        if self.ddp is not None:
+            self.ddp.sync_buffers()
+
+    def save_cpk(self):
+        if not distributed.is_master() or self.ckp_dir is None:
+            return
+        ckp = {**{k: m.state_dict() for k, m in self.g_models.items()},
+               **{"optimizer_" + k: o.state_dict() for k, o in self.g_optimizers.items()},
+               "epoch": self.epoch}
+        torch.save(ckp, os.path.join(self.ckp_dir, "%s-checkpoint.pth.tar" % str(self.epoch).zfill(self.zfill_num)))
+
+    def load_cpk(self, epoch):
+        path = os.path.join(self.ckp_dir, "%s-checkpoint.pth.tar" % str(epoch).zfill(self.zfill_num))
+        ckp = torch.load(path, map_location="cpu", weights_only=True)
+        for k, m in self.g_models.items():
+            m.load_state_dict(ckp[k])
+        for k, o in self.g_optimizers.items():
+            o.load_state_dict(ckp["optimizer_" + k])
+        self.epoch = ckp["epoch"] + 1

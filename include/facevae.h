@@ -1,0 +1,217 @@
+/* libfacevae — MI355X (gfx950) C-ABI for the FaceVAE training step.
+ *
+ * Plain C ABI: raw device pointers, sizes, a dtype enum and an explicit hipStream_t
+ * (passed as void*).  No torch types.  Every entry returns an int status (FV_OK = 0;
+ * >0 = FV_E_* or a hipError_t); the message of the last failure on the calling thread is
+ * available from fv_last_error().  Nothing aborts, nothing allocates device memory on
+ * the hot path: callers size workspaces with the *_ws_bytes / *_elems helpers.
+ *
+ * Activations are NHWC ("channels_last") with a channel stride `ld*` ≥ valid channels.
+ * Conv weights are handed over in the reference parameter layout
+ * (nn.Conv2d.weight [Cout][Cin][k][k], fp32) and re-laid out per forward by
+ * fv_conv_weight_prep into the kernel layout [rows][Kpad] with k = (r*k + s)*cin + ci.
+ *
+ * Which reference interface each entry replaces (file:line in Luh1124/face-vae):
+ *   fv_conv2d_fwd            F.conv2d inside _ConvBlock / nn.Conv2d (modules.py:32-42,
+ *                            models.py:934,1096,1099) incl. nn.Upsample (modules.py:81)
+ *                            folded into addressing, BN-apply+act prologue (NAC,
+ *                            modules.py:13,31-39), bias/residual (modules.py:125)/sigmoid
+ *                            (models.py:1110) epilogue and BN statistics partials.
+ *   fv_conv2d_bwd_data       conv backward-data == transposed conv (ConvTranspose2dELR's
+ *                            F.conv_transpose2d, models_utils.py:498-499, stride 1 case).
+ *   fv_conv2d_bwd_weight     conv weight/bias gradient (autograd of modules.py:32).
+ *   fv_spectral_norm_*       torch.nn.utils.spectral_norm as used by modules.py:14,32.
+ *   fv_bn_*                  nn.SyncBatchNorm train/eval (modules.py:19; logger.py:55).
+ *   fv_reparam_*             flatten_vae_nl split + reparameterisation (models.py:559-561).
+ *   fv_kl_*                  KLDivergenceLoss (losses.py:385-393).
+ *   fv_mse_*                 ReconLoss / nn.MSELoss (losses.py:396-403).
+ *   fv_l1_*                  PerceptualLoss pixel term nn.L1Loss (losses.py:128,135).
+ *   fv_adam_step             torch.optim.Adam(lr, betas=(0.5,0.999)) (logger.py:60-61).
+ *   fv_comm_*                distributed.py:24-31 init_process_group("nccl") + DDP's
+ *                            gradient all-reduce (logger.py:55,58) + SyncBN collectives.
+ */
+#ifndef FACEVAE_H
+#define FACEVAE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FV_ABI_VERSION 1
+
+enum fv_status {
+  FV_OK = 0,
+  FV_E_BADARG = 1001,
+  FV_E_UNSUPPORTED = 1002,
+  FV_E_COMM = 1003
+};
+
+enum fv_dtype { FV_F32 = 0, FV_BF16 = 1, FV_F64 = 2 };
+
+int fv_abi_version(void);
+const char* fv_last_error(void);
+
+/* ---------------------------------------------------------------- convolution ---- */
+typedef struct fv_conv_desc {
+  int dtype;         /* FV_F32 (exact fp32 MFMA) or FV_BF16 (bf16 MFMA, fp32 accumulate) */
+  int n, h, w;       /* output spatial size (== conv input size unless upsample) */
+  int cin;           /* channel stride of x: power of two >= 8 (zero padded channels) */
+  int cin_valid;     /* real input channels (<= cin) */
+  int cout;          /* valid output channels */
+  int ldy;           /* channel stride of y and res (>= cout; ignored for out_nchw_f32) */
+  int ksize;         /* 1, 3 or 7; stride 1, padding ksize/2 */
+  int upsample;      /* 1: x is (h/2, w/2), nearest x2 upsample folded into addressing */
+  int pro_act;       /* 1: conv input is act(x*scale[c]+shift[c]) (BN-apply + act) */
+  float pro_slope;   /* act slope for negatives: 0 = ReLU, 0.2 = LeakyReLU */
+  int epi_sigmoid;   /* 1: y = sigmoid(conv + bias [+ res]) */
+  int out_nchw_f32;  /* 1: store y as NCHW fp32 [n][cout][h][w] */
+} fv_conv_desc;
+
+/* elements of the kernel-layout weight buffers (wk for fwd, wt for bwd-data) */
+size_t fv_conv_wk_elems(const fv_conv_desc* d);
+size_t fv_conv_wt_elems(const fv_conv_desc* d);
+/* number of per-block BN partial records written by fv_conv2d_fwd (stats: [blocks][2][cout]) */
+int fv_conv2d_stats_blocks(const fv_conv_desc* d);
+int fv_conv2d_stats_block_pixels(const fv_conv_desc* d);
+
+/* w_param [cout][cin_valid][k][k] fp32 -> wk [rows][Kpad], wt [rows_t][Kpad_t] (either may be
+ * NULL), both scaled by 1/sigma[0] when sigma != NULL (spectral norm), dtype d->dtype. */
+int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma,
+                        void* wk, void* wt, void* stream);
+
+/* y = epi(conv(pro(x), wk) + bias [+ res]); stats (optional) receives per-block
+ * (sum, centred sum of squares) of the pre-sigmoid output per channel. */
+int fv_conv2d_fwd(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
+                  const float* pro_scale, const float* pro_shift, const void* res, void* y,
+                  float* stats, void* stream);
+
+/* dx[n][h'][w'][cin] = conv_transpose(dy, w) at the conv INPUT resolution of `d` with
+ * upsample == 0 (dgrad at the upsampled resolution when d->upsample; see
+ * fv_upsample2x_bwd).  dy has channel stride ldy_dy (>= cout, multiple of 8). */
+int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt,
+                       void* dx, void* stream);
+
+/* weight gradient w.r.t. the effective (post-SN) weight, split over pixels:
+ * slab [nsplit][rows][Kpad] fp32 and bias slab [nsplit][cout] fp32. */
+int fv_conv2d_wgrad_nsplit(const fv_conv_desc* d);
+size_t fv_conv2d_wgrad_slab_elems(const fv_conv_desc* d);
+int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_scale,
+                         const float* pro_shift, const void* dy, int ldy_dy, float* slab,
+                         float* bias_slab, void* stream);
+/* reduce the slabs into dw_param [cout][cin_valid][k][k] (fp32, reference layout) and
+ * db [cout] (db may be NULL). */
+int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab,
+                           float* dw_param, float* db, void* stream);
+
+/* ------------------------------------------------------------- spectral norm ---- */
+size_t fv_spectral_norm_ws_bytes(int rows, int cols);
+/* one power iteration (u, v updated in place) when power_iter, then sigma = u.(W v) */
+int fv_spectral_norm_fwd(const float* w, int rows, int cols, float* u, float* v, float* sigma,
+                         int power_iter, void* ws, void* stream);
+/* g_orig = g_sn/sigma - <g_sn, w>/sigma^2 * u v^T   (in place allowed: g_orig == g_sn) */
+int fv_spectral_norm_bwd(const float* w, const float* g_sn, int rows, int cols, const float* u,
+                         const float* v, const float* sigma, float* g_orig, void* ws,
+                         void* stream);
+
+/* ---------------------------------------------------------------- batch norm ---- */
+size_t fv_bn_ws_bytes(int c);
+/* (count, sum, centred-M2) conv partials -> stats [3][c] doubles (count, sum, sumsq) */
+int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixels,
+                              long total_pixels, int c, double* stats, void* ws, void* stream);
+/* statistics of an NHWC tensor (pixels x c, channel stride ldc) -> stats [3][c] */
+int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, double* stats,
+                       void* ws, void* stream);
+/* mean/var from stats (already all-reduced for SyncBN) -> save_mean, save_invstd and the
+ * fused affine scale = gamma*invstd, shift = beta - mean*scale; running stats updated
+ * with momentum and the unbiased variance when training.  In eval mode the running
+ * statistics are used and stats may be NULL. */
+int fv_bn_finalize(const double* stats, int c, const float* gamma, const float* beta, float eps,
+                   float momentum, int training, float* running_mean, float* running_var,
+                   float* save_mean, float* save_invstd, float* scale, float* shift,
+                   void* stream);
+/* out = [avgpool2](act(y*scale + shift)); y [n][h][w][ldc], out [n][h/p][w/p][c] */
+int fv_bn_act_fwd(int dtype, const void* y, int n, int h, int w, int c, int ldc,
+                  const float* scale, const float* shift, float slope, int pool, void* out,
+                  void* stream);
+/* sums over pixels of g and g*yhat with g = dout_full * act'(.) -> red [2][c] doubles */
+int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
+                         int ldc, const float* mean, const float* invstd, const float* gamma,
+                         const float* beta, float slope, int pool, double* red, void* ws,
+                         void* stream);
+/* dgamma/dbeta (accumulated) and the two BN-backward coefficients k [2][c] */
+int fv_bn_bwd_finalize(const double* red, int c, long count, float* dgamma, float* dbeta,
+                       float* k, void* stream);
+/* dx = gamma*invstd*(g - k0 - yhat*k1) [+ addend]; dx/addend [n][h][w][ldc] */
+int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
+                        int ldc, const float* mean, const float* invstd, const float* gamma,
+                        const float* beta, float slope, int pool, const float* k,
+                        const void* addend, void* dx, void* stream);
+
+/* ------------------------------------------------------ elementwise / layout ---- */
+int fv_nchw_to_nhwc(int dtype_out, const float* x, int n, int c, int hw, int ldc, void* out,
+                    void* stream);
+int fv_nhwc_to_nchw(int dtype_in, const void* x, int n, int c, int hw, int ldc, float* out,
+                    void* stream);
+int fv_cast(int dtype_in, const void* x, int dtype_out, void* y, long count, void* stream);
+/* g_src[n][i][j][c] = sum_{a,b} g[n][2i+a][2j+b][c]  (nearest x2 upsample backward) */
+int fv_upsample2x_bwd(int dtype, const void* g, int n, int h_src, int w_src, int c, void* out,
+                      void* stream);
+/* dpre (NHWC, channel stride ldc, zero padded) = dy * y * (1 - y), dy/y NCHW fp32 */
+int fv_sigmoid_bwd_to_nhwc(int dtype_out, const float* dy, const float* y, int n, int c, int hw,
+                           int ldc, void* dpre, void* stream);
+
+/* --------------------------------------------------------- latent and losses ---- */
+size_t fv_loss_ws_bytes(void);
+/* h [P][2L] (NHWC, mu = channels [0,L), logstd = [L,2L)); eps NCHW fp32 [n][L][hw];
+ * mu/logstd/z [P][L] NHWC */
+int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu,
+                   void* logstd, void* z, void* stream);
+/* dh = [dz + dmu | dz*exp(logstd)*eps + dlogstd]; dmu/dlogstd may be NULL */
+int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw,
+                   const void* dz, const void* dmu, const void* dlogstd, void* dh, void* stream);
+int fv_kl_fwd(int dtype, const void* mu, const void* logstd, long count, float* loss, void* ws,
+              void* stream);
+int fv_kl_bwd(int dtype, const void* mu, const void* logstd, long count, const float* gout,
+              void* dmu, void* dlogstd, void* stream);
+int fv_mse_fwd(const float* a, const float* b, long count, float* loss, void* ws, void* stream);
+int fv_mse_bwd(const float* a, const float* b, long count, const float* gout, float* da,
+               float* db, void* stream);
+int fv_l1_fwd(const float* a, const float* b, long count, float* loss, void* ws, void* stream);
+int fv_l1_bwd(const float* a, const float* b, long count, const float* gout, float* da,
+              float* db, void* stream);
+
+/* ----------------------------------------------------------------- optimiser ---- */
+typedef struct fv_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  long numel;
+} fv_adam_tensor;
+#define FV_ADAM_CHUNK 4096
+/* multi-tensor Adam (torch.optim.Adam math, no weight decay / amsgrad).  `tensors` is a
+ * DEVICE array of descriptors; `blocks` a DEVICE array of nblocks (tensor, chunk) int pairs,
+ * one per FV_ADAM_CHUNK elements of each tensor; `step` is the step count after increment. */
+int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, float lr,
+                 float beta1, float beta2, float eps, long step, void* stream);
+
+/* ------------------------------------------------------------ communication ---- */
+typedef void* fv_comm_t;
+int fv_comm_unique_id(uint8_t out[128]);
+int fv_comm_init(const uint8_t id[128], int nranks, int rank, int device, fv_comm_t* comm);
+/* op: 0 = sum, 1 = average; dtype: FV_F32 / FV_BF16 / FV_F64 */
+int fv_comm_allreduce(fv_comm_t comm, void* buf, size_t count, int dtype, int op,
+                      void* stream);
+int fv_comm_allgather(fv_comm_t comm, const void* send, void* recv, size_t count_per_rank,
+                      int dtype, void* stream);
+int fv_comm_broadcast(fv_comm_t comm, void* buf, size_t count, int dtype, int root,
+                      void* stream);
+int fv_comm_destroy(fv_comm_t comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FACEVAE_H */

@@ -1,0 +1,245 @@
+"""GPU parity of each HIP kernel family against a plain torch fp32 reference of the same op
+(computed on the host CPU).  fp32 mode is the exact-fp32 MFMA path (tolerance 1e-5
+relative L2); bf16 mode is checked at bf16 tolerance (2e-2)."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+import fvamd  # noqa: E402,F401
+import facevae_amd as fv  # noqa: E402
+from facevae_amd import _lib as L  # noqa: E402
+from facevae_amd import ops  # noqa: E402
+
+CL = torch.channels_last
+TOL = {torch.float32: 1e-5, torch.bfloat16: 2e-2}
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+def conv_setup(x, w, k, dtype, ups=False, pro=False, slope=0.0, sigmoid=False, need_wt=False):
+    N, C, Hi, Wi = x.shape
+    cout = w.shape[0]
+    H, W = (2 * Hi, 2 * Wi) if ups else (Hi, Wi)
+    xb, cp = ops.to_nhwc(x.cuda(), dtype)
+    d = ops.desc(dtype, N, H, W, cp, C, cout, cout, k, ups, pro, slope, sigmoid, 0)
+    wk = torch.empty(L.query("fv_conv_wk_elems", ctypes.byref(d)), dtype=dtype, device="cuda")
+    wt = torch.empty(L.query("fv_conv_wt_elems", ctypes.byref(d)), dtype=dtype, device="cuda") if need_wt else None
+    wc = w.cuda().float().contiguous()
+    L.call("fv_conv_weight_prep", ctypes.byref(d), wc.data_ptr(), None, wk.data_ptr(), L.ptr(wt), L.stream())
+    return d, xb, wk, wt, (N, cout, H, W)
+
+
+CONV_CASES = [
+    # k, cin, cout, H, W, ups, pro
+    (3, 32, 64, 12, 10, False, False),
+    (3, 64, 128, 16, 16, False, True),
+    (1, 256, 512, 8, 8, False, False),
+    (7, 3, 64, 16, 16, False, False),
+    (7, 64, 3, 16, 16, False, False),
+    (3, 128, 64, 8, 8, True, False),
+    (3, 32, 32, 8, 6, True, True),
+    (3, 16, 32, 7, 9, False, False),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd(case, dtype):
+    k, cin, cout, H, W, ups, pro = case
+    g = gen(100 + k + cin)
+    x = torch.randn(2, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    b = torch.randn(cout, generator=g)
+    sc = torch.rand(cin, generator=g) + 0.5
+    sh = torch.randn(cin, generator=g) * 0.1
+    slope = 0.2 if pro else 0.0
+    xi = x
+    if pro:
+        xi = F.leaky_relu(x * sc[None, :, None, None] + sh[None, :, None, None], slope)
+    if ups:
+        xi = F.interpolate(xi, scale_factor=2, mode="nearest")
+    ref = F.conv2d(xi, w, b, padding=k // 2)
+    d, xb, wk, _, shp = conv_setup(x, w, k, dtype, ups, pro, slope)
+    if cout % 4:
+        d.out_nchw_f32 = 1
+        y = torch.empty(shp, dtype=torch.float32, device="cuda")
+    else:
+        y = torch.empty(shp, dtype=dtype, device="cuda", memory_format=CL)
+    scd, shd = sc.cuda(), sh.cuda()
+    nb = L.query("fv_conv2d_stats_blocks", ctypes.byref(d))
+    part = torch.empty(nb * 2 * cout, device="cuda")
+    L.call("fv_conv2d_fwd", ctypes.byref(d), xb.data_ptr(), wk.data_ptr(), b.cuda().data_ptr(),
+           L.ptr(scd if pro else None), L.ptr(shd if pro else None), None, y.data_ptr(), part.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert rel(y.float(), ref) < TOL[dtype] * (1 if dtype == torch.float32 else 1.5)
+    # block partials -> exact batch statistics
+    if cout % 8 == 0:
+        stats = torch.empty(3 * cout, dtype=torch.float64, device="cuda")
+        ws = torch.empty(L.query("fv_bn_ws_bytes", cout) // 8, dtype=torch.float64, device="cuda")
+        P = shp[0] * shp[2] * shp[3]
+        L.call("fv_bn_stats_from_partials", part.data_ptr(), nb, L.query("fv_conv2d_stats_block_pixels",
+               ctypes.byref(d)), P, cout, stats.data_ptr(), ws.data_ptr(), L.stream())
+        s = stats.cpu().view(3, cout)
+        yr = y.float().cpu().permute(1, 0, 2, 3).reshape(cout, -1).double()
+        assert torch.allclose(s[0], torch.full((cout,), float(P), dtype=torch.float64))
+        assert rel(s[1], yr.sum(1)) < 1e-5
+        assert rel(s[2], (yr * yr).sum(1)) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_bwd(case, dtype):
+    k, cin, cout, H, W, ups, pro = case
+    g = gen(200 + k + cin)
+    x = torch.randn(2, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    sc = torch.rand(cin, generator=g) + 0.5
+    sh = torch.randn(cin, generator=g) * 0.1
+    slope = 0.0
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = torch.zeros(cout, requires_grad=True)
+    xi = xr
+    if pro:
+        xi = F.relu(xr * sc[None, :, None, None] + sh[None, :, None, None])
+    if ups:
+        xi = F.interpolate(xi, scale_factor=2, mode="nearest")
+    out = F.conv2d(xi, wr, br, padding=k // 2)
+    gy = torch.randn(out.shape, generator=g)
+    (out * gy).sum().backward()
+    d, xb, wk, wt, shp = conv_setup(x, w, k, dtype, ups, pro, slope, need_wt=True)
+    ldd = ops.pad_pow2(cout)
+    gyb = torch.zeros((2, ldd, shp[2], shp[3]), dtype=dtype, device="cuda", memory_format=CL)
+    gyb[:, :cout] = gy.cuda().to(dtype)
+    # weight + bias gradient
+    slab = torch.empty(L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), device="cuda")
+    ns = L.query("fv_conv2d_wgrad_nsplit", ctypes.byref(d))
+    bslab = torch.empty(ns * ((cout + 127) // 128) * 128, device="cuda")
+    scd, shd = sc.cuda(), sh.cuda()
+    L.call("fv_conv2d_bwd_weight", ctypes.byref(d), xb.data_ptr(), L.ptr(scd if pro else None),
+           L.ptr(shd if pro else None), gyb.data_ptr(), ldd, slab.data_ptr(), bslab.data_ptr(), L.stream())
+    dw = torch.empty(cout, cin, k, k, device="cuda")
+    db = torch.empty(cout, device="cuda")
+    L.call("fv_conv2d_wgrad_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(), dw.data_ptr(),
+           db.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    tol = TOL[dtype] * (1 if dtype == torch.float32 else 1.5)
+    assert rel(dw, wr.grad) < tol
+    assert rel(db, br.grad) < tol
+    # data gradient (w.r.t. the conv input, before the prologue)
+    if not pro:
+        dx = torch.empty((2, xb.shape[1], shp[2], shp[3]), dtype=dtype, device="cuda", memory_format=CL)
+        L.call("fv_conv2d_bwd_data", ctypes.byref(d), gyb.data_ptr(), ldd, wt.data_ptr(), dx.data_ptr(), L.stream())
+        if ups:
+            src = torch.empty((2, xb.shape[1], H, W), dtype=dtype, device="cuda", memory_format=CL)
+            L.call("fv_upsample2x_bwd", L.dtype_code(dtype), dx.data_ptr(), 2, H, W, xb.shape[1], src.data_ptr(),
+                   L.stream())
+            dx = src
+        torch.cuda.synchronize()
+        assert rel(dx[:, :cin].float(), xr.grad) < tol
+
+
+def test_spectral_norm():
+    g = gen(7)
+    w = torch.randn(64, 32, 3, 3, generator=g)
+    u = F.normalize(torch.randn(64, generator=g), dim=0)
+    v = F.normalize(torch.randn(288, generator=g), dim=0)
+    wm = w.reshape(64, -1)
+    v2 = F.normalize(wm.t() @ u, dim=0)
+    u2 = F.normalize(wm @ v2, dim=0)
+    sig = torch.dot(u2, wm @ v2)
+    wc, uc, vc = w.cuda(), u.cuda(), v.cuda()
+    sigma = ops.spectral_norm_fwd(wc, uc, vc, True)
+    torch.cuda.synchronize()
+    assert rel(uc, u2) < 1e-5 and rel(vc, v2) < 1e-5
+    assert abs(sigma.item() - sig.item()) < 1e-5 * sig.item()
+    # backward through W / sigma (u, v constants)
+    wr = w.clone().requires_grad_(True)
+    gsn = torch.randn(64, 32, 3, 3, generator=g)
+    (wr / torch.dot(u2, wr.reshape(64, -1) @ v2) * gsn).sum().backward()
+    gc = gsn.cuda().contiguous()
+    ops.spectral_norm_bwd(wc, gc, uc, vc, sigma)
+    torch.cuda.synchronize()
+    assert rel(gc, wr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_losses_and_reparam(dtype):
+    g = gen(11)
+    N, Lc, H = 2, 16, 8
+    h = torch.randn(N, 2 * Lc, H, H, generator=g) * 0.5
+    eps = torch.randn(N, Lc, H, H, generator=g)
+    hr = h.to(dtype).float().requires_grad_(True)
+    mu_r, ls_r = hr[:, :Lc], hr[:, Lc:]
+    z_r = mu_r + torch.exp(ls_r) * eps
+    K_r = torch.mean(-0.5 - ls_r + 0.5 * mu_r ** 2 + 0.5 * torch.exp(2 * ls_r), dim=-1).mean()
+    gz = torch.randn(z_r.shape, generator=g)
+    ((z_r * gz).sum() + 3.0 * K_r).backward()
+    hc = h.cuda().to(dtype).contiguous(memory_format=CL).requires_grad_(True)
+    mu, ls, z = ops.reparameterise(hc, eps.cuda(), dtype)
+    K = fv.KLDivergenceLoss()((mu, ls))
+    ((z.float() * gz.cuda()).sum() + 3.0 * K).backward()
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert rel(z.float(), z_r) < tol
+    assert abs(K.item() - K_r.item()) < tol * abs(K_r.item())
+    assert rel(hc.grad.float(), hr.grad) < tol * 2
+    # MSE / L1 on fp32 NCHW images
+    a = torch.rand(2, 3, 16, 16, generator=g)
+    b = torch.rand(2, 3, 16, 16, generator=g)
+    for fn_ours, fn_ref in ((fv.ReconLoss(), lambda p: F.mse_loss(p[0], p[1])),):
+        ar, br_ = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+        lr_ = fn_ref((ar, br_))
+        lr_.backward()
+        ac, bc = a.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+        lo = fn_ours((ac, bc))
+        lo.backward()
+        assert abs(lo.item() - lr_.item()) < 1e-6 * lr_.item()
+        assert rel(ac.grad, ar.grad) < 1e-6 and rel(bc.grad, br_.grad) < 1e-6
+    ar, br_ = a.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.l1_loss(ar, br_).backward()
+    ac, bc = a.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    lo = fv.L1Loss()(ac, bc)
+    lo.backward()
+    assert abs(lo.item() - F.l1_loss(a, b).item()) < 1e-6
+    assert rel(ac.grad, ar.grad) < 1e-6
+
+
+def test_adam_matches_torch():
+    g = gen(5)
+    ps = [torch.randn(s, generator=g) for s in (10, 5000, 4096 * 3 + 7)]
+    gs = [[torch.randn(p.shape, generator=g) for p in ps] for _ in range(3)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    ours = [p.cuda().requires_grad_(True) for p in ps]
+    o_ref = torch.optim.Adam(ref, lr=5e-3, betas=(0.5, 0.999))
+    o_ours = fv.Adam(ours, lr=5e-3, betas=(0.5, 0.999))
+    for step in range(3):
+        for p, gg in zip(ref, gs[step]):
+            p.grad = gg.clone()
+        for p, gg in zip(ours, gs[step]):
+            p.grad = gg.cuda()
+        o_ref.step()
+        o_ours.step()
+    torch.cuda.synchronize()
+    for a, b in zip(ours, ref):
+        assert rel(a.detach(), b.detach()) < 1e-6
+    sa, sb = o_ours.state_dict(), o_ref.state_dict()
+    assert sa["state"][1]["step"].item() == sb["state"][1]["step"].item() == 3
+    assert rel(sa["state"][2]["exp_avg_sq"], sb["state"][2]["exp_avg_sq"]) < 1e-6
+
+
+def test_error_is_reported_not_aborted():
+    d = ops.desc(torch.float32, 1, 8, 8, 12, 12, 16, 16, 3)    # cin 12 is not a power of two
+    with pytest.raises(L.FaceVAELibError, match="power of two"):
+        L.call("fv_conv2d_fwd", ctypes.byref(d), 1, 1, None, None, None, None, 1, None, L.stream())
