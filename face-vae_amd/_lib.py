@@ -76,7 +76,8 @@ _SIGS = {
     "fv_mse_bwd": (c_int, [P, P, c_long, P, P, P, P]),
     "fv_l1_fwd": (c_int, [P, P, c_long, P, P, P]),
     "fv_l1_bwd": (c_int, [P, P, c_long, P, P, P, P]),
-    "fv_adam_step": (c_int, [P, P, c_int, c_float, c_float, c_float, c_float, c_long, P]),
+    "fv_adam_step": (c_int, [P, P, c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                             c_long, P]),
     "fv_comm_unique_id": (c_int, [P]),
     "fv_comm_init": (c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
     "fv_comm_allreduce": (c_int, [c_void_p, P, c_size_t, c_int, c_int, P]),

@@ -363,7 +363,7 @@ conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         f[i] = acc[n][m][i];
-        if (a.sigmoid) f[i] = 1.f / (1.f + __expf(-f[i]));
+        if (a.sigmoid) f[i] = 1.f / (1.f + expf(-f[i]));
       }
       if (a.nchw) {
         float* yp = reinterpret_cast<float*>(a.y);

@@ -138,7 +138,7 @@ __global__ void reparam_fwd_kernel(const T* __restrict__ h, const float* __restr
     float fz[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      fz[j] = m.get(j) + __expf(s.get(j)) * eps[((long)n * L + cg * 8 + j) * HW + hw];
+      fz[j] = m.get(j) + expf(s.get(j)) * eps[((long)n * L + cg * 8 + j) * HW + hw];
     m.store(mu + p * L + cg * 8);
     s.store(ls + p * L + cg * 8);
     Chunk8<T> o;
@@ -167,7 +167,7 @@ __global__ void reparam_bwd_kernel(const T* __restrict__ h, const float* __restr
     for (int j = 0; j < 8; ++j) {
       const float ep = eps[((long)n * L + cg * 8 + j) * HW + hw];
       om[j] = gz.get(j) + gm.get(j);
-      os[j] = gz.get(j) * __expf(s.get(j)) * ep + gs.get(j);
+      os[j] = gz.get(j) * expf(s.get(j)) * ep + gs.get(j);
     }
     Chunk8<T> a, b;
     a.set8(om);
@@ -184,7 +184,7 @@ __global__ void loss_partial_kernel(const T* __restrict__ a, const T* __restrict
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float x = ldf(a, i), y = ldf(b, i);
     float v;
-    if constexpr (KIND == 0) v = -0.5f - y + 0.5f * x * x + 0.5f * __expf(2.f * y);
+    if constexpr (KIND == 0) v = -0.5f - y + 0.5f * x * x + 0.5f * expf(2.f * y);
     else if constexpr (KIND == 1) v = (x - y) * (x - y);
     else v = fabsf(x - y);
     acc += v;
@@ -221,7 +221,7 @@ __global__ void kl_bwd_kernel(const T* __restrict__ mu, const T* __restrict__ ls
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float m = ldf(mu, i), s = ldf(ls, i);
     if (dmu) dmu[i] = Elt<T>::from_f(g * m);
-    if (dls) dls[i] = Elt<T>::from_f(g * (__expf(2.f * s) - 1.f));
+    if (dls) dls[i] = Elt<T>::from_f(g * (expf(2.f * s) - 1.f));
   }
 }
 
@@ -336,8 +336,8 @@ __global__ void sn_bwd_apply_kernel(const float* __restrict__ g, int rows, int c
 }
 
 // ------------------------------------------------------------------------------ Adam
-__global__ void adam_kernel(const fv_adam_tensor* __restrict__ ts, const int* __restrict__ blocks, float lr,
-                            float b1, float b2, float eps, float step_size, float bc2_sqrt) {
+__global__ void adam_kernel(const fv_adam_tensor* __restrict__ ts, const int* __restrict__ blocks, float omb1,
+                            float b2, float omb2, float eps, float step_size, float bc2_sqrt) {
   const int t = blocks[2 * blockIdx.x], ch = blocks[2 * blockIdx.x + 1];
   const fv_adam_tensor d = ts[t];
   const long base = (long)ch * FV_ADAM_CHUNK;
@@ -345,8 +345,8 @@ __global__ void adam_kernel(const fv_adam_tensor* __restrict__ ts, const int* __
   for (long i = base + threadIdx.x; i < end; i += NTH) {
     const float g = d.grad[i];
     float m = d.exp_avg[i], v = d.exp_avg_sq[i];
-    m = m + (1.f - b1) * (g - m);
-    v = v * b2 + (1.f - b2) * g * g;
+    m = m + omb1 * (g - m);                 // exp_avg.lerp_(grad, 1 - beta1)
+    v = v * b2 + omb2 * g * g;              // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
     d.exp_avg[i] = m;
     d.exp_avg_sq[i] = v;
     const float denom = sqrtf(v) / bc2_sqrt + eps;
@@ -550,13 +550,15 @@ int fv_spectral_norm_bwd(const float* w, const float* g_sn, int rows, int cols, 
   return fv_check_launch("sn_bwd");
 }
 
-int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, float lr, float beta1, float beta2,
-                 float eps, long step, void* stream) {
+int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, double lr, double beta1,
+                 double beta2, double eps, long step, void* stream) {
   FV_REQUIRE(tensors && blocks && nblocks > 0 && step > 0, "adam: bad args");
-  const double bc1 = 1.0 - pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - pow((double)beta2, (double)step);
-  hipLaunchKernelGGL(adam_kernel, dim3(nblocks), dim3(NTH), 0, (hipStream_t)stream, tensors, blocks, lr, beta1, beta2,
-                     eps, (float)(lr / bc1), (float)sqrt(bc2));
+  // scalar coefficients in double on the host, as torch.optim.Adam computes them in Python
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel, dim3(nblocks), dim3(NTH), 0, (hipStream_t)stream, tensors, blocks,
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, (float)(lr / bc1),
+                     (float)sqrt(bc2));
   return fv_check_launch("adam");
 }
 

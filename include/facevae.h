@@ -195,8 +195,8 @@ typedef struct fv_adam_tensor {
 /* multi-tensor Adam (torch.optim.Adam math, no weight decay / amsgrad).  `tensors` is a
  * DEVICE array of descriptors; `blocks` a DEVICE array of nblocks (tensor, chunk) int pairs,
  * one per FV_ADAM_CHUNK elements of each tensor; `step` is the step count after increment. */
-int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, float lr,
-                 float beta1, float beta2, float eps, long step, void* stream);
+int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, double lr,
+                 double beta1, double beta2, double eps, long step, void* stream);
 
 /* ------------------------------------------------------------ communication ---- */
 typedef void* fv_comm_t;

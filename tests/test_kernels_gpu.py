@@ -91,10 +91,12 @@ def test_conv_fwd(case, dtype):
         L.call("fv_bn_stats_from_partials", part.data_ptr(), nb, L.query("fv_conv2d_stats_block_pixels",
                ctypes.byref(d)), P, cout, stats.data_ptr(), ws.data_ptr(), L.stream())
         s = stats.cpu().view(3, cout)
-        yr = y.float().cpu().permute(1, 0, 2, 3).reshape(cout, -1).double()
+        # statistics come from the fp32 accumulators (before the bf16 rounding of y)
+        yr = ref.permute(1, 0, 2, 3).reshape(cout, -1).double()
         assert torch.allclose(s[0], torch.full((cout,), float(P), dtype=torch.float64))
-        assert rel(s[1], yr.sum(1)) < 1e-5
-        assert rel(s[2], (yr * yr).sum(1)) < 1e-5
+        t = 1e-5 if dtype == torch.float32 else 1e-2
+        assert ((s[1] - yr.sum(1)).abs() / yr.abs().sum(1)).max() < t
+        assert rel(s[2], (yr * yr).sum(1)) < t
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -120,7 +122,7 @@ def test_conv_bwd(case, dtype):
     (out * gy).sum().backward()
     d, xb, wk, wt, shp = conv_setup(x, w, k, dtype, ups, pro, slope, need_wt=True)
     ldd = ops.pad_pow2(cout)
-    gyb = torch.zeros((2, ldd, shp[2], shp[3]), dtype=dtype, device="cuda", memory_format=CL)
+    gyb = torch.zeros((2, ldd, shp[2], shp[3]), dtype=dtype, device="cuda").contiguous(memory_format=CL)
     gyb[:, :cout] = gy.cuda().to(dtype)
     # weight + bias gradient
     slab = torch.empty(L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), device="cuda")
@@ -180,13 +182,13 @@ def test_losses_and_reparam(dtype):
     N, Lc, H = 2, 16, 8
     h = torch.randn(N, 2 * Lc, H, H, generator=g) * 0.5
     eps = torch.randn(N, Lc, H, H, generator=g)
-    hr = h.to(dtype).float().requires_grad_(True)
+    hr = h.to(dtype).float().clone().requires_grad_(True)
     mu_r, ls_r = hr[:, :Lc], hr[:, Lc:]
     z_r = mu_r + torch.exp(ls_r) * eps
     K_r = torch.mean(-0.5 - ls_r + 0.5 * mu_r ** 2 + 0.5 * torch.exp(2 * ls_r), dim=-1).mean()
     gz = torch.randn(z_r.shape, generator=g)
     ((z_r * gz).sum() + 3.0 * K_r).backward()
-    hc = h.cuda().to(dtype).contiguous(memory_format=CL).requires_grad_(True)
+    hc = h.detach().cuda().to(dtype).contiguous(memory_format=CL).requires_grad_(True)
     mu, ls, z = ops.reparameterise(hc, eps.cuda(), dtype)
     K = fv.KLDivergenceLoss()((mu, ls))
     ((z.float() * gz.cuda()).sum() + 3.0 * K).backward()

@@ -57,7 +57,9 @@ def test_block_matches_reference(name, dtype):
     named = dict(m.named_parameters())
     for k, g in c["grads"].items():
         if k.endswith("bias") and (g.abs().max() < 1e-4):      # dead bias before a BN
-            assert (named[k].grad.cpu() - g).abs().max() < 1e-3
+            # its gradient is rounding noise of sum(dy): ~1e-6 in fp32,
+            # ~1e-2..1e-1 with bf16-stored dy; it cannot affect any output
+            assert (named[k].grad.cpu() - g).abs().max() < (1e-3 if dtype == torch.float32 else 0.5)
         else:
             assert rel(named[k].grad, g) < tol * 2, k
     sd = m.state_dict()
