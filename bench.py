@@ -105,7 +105,7 @@ def main():
     res_c = cfg.up_seq[0]
 
     def is_res(kind, d):
-        return d.ksize == 3 and d.pro_act == 1 and d.cin_valid == res_c and d.cout == res_c
+        return d.ksize == 3 and d.cin_valid == res_c and d.cout == res_c and d.h == cfg.latent_hw
 
     timer = ops.KernelTimer(is_res)
     ops.TIMER = timer

@@ -11,8 +11,18 @@
 
 namespace {
 
-constexpr int NSPLIT = 128;  // pixel splits of the streaming reductions
+constexpr int NSPLIT = 128;   // level-1 splits of the conv-partials reduction
+constexpr int MAXBLK = 1024;  // max blocks (= level-1 records) of the streaming reductions
 constexpr int NTH = 256;
+
+// blocks of a streaming per-channel reduction over `pixels` x (C/8) chunks: >= 8 chunks per thread
+int stream_blocks(long pixels, int C) {
+  const long work = pixels * (C / 8);
+  long b = (work + NTH * 8 - 1) / (NTH * 8);
+  if (b < 1) b = 1;
+  if (b > MAXBLK) b = MAXBLK;
+  return (int)b;
+}
 
 template <typename T>
 __device__ __forceinline__ void ld8(const T* p, float* f) {
@@ -60,59 +70,61 @@ __global__ void partials_kernel(const float* __restrict__ part, int nb, int bpix
   }
 }
 
-// streaming statistics of x [P][ldc] -> ws [split][3][C]
+// streaming statistics of x [P][ldc] -> ws [block][3][C]; thread = (pixel row, 8-channel group)
 template <typename T>
 __global__ void tensor_stats_kernel(const T* __restrict__ x, long P, int C, int ldc, double* ws) {
-  const int tpp = C / 8;                 // threads per pixel (C % 8 == 0, C <= 8*NTH)
+  const int tpp = C / 8;                 // threads per pixel (NTH % tpp == 0)
   const int rows = NTH / tpp;
   const int cg = threadIdx.x % tpp, row = threadIdx.x / tpp;
-  const long per = (P + gridDim.x - 1) / gridDim.x;
-  const long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  double s[8], q[8];
+  float s[8], q[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0;
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
   long cnt = 0;
-  if (row < rows) {
-    for (long p = p0 + row; p < p1; p += rows) {
-      float f[8];
-      ld8<T>(x + p * ldc + cg * 8, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s[j] += f[j];
-        q[j] += (double)f[j] * f[j];
-      }
-      ++cnt;
-    }
-  }
-  extern __shared__ double sh[];   // [rows][C] x2
-  double* ss = sh;
-  double* sq = sh + (long)rows * C;
-  if (row < rows) {
+  for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
+    float f[8];
+    ld8<T>(x + p * ldc + cg * 8, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      ss[row * C + cg * 8 + j] = s[j];
-      sq[row * C + cg * 8 + j] = q[j];
+      s[j] += f[j];
+      q[j] += f[j] * f[j];
     }
+    ++cnt;
   }
+  __shared__ float ss[2][NTH * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ss[0][row * C + cg * 8 + j] = s[j];
+    ss[1][row * C + cg * 8 + j] = q[j];
+  }
+  __shared__ long cn[NTH];
+  cn[threadIdx.x] = cnt;
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += NTH) {
     double a = 0, b = 0;
+    long n = 0;
     for (int r = 0; r < rows; ++r) {
-      a += ss[r * C + c];
-      b += sq[r * C + c];
+      a += ss[0][r * C + c];
+      b += ss[1][r * C + c];
+      n += cn[r * tpp];
     }
-    ws[((long)blockIdx.x * 3 + 0) * C + c] = (double)(p1 > p0 ? p1 - p0 : 0);
+    ws[((long)blockIdx.x * 3 + 0) * C + c] = (double)n;
     ws[((long)blockIdx.x * 3 + 1) * C + c] = a;
     ws[((long)blockIdx.x * 3 + 2) * C + c] = b;
   }
 }
 
+// out[i] = sum_s ws[s][i], i < rec*C : 64 outputs x 4 lanes per block
 __global__ void sum_splits_kernel(const double* ws, int nsplit, int rec, int C, double* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= rec * C) return;
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane4 = threadIdx.x >> 6;
+  const int n = rec * C;
   double t = 0;
-  for (int s = 0; s < nsplit; ++s) t += ws[(long)s * rec * C + i];
-  out[i] = t;
+  if (i < n)
+    for (int s = lane4; s < nsplit; s += 4) t += ws[(long)s * n + i];
+  __shared__ double sh[4][64];
+  sh[lane4][threadIdx.x & 63] = t;
+  __syncthreads();
+  if (lane4 == 0 && i < n) out[i] = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
 }
 
 __global__ void finalize_kernel(const double* stats, int C, const float* gamma, const float* beta,
@@ -216,41 +228,33 @@ __global__ void act_bwd_reduce_kernel(const T* __restrict__ dout, const T* __res
   const int rows = NTH / tpp;
   const int cg = threadIdx.x % tpp, row = threadIdx.x / tpp;
   const long P = (long)N * H * W;
-  const long per = (P + gridDim.x - 1) / gridDim.x;
-  const long p0 = blockIdx.x * per, p1 = min(P, p0 + per);
-  double s[8], q[8];
+  float s[8], q[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0;
-  if (row < rows) {
-    for (long p = p0 + row; p < p1; p += rows) {
-      const int n = (int)(p / ((long)H * W));
-      const int rem = (int)(p - (long)n * H * W);
-      const int h = rem / W, w = rem - h * W;
-      float g[8], yh[8];
-      grad_g<T>(dout, y, p, n, h, w, H, W, C, ldc, cg * 8, pool, mean, invstd, gamma, beta, slope, g, yh);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s[j] += g[j];
-        q[j] += (double)g[j] * yh[j];
-      }
-    }
-  }
-  extern __shared__ double sh[];
-  double* ss = sh;
-  double* sq = sh + (long)rows * C;
-  if (row < rows) {
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
+    const int n = (int)(p / ((long)H * W));
+    const int rem = (int)(p - (long)n * H * W);
+    const int h = rem / W, w = rem - h * W;
+    float g[8], yh[8];
+    grad_g<T>(dout, y, p, n, h, w, H, W, C, ldc, cg * 8, pool, mean, invstd, gamma, beta, slope, g, yh);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      ss[row * C + cg * 8 + j] = s[j];
-      sq[row * C + cg * 8 + j] = q[j];
+      s[j] += g[j];
+      q[j] += g[j] * yh[j];
     }
+  }
+  __shared__ float ss[2][NTH * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ss[0][row * C + cg * 8 + j] = s[j];
+    ss[1][row * C + cg * 8 + j] = q[j];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += NTH) {
     double a = 0, b = 0;
     for (int r = 0; r < rows; ++r) {
-      a += ss[r * C + c];
-      b += sq[r * C + c];
+      a += ss[0][r * C + c];
+      b += ss[1][r * C + c];
     }
     ws[((long)blockIdx.x * 2 + 0) * C + c] = a;
     ws[((long)blockIdx.x * 2 + 1) * C + c] = b;
@@ -303,7 +307,8 @@ int grid_for(long work, int cap = 8192) {
 }
 
 int check_c(int c, int ldc) {
-  FV_REQUIRE(c > 0 && c % 8 == 0 && c <= 8 * NTH, "bn: channels must be a multiple of 8 <= 2048 (got %d)", c);
+  FV_REQUIRE(c > 0 && c % 8 == 0 && c <= 8 * NTH && NTH % (c / 8) == 0,
+             "bn: channels must be 8 * a power of two <= 2048 (got %d)", c);
   FV_REQUIRE(ldc >= c && ldc % 8 == 0, "bn: bad channel stride %d", ldc);
   return FV_OK;
 }
@@ -312,7 +317,7 @@ int check_c(int c, int ldc) {
 
 extern "C" {
 
-size_t fv_bn_ws_bytes(int c) { return (size_t)NSPLIT * 3 * c * sizeof(double); }
+size_t fv_bn_ws_bytes(int c) { return (size_t)MAXBLK * 3 * c * sizeof(double); }
 
 int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixels, long total_pixels,
                               int c, double* stats, void* ws, void* stream) {
@@ -323,7 +328,7 @@ int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixe
                      block_pixels, total_pixels, c, (double*)ws);
   int st = fv_check_launch("bn_partials");
   if (st) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, NTH)), dim3(NTH), 0, s, (const double*)ws, NSPLIT,
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 64)), dim3(NTH), 0, s, (const double*)ws, NSPLIT,
                      3, c, stats);
   return fv_check_launch("bn_sum_splits");
 }
@@ -334,17 +339,16 @@ int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, do
   if (st) return st;
   FV_REQUIRE(x && stats && ws, "null pointer");
   hipStream_t s = (hipStream_t)stream;
-  const int rows = NTH / (c / 8);
-  const size_t shm = 2 * (size_t)rows * c * sizeof(double);
+  const int nb = stream_blocks(pixels, c);
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(tensor_stats_kernel<bf16>, dim3(NSPLIT), dim3(NTH), shm, s, (const bf16*)x, pixels, c, ldc,
+    hipLaunchKernelGGL(tensor_stats_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)x, pixels, c, ldc,
                        (double*)ws);
   else
-    hipLaunchKernelGGL(tensor_stats_kernel<float>, dim3(NSPLIT), dim3(NTH), shm, s, (const float*)x, pixels, c,
-                       ldc, (double*)ws);
+    hipLaunchKernelGGL(tensor_stats_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)x, pixels, c, ldc,
+                       (double*)ws);
   if ((st = fv_check_launch("bn_tensor_stats"))) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, NTH)), dim3(NTH), 0, s, (const double*)ws, NSPLIT,
-                     3, c, stats);
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 64)), dim3(NTH), 0, s, (const double*)ws, nb, 3, c,
+                     stats);
   return fv_check_launch("bn_sum_splits");
 }
 
@@ -383,17 +387,16 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
   if (st) return st;
   FV_REQUIRE(!pool || ldc == c, "pooled bwd needs dense channels");
   hipStream_t s = (hipStream_t)stream;
-  const int rows = NTH / (c / 8);
-  const size_t shm = 2 * (size_t)rows * c * sizeof(double);
+  const int nb = stream_blocks((long)n * h * w, c);
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(NSPLIT), dim3(NTH), shm, s, (const bf16*)dout,
+    hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
                        (const bf16*)y, n, h, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   else
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(NSPLIT), dim3(NTH), shm, s, (const float*)dout,
+    hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
                        (const float*)y, n, h, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, NTH)), dim3(NTH), 0, s, (const double*)ws, NSPLIT,
-                     2, c, red);
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, 64)), dim3(NTH), 0, s, (const double*)ws, nb, 2, c,
+                     red);
   return fv_check_launch("bn_sum_splits");
 }
 

@@ -12,6 +12,8 @@
 //   (cols = pixels).  The accumulator layout then gives each lane 4 consecutive output
 //   channels of one pixel -> contiguous NHWC stores.  K = (tap, ci), ci fastest, chunks
 //   of 8 k never straddle a tap (cin is a power of two >= 8).
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "common.h"
@@ -97,6 +99,152 @@ __device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b,
 #pragma unroll
   for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], c, 0, 0, 0);
   return c;
+}
+
+// shared epilogue: bias [+ residual] -> BN partials -> [sigmoid] -> store (NHWC T or NCHW f32)
+template <typename T, int WN, int WM, int RN, int RM>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN][RM], char* smem, int co0, int p0,
+                                              int tm, int wn, int wm, int lane, int tid) {
+  constexpr int NT = 64 * WN * WM;
+  constexpr int BN = WN * RN * 16;
+  constexpr int BM = WM * RM * 16;
+  const int HW = a.H * a.W;
+  const int lr = lane & 15, lh = lane >> 4;
+  float bv[RN][4];
+#pragma unroll
+  for (int n = 0; n < RN; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co0 + wn * RN * 16 + n * 16 + lh * 4 + i;
+      bv[n][i] = (a.bias && co < a.Cout) ? a.bias[co] : 0.f;
+    }
+  bool pv[RM];
+  int pix_of[RM];
+#pragma unroll
+  for (int m = 0; m < RM; ++m) {
+    pix_of[m] = p0 + wm * RM * 16 + m * 16 + lr;
+    pv[m] = pix_of[m] < a.P;
+  }
+#pragma unroll
+  for (int n = 0; n < RN; ++n) {
+    const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[n][m][i] += bv[n][i];
+      if (a.res && pv[m]) {
+        const T* rp = reinterpret_cast<const T*>(a.res) + (long)pix_of[m] * a.ldy + cb;
+        if (cb + 3 < a.Cout) {
+          float f[4];
+          load4<T>(rp, f);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[n][m][i] += f[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (cb + i < a.Cout) acc[n][m][i] += Elt<T>::to_f(rp[i]);
+        }
+      }
+    }
+  }
+
+  if (a.stats) {
+    // per-block (sum, centred M2) per output channel; rows of this block = valid pixels
+    float* red = reinterpret_cast<float*>(smem);        // [WM][BN]
+    float* meanv = red + WM * BN;                         // [BN]
+    const int cnt = min(BM, a.P - p0);
+    float s[RN][4];
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < RM; ++m) t += pv[m] ? acc[n][m][i] : 0.f;
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        s[n][i] = t;
+      }
+    if (lr == 0) {
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float S = 0.f;
+#pragma unroll
+      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
+      meanv[c] = S / (float)cnt;
+      if (co0 + c < a.Cout) a.stats[(long)(tm * 2) * a.Cout + co0 + c] = S;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float mu = meanv[wn * RN * 16 + n * 16 + lh * 4 + i];
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < RM; ++m) {
+          const float d = acc[n][m][i] - mu;
+          t += pv[m] ? d * d : 0.f;
+        }
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        s[n][i] = t;
+      }
+    __syncthreads();
+    if (lr == 0) {
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float S = 0.f;
+#pragma unroll
+      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
+      if (co0 + c < a.Cout) a.stats[(long)(tm * 2 + 1) * a.Cout + co0 + c] = S;
+    }
+  }
+
+#pragma unroll
+  for (int n = 0; n < RN; ++n) {
+    const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      if (!pv[m]) continue;
+      float f[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f[i] = acc[n][m][i];
+        if (a.sigmoid) f[i] = 1.f / (1.f + expf(-f[i]));
+      }
+      if (a.nchw) {
+        float* yp = reinterpret_cast<float*>(a.y);
+        const int img = pix_of[m] / HW, hw = pix_of[m] - img * HW;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (cb + i < a.Cout) yp[((long)img * a.Cout + cb + i) * HW + hw] = f[i];
+      } else {
+        T* yp = reinterpret_cast<T*>(a.y) + (long)pix_of[m] * a.ldy + cb;
+        if (cb + 3 < a.Cout) {
+          store4<T>(yp, f);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (cb + i < a.Cout) yp[i] = Elt<T>::from_f(f[i]);
+        }
+      }
+    }
+  }
 }
 
 template <typename T, int KS, int WN, int WM, int RN, int RM, bool PRO, bool UPS>
@@ -247,142 +395,140 @@ conv_fwd_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ------------------------------------------------------------------ epilogue
-  float bv[RN][4];
+  conv_epilogue<T, WN, WM, RN, RM>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+}
+
+// ----------------------------------------------------------------------------------------
+// v2 forward (bf16, cin % 64 == 0): both operands land in LDS by DMA (buffer/global_load
+// ... lds, no VGPR staging, no ds_write), BK = 64 (one tap x 64 channels per step), 128-B
+// rows XOR-swizzled through the SOURCE address (the DMA destination is lane-linear),
+// double-buffered with one barrier per step.  Zero padding comes from the buffer range
+// check: an out-of-image tap gets voffset >= num_records and the hardware returns 0.
+// ----------------------------------------------------------------------------------------
+constexpr int BK2 = 64;
+__device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int KS, int WN, int WM, int RN, int RM, bool UPS>
+__global__ void __launch_bounds__(64 * WN * WM, 2)
+conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
+  constexpr int NW = WN * WM;
+  constexpr int BN = WN * RN * 16, BM = WM * RM * 16;
+  constexpr int PAD = KS / 2;
+  constexpr int ROWB = BK2 * 2;
+  constexpr int QA = BM / 8, QB = BN / 8;            // 1-KB DMA pieces per stage
+  constexpr int JA = (QA + NW - 1) / NW, JB = (QB + NW - 1) / NW;
+  constexpr int STAGE = (BM + BN) * ROWB;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const bf16* __restrict__ wk = reinterpret_cast<const bf16*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  // XCD-aware tile order: blocks b, b+8, ... share an XCD (observed round-robin dispatch);
+  // give each XCD a contiguous run of logical tiles (co tiles of a pixel tile, then its
+  // neighbours, which share halo rows).  Bijective for any grid size.  Speed only.
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tn = lid % a.ntn, tm = lid / a.ntn;
+  const int co0 = tn * BN, p0 = tm * BM;
+  const int HW = a.H * a.W;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const int lrow = lane >> 3, lchk = lane & 7;
+  int rh[JA], rw[JA], rb[JA];
+  bool rv[JA];
+#pragma unroll
+  for (int j = 0; j < JA; ++j) {
+    const int q = wave + j * NW;
+    const int pix = p0 + q * 8 + lrow;
+    rv[j] = q < QA && pix < a.P;
+    const int n = pix / HW, rem = pix - (pix / HW) * HW;
+    rh[j] = rem / a.W;
+    rw[j] = rem - rh[j] * a.W;
+    rb[j] = n * a.Hin * a.Win;
+  }
+
+  auto issue = [&](int ks, int buf) {
+    const int k0 = ks * BK2;
+    const int tap = k0 >> a.lgCin, ci0 = k0 & (a.Cin - 1);
+    const int r = tap / KS, s = tap - (tap / KS) * KS;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + BM * ROWB;
+#pragma unroll
+    for (int j = 0; j < JA; ++j) {
+      const int q = wave + j * NW;
+      if (QA % NW == 0 || q < QA) {
+        const int row = q * 8 + lrow;
+        const int ci = ci0 + ((lchk ^ swz8(row)) << 3);
+        const int hh = rh[j] + r - PAD, ww = rw[j] + s - PAD;
+        bool ok = rv[j];
+        int hs, ws;
+        if constexpr (UPS) {
+          ok = ok && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          hs = hh >> 1;
+          ws = ww >> 1;
+        } else {
+          ok = ok && hh >= 0 && hh < a.Hin && ww >= 0 && ww < a.Win;
+          hs = hh;
+          ws = ww;
+        }
+        const unsigned off = ok ? ((unsigned)((rb[j] + hs * a.Win + ws) << a.lgCin) + (unsigned)ci) * 2u : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(As + q * 1024), 16, off, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int q = wave + j * NW;
+      if (QB % NW == 0 || q < QB) {
+        const int row = q * 8 + lrow;
+        const bf16* src = wk + (long)(co0 + row) * a.Kpad + k0 + ((lchk ^ swz8(row)) << 3);
+        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(Bs + q * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[RN][RM];
 #pragma unroll
   for (int n = 0; n < RN; ++n)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + wn * RN * 16 + n * 16 + lh * 4 + i;
-      bv[n][i] = (a.bias && co < a.Cout) ? a.bias[co] : 0.f;
-    }
-  bool pv[RM];
-  int pix_of[RM];
-#pragma unroll
-  for (int m = 0; m < RM; ++m) {
-    pix_of[m] = p0 + wm * RM * 16 + m * 16 + lr;
-    pv[m] = pix_of[m] < a.P;
-  }
-#pragma unroll
-  for (int n = 0; n < RN; ++n) {
-    const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
-#pragma unroll
-    for (int m = 0; m < RM; ++m) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[n][m][i] += bv[n][i];
-      if (a.res && pv[m]) {
-        const T* rp = reinterpret_cast<const T*>(a.res) + (long)pix_of[m] * a.ldy + cb;
-        if (cb + 3 < a.Cout) {
-          float f[4];
-          load4<T>(rp, f);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[n][m][i] += f[i];
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (cb + i < a.Cout) acc[n][m][i] += Elt<T>::to_f(rp[i]);
-        }
-      }
-    }
-  }
+    for (int m = 0; m < RM; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (a.stats) {
-    // per-block (sum, centred M2) per output channel; rows of this block = valid pixels
-    float* red = reinterpret_cast<float*>(smem);        // [WM][BN]
-    float* meanv = red + WM * BN;                         // [BN]
-    const int cnt = min(BM, a.P - p0);
-    float s[RN][4];
+  const int lr = lane & 15, lh = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * ROWB;
 #pragma unroll
-    for (int n = 0; n < RN; ++n)
+    for (int kk = 0; kk < 2; ++kk) {
+      Frag<bf16> af[RN], bfm[RM];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float t = 0.f;
-#pragma unroll
-        for (int m = 0; m < RM; ++m) t += pv[m] ? acc[n][m][i] : 0.f;
-        t += __shfl_xor(t, 1, 64);
-        t += __shfl_xor(t, 2, 64);
-        t += __shfl_xor(t, 4, 64);
-        t += __shfl_xor(t, 8, 64);
-        s[n][i] = t;
+      for (int n = 0; n < RN; ++n) {
+        const int row = wn * RN * 16 + n * 16 + lr;
+        af[n].lds(Bs + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
       }
-    if (lr == 0) {
+#pragma unroll
+      for (int m = 0; m < RM; ++m) {
+        const int row = wm * RM * 16 + m * 16 + lr;
+        bfm[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
+      }
 #pragma unroll
       for (int n = 0; n < RN; ++n)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
+        for (int m = 0; m < RM; ++m) acc[n][m] = mma(af[n], bfm[m], acc[n][m]);
     }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float S = 0.f;
-#pragma unroll
-      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
-      meanv[c] = S / (float)cnt;
-      if (co0 + c < a.Cout) a.stats[(long)(tm * 2) * a.Cout + co0 + c] = S;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < RN; ++n)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float mu = meanv[wn * RN * 16 + n * 16 + lh * 4 + i];
-        float t = 0.f;
-#pragma unroll
-        for (int m = 0; m < RM; ++m) {
-          const float d = acc[n][m][i] - mu;
-          t += pv[m] ? d * d : 0.f;
-        }
-        t += __shfl_xor(t, 1, 64);
-        t += __shfl_xor(t, 2, 64);
-        t += __shfl_xor(t, 4, 64);
-        t += __shfl_xor(t, 8, 64);
-        s[n][i] = t;
-      }
-    __syncthreads();
-    if (lr == 0) {
-#pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float S = 0.f;
-#pragma unroll
-      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
-      if (co0 + c < a.Cout) a.stats[(long)(tm * 2 + 1) * a.Cout + co0 + c] = S;
-    }
-  }
+  };
 
-#pragma unroll
-  for (int n = 0; n < RN; ++n) {
-    const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
-#pragma unroll
-    for (int m = 0; m < RM; ++m) {
-      if (!pv[m]) continue;
-      float f[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f[i] = acc[n][m][i];
-        if (a.sigmoid) f[i] = 1.f / (1.f + expf(-f[i]));
-      }
-      if (a.nchw) {
-        float* yp = reinterpret_cast<float*>(a.y);
-        const int img = pix_of[m] / HW, hw = pix_of[m] - img * HW;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (cb + i < a.Cout) yp[((long)img * a.Cout + cb + i) * HW + hw] = f[i];
-      } else {
-        T* yp = reinterpret_cast<T*>(a.y) + (long)pix_of[m] * a.ldy + cb;
-        if (cb + 3 < a.Cout) {
-          store4<T>(yp, f);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (cb + i < a.Cout) yp[i] = Elt<T>::from_f(f[i]);
-        }
-      }
-    }
+  issue(0, 0);
+  for (int ks = 0; ks < a.nks; ++ks) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (ks + 1 < a.nks) issue(ks + 1, (ks + 1) & 1);
+    compute(ks & 1);
   }
+  __syncthreads();
+  conv_epilogue<bf16, WN, WM, RN, RM>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -722,6 +868,53 @@ int launch_fwd(const ConvArgs& a, int ks, FwdTile t, int pro, int ups, int nblk,
   return FV_E_UNSUPPORTED;
 }
 
+// v2 (DMA-fed bf16) path: bf16, no BN prologue, cin a multiple of 64, input < 2 GB
+static int g_disable_v2 = -1;
+bool use_v2(const fv_conv_desc* d) {
+  if (g_disable_v2 < 0) {
+    const char* e = getenv("FV_DISABLE_V2");
+    g_disable_v2 = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_disable_v2) return false;
+  if (d->dtype != FV_BF16 || d->pro_act || d->cin % 64) return false;
+  const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
+  return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
+}
+
+FwdTile fwd_tile_v2(int rows_needed) {
+  if (rows_needed > 64) return {128, 128};
+  if (rows_needed > 16) return {64, 256};
+  return {16, 256};
+}
+
+template <int KS, int WN, int WM, int RN, int RM>
+int launch_v2_t(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s) {
+  dim3 g(nblk), b(64 * WN * WM);
+  if (ups) {
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, true>), g, b, 0, s, a, xb);
+    else return FV_E_UNSUPPORTED;
+  } else {
+    hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, false>), g, b, 0, s, a, xb);
+  }
+  return FV_OK;
+}
+
+template <int KS>
+int launch_v2_ks(const ConvArgs& a, FwdTile t, int ups, int nblk, unsigned xb, hipStream_t s) {
+  if (t.bn == 128) return launch_v2_t<KS, 2, 2, 4, 4>(a, ups, nblk, xb, s);
+  if (t.bn == 64) return launch_v2_t<KS, 1, 4, 4, 4>(a, ups, nblk, xb, s);
+  return launch_v2_t<KS, 1, 4, 1, 4>(a, ups, nblk, xb, s);
+}
+
+int launch_v2(const ConvArgs& a, int ks, FwdTile t, int ups, int nblk, unsigned xb, hipStream_t s) {
+  switch (ks) {
+    case 1: return launch_v2_ks<1>(a, t, ups, nblk, xb, s);
+    case 3: return launch_v2_ks<3>(a, t, ups, nblk, xb, s);
+    case 7: return launch_v2_ks<7>(a, t, ups, nblk, xb, s);
+  }
+  return FV_E_UNSUPPORTED;
+}
+
 int check_desc(const fv_conv_desc* d) {
   FV_REQUIRE(d, "null conv descriptor");
   FV_REQUIRE(d->dtype == FV_F32 || d->dtype == FV_BF16, "conv dtype must be f32 or bf16");
@@ -752,7 +945,7 @@ int wg_nsplit(const fv_conv_desc* d) {
   const int ntk = fv_cdiv(K, t.bkt), ntc = fv_cdiv(d->cout, t.bc);
   const long P = (long)d->n * d->h * d->w;
   const int nsteps = fv_cdiv(P, 32);
-  int ns = 2048 / (ntk * ntc);
+  int ns = 768 / (ntk * ntc);
   if (ns < 1) ns = 1;
   if (ns > nsteps) ns = nsteps;
   const int per = fv_cdiv(nsteps, ns);
@@ -811,11 +1004,13 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   return (size_t)fv_cdiv(d->cin, t.bn) * t.bn * kpad_of(d->ksize, cin_t);
 }
 
-int fv_conv2d_stats_block_pixels(const fv_conv_desc* d) { return fwd_tile(d->cout).bm; }
+static FwdTile plan_tile(const fv_conv_desc* d) { return use_v2(d) ? fwd_tile_v2(d->cout) : fwd_tile(d->cout); }
+
+int fv_conv2d_stats_block_pixels(const fv_conv_desc* d) { return plan_tile(d).bm; }
 
 int fv_conv2d_stats_blocks(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
-  return fv_cdiv((long)d->n * d->h * d->w, fwd_tile(d->cout).bm);
+  return fv_cdiv((long)d->n * d->h * d->w, plan_tile(d).bm);
 }
 
 int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma, void* wk,
@@ -870,9 +1065,23 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   a.K = d->ksize * d->ksize * d->cin; a.Kpad = kpad_of(d->ksize, d->cin); a.nks = a.Kpad / BK;
   a.sigmoid = d->epi_sigmoid; a.nchw = d->out_nchw_f32;
   a.ntn = fv_cdiv(d->cout, t.bn);
+  int st;
+  if (use_v2(d)) {
+    const FwdTile t2 = fwd_tile_v2(d->cout);
+    a.ntn = fv_cdiv(d->cout, t2.bn);
+    a.nks = a.Kpad / BK2;
+    const int nblk2 = a.ntn * fv_cdiv(a.P, t2.bm);
+    const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
+    st = launch_v2(a, d->ksize, t2, d->upsample, nblk2, (unsigned)xb, s);
+    if (st) {
+      fv_set_error("conv v2 variant unsupported (k=%d ups=%d)", d->ksize, d->upsample);
+      return st;
+    }
+    return fv_check_launch("conv2d_fwd_v2");
+  }
   const int nblk = a.ntn * fv_cdiv(a.P, t.bm);
-  int st = d->dtype == FV_BF16 ? launch_fwd<bf16>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s)
-                               : launch_fwd<float>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s);
+  st = d->dtype == FV_BF16 ? launch_fwd<bf16>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s)
+                           : launch_fwd<float>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s);
   if (st) {
     fv_set_error("conv variant unsupported (k=%d pro=%d ups=%d)", d->ksize, d->pro_act, d->upsample);
     return st;

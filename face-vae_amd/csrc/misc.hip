@@ -240,20 +240,25 @@ __global__ void pair_bwd_kernel(const float* __restrict__ a, const float* __rest
 }
 
 // --------------------------------------------------------------------- spectral norm
-// t = W^T u (cols), per-block partial of |t|^2
+// t = W^T u (cols): block = 64 columns x 4 row groups; per-block partial of |t|^2
 __global__ void sn_wtu_kernel(const float* __restrict__ w, int rows, int cols, const float* __restrict__ u,
                               float* t, float* part) {
-  const int j = blockIdx.x * NTH + threadIdx.x;
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
   float acc = 0.f;
-  if (j < cols) {
-    for (int i = 0; i < rows; ++i) acc += w[(long)i * cols + j] * u[i];
-    t[j] = acc;
-  }
-  float sq = wave_sum(acc * acc);
-  __shared__ float sh[NTH / 64];
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = sq;
+  if (j < cols)
+    for (int i = rg; i < rows; i += 4) acc += w[(long)i * cols + j] * u[i];
+  __shared__ float sh[4][64];
+  sh[rg][threadIdx.x & 63] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+  float sq = 0.f;
+  if (rg == 0) {
+    const float v = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
+    if (j < cols) t[j] = v;
+    sq = j < cols ? v * v : 0.f;
+    sq = wave_sum(sq);
+    if (threadIdx.x == 0) part[blockIdx.x] = sq;
+  }
 }
 
 // s = W v  (one wave per row), v = t / max(|t|, eps) when normalize (written out too)
@@ -520,7 +525,7 @@ int fv_spectral_norm_fwd(const float* w, int rows, int cols, float* u, float* v,
   float* t = (float*)ws;
   float* sv = t + cols;
   float* part = sv + rows;
-  const int nparts = fv_cdiv(cols, NTH);
+  const int nparts = fv_cdiv(cols, 64);
   FV_REQUIRE(nparts <= 2 * NTH, "spectral norm: too many columns");
   if (power_iter) {
     hipLaunchKernelGGL(sn_wtu_kernel, dim3(nparts), dim3(NTH), 0, s, w, rows, cols, u, t, part);

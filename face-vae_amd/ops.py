@@ -335,7 +335,9 @@ class ConvBNActFn(torch.autograd.Function):
 
 
 class ResBlockFn(torch.autograd.Function):
-    """ResBlock2D: x + NAC(NAC(x)), NAC = BN -> ReLU -> conv3x3 (modules.py:116-130)."""
+    """ResBlock2D: x + NAC(NAC(x)), NAC = BN -> ReLU -> conv3x3 (modules.py:116-130).
+    The BN-apply+ReLU output of each NAC is materialised once (one HBM pass) so the conv and
+    its weight gradient read a plain bf16 tensor; the residual add runs in conv2's epilogue."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, blk):
@@ -347,39 +349,40 @@ class ResBlockFn(torch.autograd.Function):
         training = blk.training
         comm = blk.bn_comm()
         c1, c2 = blk.conv1, blk.conv2
-        need_wt = any(ctx.needs_input_grad[:9])
         r1 = bn_from_tensor(blk.bn1, xb, training, comm)
-        d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size, pro=1, slope=0.0)
-        cs1 = ConvState(c1, d1, dtype, x.device, training, need_wt)
+        a1 = bn_act_forward(xb, r1, 0.0, False)
+        d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size)
+        cs1 = ConvState(c1, d1, dtype, x.device, training, True)
         t1 = torch.empty_like(xb)
-        part = conv_forward(cs1, xb, b1, pro=(r1.scale, r1.shift), y=t1, stats=training)
+        part = conv_forward(cs1, a1, b1, y=t1, stats=training)
         r2 = bn_from_partials(blk.bn2, part, d1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
-        d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size, pro=1, slope=0.0)
-        cs2 = ConvState(c2, d2, dtype, x.device, training, need_wt)
+        a2 = bn_act_forward(t1, r2, 0.0, False)
+        d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size)
+        cs2 = ConvState(c2, d2, dtype, x.device, training, True)
         out = torch.empty_like(xb)
-        conv_forward(cs2, t1, b2, pro=(r2.scale, r2.shift), res=xb, y=out)
+        conv_forward(cs2, a2, b2, res=xb, y=out)
         cs1.release()
         cs2.release()
         ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm = blk, cs1, cs2, r1, r2, comm
-        ctx.save_for_backward(x, xb, t1)
+        ctx.save_for_backward(x, xb, t1, a1, a2)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, xb, t1 = ctx.saved_tensors
+        x, xb, t1, a1, a2 = ctx.saved_tensors
         blk, cs1, cs2, r1, r2, comm = ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm
         C = xb.shape[1]
         dout = grad_in(dout, xb.dtype)
-        da2, dw2, db2 = conv_backward(cs2, t1, dout, C, pro=(r2.scale, r2.shift))
+        da2, dw2, db2 = conv_backward(cs2, a2, dout, C)
         dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm)
-        da1, dw1, db1 = conv_backward(cs1, xb, dt1, C, pro=(r1.scale, r1.shift))
+        da1, dw1, db1 = conv_backward(cs1, a1, dt1, C)
         dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout)
         dx = from_nhwc(dxb, x)
         return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None
 
 
 class NACFn(torch.autograd.Function):
-    """Standalone "NAC" ConvBlock2D: conv(act(BN(x))) with BN-apply + act in the conv prologue."""
+    """Standalone "NAC" ConvBlock2D: conv(act(BN(x))), the BN-apply+act output materialised once."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, blk):
@@ -394,21 +397,22 @@ class NACFn(torch.autograd.Function):
             raise RuntimeError("NAC block output channels must be a multiple of 8")
         comm = blk.bn_comm()
         r = bn_from_tensor(blk.bn, xb, blk.training, comm)
-        d = desc(dtype, N, H, W, C, C, cout, cout, conv.kernel_size, pro=1, slope=blk.slope)
+        a = bn_act_forward(xb, r, blk.slope, False)
+        d = desc(dtype, N, H, W, C, C, cout, cout, conv.kernel_size)
         cs = ConvState(conv, d, dtype, x.device, blk.training, need_wt=True)
         y = torch.empty((N, cout, H, W), dtype=dtype, device=x.device, memory_format=CL)
-        conv_forward(cs, xb, bias, pro=(r.scale, r.shift), y=y)
+        conv_forward(cs, a, bias, y=y)
         cs.release()
         ctx.blk, ctx.cs, ctx.r, ctx.comm = blk, cs, r, comm
-        ctx.save_for_backward(x, xb)
+        ctx.save_for_backward(x, xb, a)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, xb = ctx.saved_tensors
+        x, xb, a = ctx.saved_tensors
         blk, cs, r = ctx.blk, ctx.cs, ctx.r
         dy = grad_in(dy, xb.dtype)
-        da, dw, db = conv_backward(cs, xb, dy, dy.shape[1], pro=(r.scale, r.shift))
+        da, dw, db = conv_backward(cs, a, dy, dy.shape[1])
         dxb, dg, dbt = bn_act_backward(da, xb, blk.bn, r, blk.slope, False, ctx.comm,
                                        need_dx=ctx.needs_input_grad[0])
         return (from_nhwc(dxb, x) if dxb is not None else None), dw, db, dg, dbt, None

@@ -50,6 +50,12 @@ CONV_CASES = [
     (3, 128, 64, 8, 8, True, False),
     (3, 32, 32, 8, 6, True, True),
     (3, 16, 32, 7, 9, False, False),
+    # DMA-fed v2 path (bf16, cin % 64 == 0): big tiles, partial tiles, upsample, 1x1, 7x7
+    (3, 256, 256, 16, 16, False, False),
+    (3, 64, 128, 12, 20, False, False),
+    (3, 128, 64, 10, 6, True, False),
+    (7, 64, 3, 9, 13, False, False),
+    (1, 512, 256, 6, 10, False, False),
 ]
 
 
