@@ -47,6 +47,7 @@ _SIGS = {
     "fv_conv2d_bwd_data": (c_int, [D, P, c_int, P, P, P]),
     "fv_conv2d_wgrad_nsplit": (c_int, [D]),
     "fv_conv2d_wgrad_slab_elems": (c_size_t, [D]),
+    "fv_conv2d_wgrad_bias_slab_elems": (c_size_t, [D]),
     "fv_conv2d_bwd_weight": (c_int, [D, P, P, P, P, c_int, P, P, P]),
     "fv_conv2d_wgrad_reduce": (c_int, [D, P, P, P, P, P]),
     "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),

@@ -113,18 +113,23 @@ __global__ void tensor_stats_kernel(const T* __restrict__ x, long P, int C, int 
   }
 }
 
-// out[i] = sum_s ws[s][i], i < rec*C : 64 outputs x 4 lanes per block
+// out[i] = sum_s ws[s][i], i < rec*C : one wave per output (lanes stride the splits), 4 per block
 __global__ void sum_splits_kernel(const double* ws, int nsplit, int rec, int C, double* out) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane4 = threadIdx.x >> 6;
   const int n = rec * C;
-  double t = 0;
-  if (i < n)
-    for (int s = lane4; s < nsplit; s += 4) t += ws[(long)s * n + i];
-  __shared__ double sh[4][64];
-  sh[lane4][threadIdx.x & 63] = t;
-  __syncthreads();
-  if (lane4 == 0 && i < n) out[i] = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  double t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  int s = lane;
+  for (; s + 192 < nsplit; s += 256) {
+    t0 += ws[(long)s * n + i];
+    t1 += ws[(long)(s + 64) * n + i];
+    t2 += ws[(long)(s + 128) * n + i];
+    t3 += ws[(long)(s + 192) * n + i];
+  }
+  for (; s < nsplit; s += 64) t0 += ws[(long)s * n + i];
+  const double t = wave_sum_d((t0 + t1) + (t2 + t3));
+  if (lane == 0) out[i] = t;
 }
 
 __global__ void finalize_kernel(const double* stats, int C, const float* gamma, const float* beta,
@@ -328,7 +333,7 @@ int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixe
                      block_pixels, total_pixels, c, (double*)ws);
   int st = fv_check_launch("bn_partials");
   if (st) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 64)), dim3(NTH), 0, s, (const double*)ws, NSPLIT,
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 4)), dim3(NTH), 0, s, (const double*)ws, NSPLIT,
                      3, c, stats);
   return fv_check_launch("bn_sum_splits");
 }
@@ -347,7 +352,7 @@ int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, do
     hipLaunchKernelGGL(tensor_stats_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)x, pixels, c, ldc,
                        (double*)ws);
   if ((st = fv_check_launch("bn_tensor_stats"))) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 64)), dim3(NTH), 0, s, (const double*)ws, nb, 3, c,
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, 3, c,
                      stats);
   return fv_check_launch("bn_sum_splits");
 }
@@ -395,7 +400,7 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
     hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
                        (const float*)y, n, h, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, 64)), dim3(NTH), 0, s, (const double*)ws, nb, 2, c,
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, 2, c,
                      red);
   return fv_check_launch("bn_sum_splits");
 }

@@ -410,6 +410,19 @@ __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
+// 16 B per lane, buffer -> LDS (wave-uniform LDS base in M0, lane-linear destination).
+// Issued as inline asm on purpose: hipcc cannot tell that the ds_reads of the buffer being
+// computed do not alias the stage in flight and would put an s_waitcnt vmcnt(0) in front
+// of them, serialising the ring.  Ordering is therefore explicit: counted vmcnt + barrier.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, unsigned voff) {
+  unsigned keep;
+  const unsigned la = (unsigned)(size_t)(lds_ptr_t)lds;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(la)
+               : "memory");
+}
+
 template <int KS, int WN, int WM, int RN, int RM, bool UPS>
 __global__ void __launch_bounds__(64 * WN * WM, 2)
 conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
@@ -422,7 +435,6 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   constexpr int STAGE = (BM + BN) * ROWB;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
-  const bf16* __restrict__ wk = reinterpret_cast<const bf16*>(a.w);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % WN, wm = wave / WN;
@@ -437,6 +449,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   const int HW = a.H * a.W;
 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
   const int lrow = lane >> 3, lchk = lane & 7;
   int rh[JA], rw[JA], rb[JA];
   bool rv[JA];
@@ -476,7 +489,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
           ws = ww;
         }
         const unsigned off = ok ? ((unsigned)((rb[j] + hs * a.Win + ws) << a.lgCin) + (unsigned)ci) * 2u : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(As + q * 1024), 16, off, 0, 0, 0);
+        dma16(xr, As + q * 1024, off);
       }
     }
 #pragma unroll
@@ -484,8 +497,8 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
       const int q = wave + j * NW;
       if (QB % NW == 0 || q < QB) {
         const int row = q * 8 + lrow;
-        const bf16* src = wk + (long)(co0 + row) * a.Kpad + k0 + ((lchk ^ swz8(row)) << 3);
-        __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(Bs + q * 1024), 16, 0, 0);
+        const unsigned woff = (unsigned)(((co0 + row) * a.Kpad + k0 + ((lchk ^ swz8(row)) << 3)) * 2);
+        dma16(wr, Bs + q * 1024, woff);
       }
     }
   };
@@ -767,6 +780,243 @@ conv_wgrad_kernel(WgArgs a) {
 }
 
 // ----------------------------------------------------------------------------------------
+// backward-weight v2 (bf16): D[k][co] = sum_p im2col(x)[p][k] * dy[p][co] as a pixel-K GEMM.
+// 8 waves, block tile BKT (k) x BC (co), PX pixels per stage, NS-stage LDS ring filled by
+// buffer_load ... lds (the DMA destination is lane-linear, so the 32-B-block XOR swizzle
+// that makes the transposed fragment reads conflict-free is applied to the SOURCE
+// address), counted vmcnt + raw s_barrier so NS-1 stages stay in flight.  Fragments are
+// read with ds_read_b64_tr_b16 (pixels are the MFMA K).  Zero padding (image border,
+// k >= K, co >= ldd, pixel >= P) comes from the buffer range check (offset 0x80000000).
+// The bias gradient sum_p dy[p][co] rides along as one extra MFMA per co tile with an
+// all-ones A operand (k-tile-0 blocks, k-wave 0 only).  Output: per-split fp32 slabs.
+// ----------------------------------------------------------------------------------------
+struct FastDiv {
+  uint32_t m, s;
+};
+FastDiv make_fastdiv(uint32_t d) {  // host side; exact for numerators < 2^31
+  uint32_t s = 0;
+  while ((1u << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return {(uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
+struct Wg2Args {
+  const void* x;
+  const void* dy;
+  float* slab;
+  float* bslab;
+  int H, W, Hin, Win, P;
+  int lgCin, K, KW, ldd, CW;
+  int ntk, ntc, nsteps, sps;
+  FastDiv fhw, fw;
+  unsigned xbytes, dybytes;
+};
+
+// 32-B-block XOR of a [row][NCOL] bf16 image: the 8 rows {0-3, 8-11} (and {4-7, 12-15}) one
+// ds_read_b64_tr_b16 lane group touches land on 8 distinct 32-B bank slots.
+template <int NCOL>
+__device__ __forceinline__ int tswz(int row) {
+  if constexpr (NCOL >= 128) return (row & 3) | (((row >> 3) & 1) << 2);
+  else if constexpr (NCOL == 64) return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  else return 0;
+}
+template <int NCOL>
+__device__ __forceinline__ int timg_off(int row, int col) {  // col % 4 == 0
+  return row * NCOL * 2 + ((((col >> 4) ^ tswz<NCOL>(row)) << 5) | ((col & 15) << 1));
+}
+// 16 columns x 32 rows (rows r0..r0+31) -> MFMA K-fragment of column (cbase + lane & 15)
+template <int NCOL>
+__device__ __forceinline__ bf16x8 tfrag(const char* base, int r0, int cbase, int lane) {
+  const int g = lane >> 4, li = lane & 15;
+  const int c = cbase + 4 * (li & 3);
+  FV_LDS char* lb = (FV_LDS char*)(base);
+  const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + timg_off<NCOL>(r0 + 8 * g + (li >> 2), c)));
+  const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + timg_off<NCOL>(r0 + 8 * g + 4 + (li >> 2), c)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <int KS, int BKT, int BC, int WK, int WC, int PX, int NS, bool UPS>
+__global__ void __launch_bounds__(512, 2)
+conv_wgrad_v2(Wg2Args a) {
+  static_assert(WK * WC == 8, "8 waves");
+  constexpr int RK = BKT / (16 * WK), RC = BC / (16 * WC);
+  static_assert(RK * 16 * WK == BKT && RC * 16 * WC == BC, "wave tiling");
+  constexpr int PAD = KS / 2;
+  constexpr int SA = PX * BKT * 2, SB = PX * BC * 2, STAGE = SA + SB;
+  constexpr int QA = SA / 1024, QB = SB / 1024;            // 1-KB DMA pieces per stage
+  static_assert(QA * 1024 == SA && QB * 1024 == SB, "pieces");
+  constexpr int JA = (QA + 7) / 8, JB = (QB + 7) / 8;      // pieces per wave
+  constexpr int PW = JA + JB;                              // upper bound of DMAs per wave per stage
+  constexpr int CPA = BKT / 8, CPB = BC / 8;               // 16-B chunks per row
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wave % WK, wc = wave / WK;
+  // XCD-aware order: the blocks of one pixel split (all k/co tiles: same dy rows, overlapping
+  // x rows) share an XCD's L2.  Bijective remap; speed only.
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int ntile = a.ntk * a.ntc;
+  const int split = lid / ntile, tile = lid - split * ntile;
+  const int tc = tile % a.ntc, tk = tile / a.ntc;
+  const int k0 = tk * BKT, c0 = tc * BC;
+  const int s_begin = split * a.sps;
+  const int nst = min(a.nsteps, s_begin + a.sps) - s_begin;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), 0, (int)a.dybytes, 0x00020000);
+
+  // per-piece constants: row in the stage image and the (tap, ci) of this lane's chunk
+  int arow[JA], adh[JA], adw[JA], aci[JA];
+  bool akin[JA];
+#pragma unroll
+  for (int j = 0; j < JA; ++j) {
+    const int q = wave + j * 8;
+    const int L = q * 64 + lane;
+    const int row = L / CPA, dch = L % CPA;
+    const int sc = (((dch >> 1) ^ tswz<BKT>(row)) << 1) | (dch & 1);
+    const int k = k0 + sc * 8;
+    const int tap = k >> a.lgCin;
+    const int r = tap / KS, s = tap - (tap / KS) * KS;
+    arow[j] = row;
+    adh[j] = r - PAD;
+    adw[j] = s - PAD;
+    aci[j] = k & ((1 << a.lgCin) - 1);
+    akin[j] = (QA % 8 == 0 || q < QA) && k < a.K;
+  }
+  int brow[JB], bco[JB];
+  bool bok[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    const int q = wave + j * 8;
+    const int L = q * 64 + lane;
+    const int row = L / CPB, dch = L % CPB;
+    const int sc = CPB >= 4 ? ((((dch >> 1) ^ tswz<BC>(row)) << 1) | (dch & 1)) : dch;
+    brow[j] = row;
+    bco[j] = c0 + sc * 8;
+    bok[j] = (QB % 8 == 0 || q < QB) && bco[j] < a.ldd;
+  }
+
+  auto issue = [&](int st, int buf) {
+    const int pbase = (s_begin + st) * PX;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + SA;
+#pragma unroll
+    for (int j = 0; j < JA; ++j) {
+      const int q = wave + j * 8;
+      if (QA % 8 == 0 || q < QA) {
+        const int p = pbase + arow[j];
+        const int n = (int)fdiv((uint32_t)p, a.fhw);
+        const int rem = p - n * a.H * a.W;
+        const int h = (int)fdiv((uint32_t)rem, a.fw);
+        const int w = rem - h * a.W;
+        const int hh = h + adh[j], ww = w + adw[j];
+        bool ok = akin[j] && p < a.P && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+        const int hs = UPS ? (hh >> 1) : hh, ws = UPS ? (ww >> 1) : ww;
+        const unsigned off = ok ? ((unsigned)(((n * a.Hin + hs) * a.Win + ws) << a.lgCin) + (unsigned)aci[j]) * 2u
+                                : 0x80000000u;
+        dma16(xr, As + q * 1024, off);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int q = wave + j * 8;
+      if (QB % 8 == 0 || q < QB) {
+        const int p = pbase + brow[j];
+        const bool ok = bok[j] && p < a.P;
+        const unsigned off = ok ? ((unsigned)p * (unsigned)a.ldd + (unsigned)bco[j]) * 2u : 0x80000000u;
+        dma16(dr, Bs + q * 1024, off);
+      }
+    }
+  };
+  // a counted vmcnt needs every wave to issue exactly PW DMAs per stage
+  static_assert((QA % 8 == 0 && QB % 8 == 0) || NS == 2, "uneven DMA split needs NS == 2 (vmcnt(0))");
+
+  f32x4 acc[RK][RC];
+#pragma unroll
+  for (int i = 0; i < RK; ++i)
+#pragma unroll
+    for (int j = 0; j < RC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bslab && tk == 0 && wk == 0;
+  f32x4 accb[RC];
+#pragma unroll
+  for (int j = 0; j < RC; ++j) accb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + SA;
+#pragma unroll
+    for (int kk = 0; kk < PX / 32; ++kk) {
+      bf16x8 af[RK], bfr[RC];
+#pragma unroll
+      for (int j = 0; j < RC; ++j) bfr[j] = tfrag<BC>(Bs, kk * 32, wc * RC * 16 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < RK; ++i) af[i] = tfrag<BKT>(As, kk * 32, wk * RK * 16 + i * 16, lane);
+#pragma unroll
+      for (int i = 0; i < RK; ++i)
+#pragma unroll
+        for (int j = 0; j < RC; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < RC; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[j], accb[j], 0, 0, 0);
+      }
+    }
+  };
+
+  // ring: NS-1 stages in flight; stage `it` is waited for with a counted vmcnt, then one
+  // raw barrier publishes it (and retires every wave's reads of the buffer re-filled next).
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nst) issue(i, i);
+  for (int it = 0; it < nst; ++it) {
+    const int ahead = min(NS - 2, nst - 1 - it);   // younger stages allowed in flight
+    if constexpr (NS >= 4) {
+      if (ahead >= 2) wait_vmcnt<2 * PW>();
+      else if (ahead == 1) wait_vmcnt<PW>();
+      else wait_vmcnt<0>();
+    } else if constexpr (NS == 3) {
+      if (ahead >= 1) wait_vmcnt<PW>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (it + NS - 1 < nst) issue(it + NS - 1, (it + NS - 1) % NS);
+    compute(it % NS);
+  }
+
+  // D[k][co]: lane holds k = kb + 4*(lane>>4) + i for co = cb + (lane & 15)
+  const int lr = lane & 15, lh = lane >> 4;
+  float* slab = a.slab + (long)split * a.CW * a.KW;
+#pragma unroll
+  for (int i = 0; i < RK; ++i) {
+    const int kb = k0 + wk * RK * 16 + i * 16 + lh * 4;
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+      const int co = c0 + wc * RC * 16 + j * 16 + lr;
+      *reinterpret_cast<float4*>(slab + (long)co * a.KW + kb) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+  if (do_bias && lh == 0) {
+#pragma unroll
+    for (int j = 0; j < RC; ++j) a.bslab[(long)split * a.CW + c0 + wc * RC * 16 + j * 16 + lr] = accb[j][0];
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // weight re-layout (+ 1/sigma) and slab reduction
 // ----------------------------------------------------------------------------------------
 template <typename T>
@@ -881,10 +1131,30 @@ bool use_v2(const fv_conv_desc* d) {
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
 
+// v2 tile configs: id -> (co per block, pixels per block); waves/layout in launch_v2_ks
+struct V2Cfg { int bn, bm; };
+constexpr V2Cfg kV2Cfg[] = {
+    {128, 128},   // 0: 4 waves 2x2, wave 64co x 64px
+    {64, 256},    // 1: 4 waves 1x4, wave 64co x 64px
+    {16, 256},    // 2: 4 waves 1x4, wave 16co x 64px
+    {256, 256},   // 3: 8 waves 4x2, wave 64co x 128px
+    {128, 256},   // 4: 8 waves 2x4, wave 64co x 64px
+    {256, 128},   // 5: 8 waves 4x2, wave 64co x 64px
+};
+static int g_v2_force = -2;
+int v2_cfg(int rows_needed) {
+  if (g_v2_force == -2) {
+    const char* e = getenv("FV_V2_CFG");
+    g_v2_force = e ? atoi(e) : -1;
+  }
+  if (g_v2_force >= 0 && rows_needed % kV2Cfg[g_v2_force].bn == 0) return g_v2_force;
+  if (rows_needed > 64) return 0;
+  if (rows_needed > 16) return 1;
+  return 2;
+}
 FwdTile fwd_tile_v2(int rows_needed) {
-  if (rows_needed > 64) return {128, 128};
-  if (rows_needed > 16) return {64, 256};
-  return {16, 256};
+  const V2Cfg c = kV2Cfg[v2_cfg(rows_needed)];
+  return {c.bn, c.bm};
 }
 
 template <int KS, int WN, int WM, int RN, int RM>
@@ -901,9 +1171,13 @@ int launch_v2_t(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s
 
 template <int KS>
 int launch_v2_ks(const ConvArgs& a, FwdTile t, int ups, int nblk, unsigned xb, hipStream_t s) {
-  if (t.bn == 128) return launch_v2_t<KS, 2, 2, 4, 4>(a, ups, nblk, xb, s);
+  if (t.bn == 128 && t.bm == 128) return launch_v2_t<KS, 2, 2, 4, 4>(a, ups, nblk, xb, s);
   if (t.bn == 64) return launch_v2_t<KS, 1, 4, 4, 4>(a, ups, nblk, xb, s);
-  return launch_v2_t<KS, 1, 4, 1, 4>(a, ups, nblk, xb, s);
+  if (t.bn == 16) return launch_v2_t<KS, 1, 4, 1, 4>(a, ups, nblk, xb, s);
+  if (t.bn == 256 && t.bm == 256) return launch_v2_t<KS, 4, 2, 4, 8>(a, ups, nblk, xb, s);
+  if (t.bn == 128 && t.bm == 256) return launch_v2_t<KS, 2, 4, 4, 4>(a, ups, nblk, xb, s);
+  if (t.bn == 256 && t.bm == 128) return launch_v2_t<KS, 4, 2, 4, 4>(a, ups, nblk, xb, s);
+  return FV_E_UNSUPPORTED;
 }
 
 int launch_v2(const ConvArgs& a, int ks, FwdTile t, int ups, int nblk, unsigned xb, hipStream_t s) {
@@ -931,25 +1205,76 @@ int check_desc(const fv_conv_desc* d) {
 
 int kpad_of(int ks, int cin) { return fv_cdiv((long)ks * ks * cin, BK) * BK; }
 
-struct WgTile { int bkt, bc; };
-WgTile wg_tile(const fv_conv_desc* d) {
-  WgTile t;
-  t.bc = d->cout > 64 ? 128 : (d->cout > 16 ? 64 : 16);
-  t.bkt = 128;
-  return t;
+// wgrad plan: v2 (bf16 DMA-fed, 8 waves) or the register-staged v1 (fp32 / BN prologue)
+struct WgPlan {
+  int v2, bkt, bc, px, ntk, ntc, nsplit, nsteps, sps, KW, CW;
+};
+static int g_disable_wg2 = -1;
+WgPlan plan_wgrad(const fv_conv_desc* d) {
+  if (g_disable_wg2 < 0) {
+    const char* e = getenv("FV_DISABLE_WG2");
+    g_disable_wg2 = (e && e[0] == '1') ? 1 : 0;
+  }
+  WgPlan p{};
+  const int K = d->ksize * d->ksize * d->cin;
+  const long P = (long)d->n * d->h * d->w;
+  const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
+  p.v2 = !g_disable_wg2 && d->dtype == FV_BF16 && !d->pro_act && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
+         P * 256 * 2 < (1L << 31);
+  if (p.v2) {
+    p.bc = d->cout > 128 ? 256 : d->cout > 64 ? 128 : d->cout > 16 ? 64 : 16;
+    if (p.bc == 64) p.bkt = 128;
+    else if (p.bc == 16) p.bkt = 256;
+    else p.bkt = (fv_cdiv(K, 256) * 256 <= fv_cdiv(K, 128) * 128) ? 256 : 128;
+    p.px = 64;
+  } else {
+    p.bc = d->cout > 64 ? 128 : (d->cout > 16 ? 64 : 16);
+    p.bkt = 128;
+    p.px = 32;
+  }
+  p.ntk = fv_cdiv(K, p.bkt);
+  p.ntc = fv_cdiv(d->cout, p.bc);
+  p.nsteps = fv_cdiv(P, p.px);
+  const int ntile = p.ntk * p.ntc;
+  int ns = p.v2 ? (256 + ntile / 2) / ntile : 768 / ntile;
+  if (ns < 1) ns = 1;
+  if (ns > p.nsteps) ns = p.nsteps;
+  p.sps = fv_cdiv(p.nsteps, ns);
+  p.nsplit = fv_cdiv(p.nsteps, p.sps);
+  p.KW = p.ntk * p.bkt;
+  p.CW = p.ntc * p.bc;
+  return p;
 }
 
-int wg_nsplit(const fv_conv_desc* d) {
-  const WgTile t = wg_tile(d);
-  const int K = d->ksize * d->ksize * d->cin;
-  const int ntk = fv_cdiv(K, t.bkt), ntc = fv_cdiv(d->cout, t.bc);
-  const long P = (long)d->n * d->h * d->w;
-  const int nsteps = fv_cdiv(P, 32);
-  int ns = 768 / (ntk * ntc);
-  if (ns < 1) ns = 1;
-  if (ns > nsteps) ns = nsteps;
-  const int per = fv_cdiv(nsteps, ns);
-  return fv_cdiv(nsteps, per);
+template <int KS, int BKT, int BC, int WK, int WC, int NS>
+int launch_wg2_t(const Wg2Args& a, int ups, int nblk, hipStream_t s) {
+  if (ups) {
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_wgrad_v2<KS, BKT, BC, WK, WC, 64, NS, true>), dim3(nblk), dim3(512), 0, s, a);
+    else return FV_E_UNSUPPORTED;
+  } else {
+    hipLaunchKernelGGL((conv_wgrad_v2<KS, BKT, BC, WK, WC, 64, NS, false>), dim3(nblk), dim3(512), 0, s, a);
+  }
+  return FV_OK;
+}
+
+template <int KS>
+int launch_wg2_ks(const Wg2Args& a, const WgPlan& p, int ups, int nblk, hipStream_t s) {
+  if (p.bkt == 256 && p.bc == 256) return launch_wg2_t<KS, 256, 256, 2, 4, 2>(a, ups, nblk, s);
+  if (p.bkt == 128 && p.bc == 256) return launch_wg2_t<KS, 128, 256, 2, 4, 3>(a, ups, nblk, s);
+  if (p.bkt == 256 && p.bc == 128) return launch_wg2_t<KS, 256, 128, 4, 2, 3>(a, ups, nblk, s);
+  if (p.bkt == 128 && p.bc == 128) return launch_wg2_t<KS, 128, 128, 2, 4, 4>(a, ups, nblk, s);
+  if (p.bkt == 128 && p.bc == 64) return launch_wg2_t<KS, 128, 64, 8, 1, 4>(a, ups, nblk, s);
+  if (p.bkt == 256 && p.bc == 16) return launch_wg2_t<KS, 256, 16, 8, 1, 2>(a, ups, nblk, s);
+  return FV_E_UNSUPPORTED;
+}
+
+int launch_wg2(const Wg2Args& a, int ks, const WgPlan& p, int ups, int nblk, hipStream_t s) {
+  switch (ks) {
+    case 1: return launch_wg2_ks<1>(a, p, ups, nblk, s);
+    case 3: return launch_wg2_ks<3>(a, p, ups, nblk, s);
+    case 7: return launch_wg2_ks<7>(a, p, ups, nblk, s);
+  }
+  return FV_E_UNSUPPORTED;
 }
 
 template <typename T, int KS, int WK, int WC, int RK, int RC>
@@ -971,14 +1296,14 @@ int launch_wg_t(const WgArgs& a, int pro, int ups, int nblk, hipStream_t s) {
 }
 
 template <typename T, int KS>
-int launch_wg_ks(const WgArgs& a, WgTile t, int pro, int ups, int nblk, hipStream_t s) {
+int launch_wg_ks(const WgArgs& a, const WgPlan& t, int pro, int ups, int nblk, hipStream_t s) {
   if (t.bc == 128) return launch_wg_t<T, KS, 2, 2, 4, 4>(a, pro, ups, nblk, s);
   if (t.bc == 64) return launch_wg_t<T, KS, 2, 2, 4, 2>(a, pro, ups, nblk, s);
   return launch_wg_t<T, KS, 4, 1, 2, 1>(a, pro, ups, nblk, s);
 }
 
 template <typename T>
-int launch_wg(const WgArgs& a, int ks, WgTile t, int pro, int ups, int nblk, hipStream_t s) {
+int launch_wg(const WgArgs& a, int ks, const WgPlan& t, int pro, int ups, int nblk, hipStream_t s) {
   switch (ks) {
     case 1: return launch_wg_ks<T, 1>(a, t, pro, ups, nblk, s);
     case 3: return launch_wg_ks<T, 3>(a, t, pro, ups, nblk, s);
@@ -1120,16 +1445,19 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
 
 int fv_conv2d_wgrad_nsplit(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
-  return wg_nsplit(d);
+  return plan_wgrad(d).nsplit;
 }
 
 size_t fv_conv2d_wgrad_slab_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
-  const WgTile t = wg_tile(d);
-  const int K = d->ksize * d->ksize * d->cin;
-  const size_t CW = (size_t)fv_cdiv(d->cout, t.bc) * t.bc;
-  const size_t KW = (size_t)fv_cdiv(K, t.bkt) * t.bkt;
-  return (size_t)wg_nsplit(d) * CW * KW;
+  const WgPlan p = plan_wgrad(d);
+  return (size_t)p.nsplit * p.CW * p.KW;
+}
+
+size_t fv_conv2d_wgrad_bias_slab_elems(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  const WgPlan p = plan_wgrad(d);
+  return (size_t)p.nsplit * p.CW;
 }
 
 int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_scale,
@@ -1140,23 +1468,45 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
   FV_REQUIRE(x && dy && slab, "null pointer");
   FV_REQUIRE(ldy_dy % 8 == 0 && ldy_dy >= d->cout, "wgrad: dy channel stride must be a multiple of 8 >= cout");
   FV_REQUIRE(!d->pro_act || (pro_scale && pro_shift), "prologue needs scale/shift");
-  const WgTile t = wg_tile(d);
+  const WgPlan t = plan_wgrad(d);
+  const int Hin = d->upsample ? d->h / 2 : d->h, Win = d->upsample ? d->w / 2 : d->w;
+  const long P = (long)d->n * d->h * d->w;
+  if (t.v2) {
+    FV_REQUIRE(P * ldy_dy * 2 < (1L << 31), "wgrad: dy larger than 2 GB");
+    Wg2Args a{};
+    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+    a.H = d->h; a.W = d->w; a.Hin = Hin; a.Win = Win; a.P = (int)P;
+    a.lgCin = fv_ilog2(d->cin);
+    a.K = d->ksize * d->ksize * d->cin;
+    a.KW = t.KW; a.ldd = ldy_dy; a.CW = t.CW;
+    a.ntk = t.ntk; a.ntc = t.ntc; a.nsteps = t.nsteps; a.sps = t.sps;
+    a.fhw = make_fastdiv((uint32_t)(d->h * d->w));
+    a.fw = make_fastdiv((uint32_t)d->w);
+    a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
+    a.dybytes = (unsigned)(P * ldy_dy * 2);
+    const int nblk = t.ntk * t.ntc * t.nsplit;
+    st = launch_wg2(a, d->ksize, t, d->upsample, nblk, (hipStream_t)stream);
+    if (st) {
+      fv_set_error("wgrad v2 variant unsupported (k=%d ups=%d bkt=%d bc=%d)", d->ksize, d->upsample, t.bkt, t.bc);
+      return st;
+    }
+    return fv_check_launch("conv2d_bwd_weight_v2");
+  }
   WgArgs a{};
   a.x = x; a.psc = pro_scale; a.psh = pro_shift; a.slope = d->pro_slope;
   a.dy = dy; a.slab = slab; a.bslab = bias_slab;
   a.N = d->n; a.H = d->h; a.W = d->w;
-  a.Hin = d->upsample ? d->h / 2 : d->h;
-  a.Win = d->upsample ? d->w / 2 : d->w;
-  a.P = d->n * d->h * d->w;
+  a.Hin = Hin;
+  a.Win = Win;
+  a.P = (int)P;
   a.Cin = d->cin; a.lgCin = fv_ilog2(d->cin);
   a.K = d->ksize * d->ksize * d->cin;
-  a.ntk = fv_cdiv(a.K, t.bkt); a.KW = a.ntk * t.bkt;
+  a.ntk = t.ntk; a.KW = t.KW;
   a.Cout = d->cout; a.ldd = ldy_dy;
-  a.ntc = fv_cdiv(d->cout, t.bc); a.CW = a.ntc * t.bc;
-  a.nsteps = fv_cdiv(a.P, 32);
-  const int ns = wg_nsplit(d);
-  a.steps_per_split = fv_cdiv(a.nsteps, ns);
-  const int nblk = a.ntk * a.ntc * ns;
+  a.ntc = t.ntc; a.CW = t.CW;
+  a.nsteps = t.nsteps;
+  a.steps_per_split = t.sps;
+  const int nblk = t.ntk * t.ntc * t.nsplit;
   st = d->dtype == FV_BF16 ? launch_wg<bf16>(a, d->ksize, t, d->pro_act, d->upsample, nblk, (hipStream_t)stream)
                            : launch_wg<float>(a, d->ksize, t, d->pro_act, d->upsample, nblk, (hipStream_t)stream);
   if (st) {
@@ -1172,13 +1522,12 @@ int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float
   if (st) return st;
   FV_REQUIRE(slab && dw_param, "null pointer");
   FV_REQUIRE(!db || bias_slab, "db needs the bias slab");
-  const WgTile t = wg_tile(d);
+  const WgPlan t = plan_wgrad(d);
   const int K = d->ksize * d->ksize * d->cin;
-  const int KW = fv_cdiv(K, t.bkt) * t.bkt, CW = fv_cdiv(d->cout, t.bc) * t.bc;
   const long tot = (long)d->cout * K;
   const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 8192);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, slab, bias_slab,
-                     dw_param, db, wg_nsplit(d), CW, KW, K, d->cout, d->cin_valid, fv_ilog2(d->cin),
+                     dw_param, db, t.nsplit, t.CW, t.KW, K, d->cout, d->cin_valid, fv_ilog2(d->cin),
                      d->ksize);
   return fv_check_launch("wgrad_reduce");
 }

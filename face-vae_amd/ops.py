@@ -175,8 +175,7 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
     d = cs.d
     dev = dy.device
     slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
-    ns = query("fv_conv2d_wgrad_nsplit", ctypes.byref(d))
-    bslab = _empty(ns * ((d.cout + 127) // 128) * 128, F32, dev) if need_db else None
+    bslab = _empty(query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), F32, dev) if need_db else None
     psc, psh = (pro if pro is not None else (None, None))
     _timed("wgrad", d, lambda: call("fv_conv2d_bwd_weight", ctypes.byref(d), ptr(x), ptr(psc), ptr(psh), ptr(dy),
                                     ldd, ptr(slab), ptr(bslab), stream()))

@@ -95,9 +95,10 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
                        void* dx, void* stream);
 
 /* weight gradient w.r.t. the effective (post-SN) weight, split over pixels:
- * slab [nsplit][rows][Kpad] fp32 and bias slab [nsplit][cout] fp32. */
+ * slab [nsplit][rows][Kpad] fp32 and bias slab [nsplit][rows] fp32 (sizes from the queries). */
 int fv_conv2d_wgrad_nsplit(const fv_conv_desc* d);
 size_t fv_conv2d_wgrad_slab_elems(const fv_conv_desc* d);
+size_t fv_conv2d_wgrad_bias_slab_elems(const fv_conv_desc* d);
 int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_scale,
                          const float* pro_shift, const void* dy, int ldy_dy, float* slab,
                          float* bias_slab, void* stream);

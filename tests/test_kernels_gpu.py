@@ -132,8 +132,7 @@ def test_conv_bwd(case, dtype):
     gyb[:, :cout] = gy.cuda().to(dtype)
     # weight + bias gradient
     slab = torch.empty(L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), device="cuda")
-    ns = L.query("fv_conv2d_wgrad_nsplit", ctypes.byref(d))
-    bslab = torch.empty(ns * ((cout + 127) // 128) * 128, device="cuda")
+    bslab = torch.empty(L.query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), device="cuda")
     scd, shd = sc.cuda(), sh.cuda()
     L.call("fv_conv2d_bwd_weight", ctypes.byref(d), xb.data_ptr(), L.ptr(scd if pro else None),
            L.ptr(shd if pro else None), gyb.data_ptr(), ldd, slab.data_ptr(), bslab.data_ptr(), L.stream())

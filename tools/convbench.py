@@ -1,0 +1,120 @@
+"""Per-layer conv kernel timing at the FaceVAE shapes (256x256, B=32 by default).
+
+    python tools/convbench.py [--batch 32] [--res 256] [--iters 20] [--only fwd,dgrad,wgrad] [--layers res,up2]
+
+Times fv_conv2d_fwd / fv_conv2d_bwd_data / fv_conv2d_bwd_weight(+reduce) with HIP events on
+the launch stream and prints us/launch and TFLOP/s (algorithmic, reference formulation).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import fvamd  # noqa: E402,F401
+from facevae_amd import _lib as L  # noqa: E402
+from facevae_amd import ops  # noqa: E402
+
+CL = torch.channels_last
+
+
+def layers(H):
+    q, e = H // 4, H // 2
+    # name, k, cin, cout, out H, ups
+    return [
+        ("in7", 7, 3, 64, H, False),
+        ("down1", 3, 64, 128, H, False),
+        ("down2", 3, 128, 256, e, False),
+        ("mid1x1", 1, 256, 512, q, False),
+        ("gin", 3, 256, 256, q, False),
+        ("gmid1x1", 1, 256, 256, q, False),
+        ("res", 3, 256, 256, q, False),
+        ("up1", 3, 256, 128, e, True),
+        ("up2", 3, 128, 64, H, True),
+        ("out7", 7, 64, 3, H, False),
+    ]
+
+
+def timeit(fn, iters):
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3   # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="fwd,dgrad,wgrad")
+    ap.add_argument("--layers", default="")
+    ap.add_argument("--dtype", default="bf16")
+    a = ap.parse_args()
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    kinds = a.only.split(",")
+    sel = set(a.layers.split(",")) if a.layers else None
+    B = a.batch
+    out = []
+    for name, k, cin, cout, H, ups in layers(a.res):
+        if sel and name not in sel:
+            continue
+        Hi = H // 2 if ups else H
+        cp = ops.pad_pow2(cin)
+        x = torch.randn(B, cp, Hi, Hi, device="cuda").to(dtype).contiguous(memory_format=CL)
+        d = ops.desc(dtype, B, H, H, cp, cin, cout, cout, k, ups)
+        w = (torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).contiguous()
+        wk = torch.empty(L.query("fv_conv_wk_elems", ctypes.byref(d)), dtype=dtype, device="cuda")
+        wt = torch.empty(L.query("fv_conv_wt_elems", ctypes.byref(d)), dtype=dtype, device="cuda")
+        L.call("fv_conv_weight_prep", ctypes.byref(d), w.data_ptr(), None, wk.data_ptr(), wt.data_ptr(), L.stream())
+        nchw = cout % 8 != 0
+        ldd = ops.pad_pow2(cout) if nchw else cout
+        if nchw:
+            d.out_nchw_f32 = 1
+            y = torch.empty(B, cout, H, H, device="cuda")
+        else:
+            y = torch.empty(B, cout, H, H, dtype=dtype, device="cuda", memory_format=CL)
+        nb = L.query("fv_conv2d_stats_blocks", ctypes.byref(d))
+        part = torch.empty(nb * 2 * cout, device="cuda")
+        flop = 2.0 * B * H * H * cout * cin * k * k
+        row = {"layer": name, "k": k, "cin": cin, "cout": cout, "H": H, "ups": ups, "gflop": flop / 1e9}
+        if "fwd" in kinds:
+            us = timeit(lambda: L.call("fv_conv2d_fwd", ctypes.byref(d), x.data_ptr(), wk.data_ptr(), None, None,
+                                       None, None, y.data_ptr(), None if nchw else part.data_ptr(), L.stream()),
+                        a.iters)
+            row["fwd_us"], row["fwd_tf"] = round(us, 1), round(flop / us / 1e6, 1)
+        dy = (torch.randn(B, ldd, H, H, device="cuda") * 0.1).to(dtype).contiguous(memory_format=CL)
+        if "dgrad" in kinds and name != "in7":
+            dx = torch.empty(B, cp, H, H, dtype=dtype, device="cuda", memory_format=CL)
+            us = timeit(lambda: L.call("fv_conv2d_bwd_data", ctypes.byref(d), dy.data_ptr(), ldd, wt.data_ptr(),
+                                       dx.data_ptr(), L.stream()), a.iters)
+            row["dgrad_us"], row["dgrad_tf"] = round(us, 1), round(flop / us / 1e6, 1)
+        if "wgrad" in kinds:
+            slab = torch.empty(L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), device="cuda")
+            bslab = torch.empty(L.query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), device="cuda")
+            dw = torch.empty_like(w)
+            db = torch.empty(cout, device="cuda")
+            us = timeit(lambda: L.call("fv_conv2d_bwd_weight", ctypes.byref(d), x.data_ptr(), None, None,
+                                       dy.data_ptr(), ldd, slab.data_ptr(), bslab.data_ptr(), L.stream()), a.iters)
+            us2 = timeit(lambda: L.call("fv_conv2d_wgrad_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(),
+                                        dw.data_ptr(), db.data_ptr(), L.stream()), a.iters)
+            row["wgrad_us"], row["wgrad_tf"], row["wred_us"] = round(us, 1), round(flop / us / 1e6, 1), round(us2, 1)
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    tot = {k: round(sum(r.get(k, 0) for r in out), 1) for k in ("fwd_us", "dgrad_us", "wgrad_us", "wred_us")}
+    print(json.dumps({"total": tot}))
+
+
+if __name__ == "__main__":
+    main()
