@@ -38,6 +38,7 @@ struct ConvArgs {
   int K, Kpad, nks;
   int sigmoid, nchw;
   int ntn;
+  int lgtw;       // > 0: a block's pixels are a (BM >> lgtw) x (1 << lgtw) rectangle at p0
 };
 
 // 16-B chunk swizzle of a 64-B bf16 LDS row (4 chunks): conflict-free ds_read_b128 for the
@@ -122,7 +123,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
   int pix_of[RM];
 #pragma unroll
   for (int m = 0; m < RM; ++m) {
-    pix_of[m] = p0 + wm * RM * 16 + m * 16 + lr;
+    const int loc = wm * RM * 16 + m * 16 + lr;
+    pix_of[m] = a.lgtw ? p0 + (loc >> a.lgtw) * a.W + (loc & ((1 << a.lgtw) - 1)) : p0 + loc;
     pv[m] = pix_of[m] < a.P;
   }
 #pragma unroll
@@ -152,7 +154,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     // per-block (sum, centred M2) per output channel; rows of this block = valid pixels
     float* red = reinterpret_cast<float*>(smem);        // [WM][BN]
     float* meanv = red + WM * BN;                         // [BN]
-    const int cnt = min(BM, a.P - p0);
+    const int cnt = a.lgtw ? BM : min(BM, a.P - p0);
     float s[RN][4];
 #pragma unroll
     for (int n = 0; n < RN; ++n)
@@ -416,7 +418,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // of them, serialising the ring.  Ordering is therefore explicit: counted vmcnt + barrier.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, unsigned voff) {
   unsigned keep;
-  const unsigned la = (unsigned)(size_t)(lds_ptr_t)lds;
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)lds);
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(voff), "s"(r), "s"(la)
@@ -542,6 +544,158 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   }
   __syncthreads();
   conv_epilogue<bf16, WN, WM, RN, RM>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+}
+
+// ----------------------------------------------------------------------------------------
+// Halo-tiled 7x7 forward for a small channel side (bf16): AFE.in_conv 3->64 forward,
+// Generator.out_conv 64->3 forward and its 3->64 backward-data.  The block's TR x 64 output
+// pixels plus the (KS-1)-pixel halo of the input are staged in LDS ONCE (DMA, per-lane
+// source addressing, zero border from the buffer range check); every tap then reads its
+// shifted window from LDS, instead of the 49x im2col re-read of the generic path.
+//   A fragment (16 pixels x 32 k): lane (i, g) reads the 16-B chunk g of k-step ks at halo
+//   pixel (pixel i + tap offset) -> one ds_read_b128; 16-B chunks inside a pixel are XOR-
+//   swizzled by the pixel index (conflict-light reads of 128-B pixels).
+//   B fragment (weights [co][Kpad]): from LDS with padded rows (WLDS) or straight from
+//   global/L1 (3 output channels: 16 padded rows, 100 KB, cache-resident).
+// 8 waves; wave w owns pixels [w*RM*16, (w+1)*RM*16) of the tile and all RN*16 channels.
+// Requires W % 64 == 0 and H % TR == 0 (host checks).
+// ----------------------------------------------------------------------------------------
+template <int KS, int CIN, int RN, int TR, bool WLDS, bool KSPLIT>
+__global__ void __launch_bounds__(512, 4)
+conv_halo_fwd(ConvArgs a, unsigned x_bytes) {
+  constexpr int PAD = KS / 2, TW = 64;
+  constexpr int MT = TR * 4;                       // 16-pixel m-tiles per block
+  // KSPLIT: every wave owns all MT m-tiles and 1/8 of the k-steps (partials summed in LDS);
+  // otherwise wave w owns m-tiles [w*RM, (w+1)*RM) and all k-steps.
+  constexpr int RM = KSPLIT ? MT : MT / 8;
+  constexpr int HR = TR + KS - 1, HW = TW + KS - 1;
+  constexpr int CPP = CIN / 8;                     // 16-B chunks per pixel
+  constexpr int HCH = HR * HW * CPP;               // halo chunks
+  constexpr int HQ = (HCH + 63) / 64;              // 1-KB pieces
+  constexpr int KPAD = ((KS * KS * CIN + 31) / 32) * 32;
+  constexpr int NKS = KPAD / 32;
+  constexpr int KPW = (NKS + 7) / 8;               // k-steps per wave (KSPLIT)
+  constexpr int WROW = KPAD / 8 + 1;               // padded weight row (16-B chunks)
+  constexpr int WCH = RN * 16 * WROW;
+  constexpr int WQ = WLDS ? (WCH + 63) / 64 : 0;
+  constexpr int HB = HQ * 1024, WB = WQ * 1024;
+  constexpr int SCR = 4096;                        // epilogue scratch (BN partials)
+  static_assert(!KSPLIT || (RN == 1 && !WLDS && 8 * MT * 1024 <= HB), "k-split layout");
+  __shared__ __attribute__((aligned(1024))) char smem[HB + WB + SCR];
+  char* halo = smem;
+  char* wlds = smem + HB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_w = a.W / TW, tiles_h = a.H / TR;
+  const int tile = blockIdx.x;
+  const int n = tile / (tiles_h * tiles_w);
+  const int rem = tile - n * tiles_h * tiles_w;
+  const int h0 = (rem / tiles_w) * TR, w0 = (rem % tiles_w) * TW;
+  const int li = lane & 15, g = lane >> 4;
+  const bf16* __restrict__ wk = reinterpret_cast<const bf16*>(a.w);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  for (int q = wave; q < HQ; q += 8) {
+    const int L = q * 64 + lane;
+    const int hp = L / CPP, ch = L - (L / CPP) * CPP;
+    const int hr = hp / HW, hc = hp - (hp / HW) * HW;
+    const int hh = h0 + hr - PAD, ww = w0 + hc - PAD;
+    const int sc = ch ^ (hp & (CPP - 1));
+    const bool ok = L < HCH && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+    const unsigned off = ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * CIN + sc * 8) * 2) : 0x80000000u;
+    dma16(xr, halo + q * 1024, off);
+  }
+  if constexpr (WLDS) {
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
+    for (int q = wave; q < WQ; q += 8) {
+      const int L = q * 64 + lane;
+      const int row = L / WROW, ch = L - (L / WROW) * WROW;
+      const bool ok = L < WCH && ch < KPAD / 8;
+      const unsigned off = ok ? (unsigned)((row * a.Kpad + ch * 8) * 2) : 0x80000000u;
+      dma16(wr, wlds + q * 1024, off);
+    }
+  }
+  const int ks0 = KSPLIT ? wave * KPW : 0;
+  const int ks1 = KSPLIT ? min(NKS, ks0 + KPW) : NKS;
+  bf16x8 bpre[KSPLIT ? KPW : 1];
+  if constexpr (KSPLIT) {   // this wave's weight fragments, straight to registers
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      const int kc = (ks0 + j) * 4 + g;
+      bpre[j] = (ks0 + j < NKS) ? *reinterpret_cast<const bf16x8*>(wk + (long)li * a.Kpad + kc * 8) : bf16x8{};
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x4 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int j = 0; j < RM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int hbase[RM];   // halo pixel of this lane's output pixel, per m-tile (tap (0,0))
+#pragma unroll
+  for (int m = 0; m < RM; ++m) {
+    const int loc = (KSPLIT ? 0 : wave * RM * 16) + m * 16 + li;
+    hbase[m] = (loc / TW) * HW + (loc % TW);
+  }
+  auto kstep = [&](int ks, const bf16x8 (&bfr)[RN]) {
+    const int kc = ks * 4 + g;                 // this lane's 16-B k chunk
+    const int tap = kc / CPP, ch = kc - (kc / CPP) * CPP;
+    const bool kin = tap < KS * KS;
+    const int r = tap / KS, s = tap - (tap / KS) * KS;
+    const int toff = r * HW + s;
+    bf16x8 afr[RM];
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int hp = hbase[m] + toff;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(halo + (hp * CPP + (ch ^ (hp & (CPP - 1)))) * 16);
+      if (!kin) v = bf16x8{};
+      afr[m] = v;
+    }
+#pragma unroll
+    for (int nn = 0; nn < RN; ++nn)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nn], afr[m], acc[nn][m], 0, 0, 0);
+  };
+  if constexpr (KSPLIT) {
+#pragma unroll
+    for (int j = 0; j < KPW; ++j) {
+      if (ks0 + j < ks1) {
+        const bf16x8 bfr[RN] = {bpre[j]};
+        kstep(ks0 + j, bfr);
+      }
+    }
+  } else {
+#pragma unroll 2
+    for (int ks = ks0; ks < ks1; ++ks) {
+      const int kc = ks * 4 + g;
+      bf16x8 bfr[RN];
+#pragma unroll
+      for (int nn = 0; nn < RN; ++nn) {
+        if constexpr (WLDS) bfr[nn] = *reinterpret_cast<const bf16x8*>(wlds + ((nn * 16 + li) * WROW + kc) * 16);
+        else bfr[nn] = *reinterpret_cast<const bf16x8*>(wk + (long)(nn * 16 + li) * a.Kpad + kc * 8);
+      }
+      kstep(ks, bfr);
+    }
+  }
+  const int p0 = (n * a.H + h0) * a.W + w0;
+  if constexpr (KSPLIT) {
+    // sum the 8 waves' partial tiles through LDS (halo no longer needed); wave w finishes m-tile w
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(halo);
+#pragma unroll
+    for (int m = 0; m < RM; ++m) red[(wave * RM + m) * 64 + lane] = acc[0][m];
+    __syncthreads();
+    f32x4 t[1][1];
+    t[0][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t[0][0] += red[(w * RM + wave) * 64 + lane];
+    conv_epilogue<bf16, 1, 8, 1, 1>(a, t, smem + HB + WB, 0, p0, tile, 0, wave, lane, tid);
+  } else {
+    conv_epilogue<bf16, 1, 8, RN, RM>(a, acc, smem + HB + WB, 0, p0, tile, 0, wave, lane, tid);
+  }
 }
 
 // ----------------------------------------------------------------------------------------
@@ -829,7 +983,9 @@ __device__ __forceinline__ int timg_off(int row, int col) {  // col % 4 == 0
 template <int NCOL>
 __device__ __forceinline__ bf16x8 tfrag(const char* base, int r0, int cbase, int lane) {
   const int g = lane >> 4, li = lane & 15;
-  const int c = cbase + 4 * (li & 3);
+  // NCOL < 16 (8 staged channels): lanes of columns >= NCOL re-read valid columns; the
+  // caller ignores those outputs (every lane must take part in a transposed read)
+  const int c = (cbase + 4 * (li & 3)) & (NCOL >= 16 ? ~0 : NCOL - 1);
   FV_LDS char* lb = (FV_LDS char*)(base);
   const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + timg_off<NCOL>(r0 + 8 * g + (li >> 2), c)));
   const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + timg_off<NCOL>(r0 + 8 * g + 4 + (li >> 2), c)));
@@ -1017,6 +1173,158 @@ conv_wgrad_v2(Wg2Args a) {
 }
 
 // ----------------------------------------------------------------------------------------
+// Halo-tiled 7x7 weight gradient (bf16): Generator.out_conv 64->3 and AFE.in_conv 3->64.
+//   dW[co][k = (tap, ci)] = sum_p dy[p][co] * x[p + off(tap)][ci]      (M = k, N = co, K = p)
+// Persistent blocks (one per CU) walk TR x 64 pixel tiles; per tile the input halo and the
+// dy tile land in LDS by DMA (double-buffered: tile t+1 streams in while t is computed),
+// and every tap's A fragment is a transposed read (ds_read_b64_tr_b16) of the halo at the
+// tap's shift -- the input is read from HBM ~once instead of 49x.  Accumulators stay in
+// registers across tiles; one fp32 slab per block, reduced by wgrad_reduce_kernel.  The
+// bias gradient uses the all-ones A operand trick (wave 0).
+// Wave w owns n-tile (w % NT) and m-tiles w/NT, w/NT + 8/NT, ...  (NT = co tiles).
+// ----------------------------------------------------------------------------------------
+struct HaloWgArgs {
+  const void* x;
+  const void* dy;
+  float* slab;
+  float* bslab;
+  int H, W, ldd, K, KW, CW, ntiles, cout;
+  unsigned xbytes, dybytes;
+};
+
+template <int KS, int CIN, int NT, int TR>
+__global__ void __launch_bounds__(512, 2)
+conv_halo_wgrad(HaloWgArgs a) {
+  constexpr int PAD = KS / 2, TW = 64;
+  constexpr int HR = TR + KS - 1, HW = TW + KS - 1;
+  constexpr int CPP = CIN / 8;
+  constexpr int HCH = HR * HW * CPP;
+  constexpr int HQ = (HCH + 63) / 64;
+  constexpr int LDD = NT == 1 ? 8 : NT * 16;       // dy channels staged per pixel
+  constexpr int DCH = TR * TW * LDD / 8;
+  constexpr int DQ = (DCH + 63) / 64;
+  constexpr int HB = HQ * 1024, DB = DQ * 1024, BUF = HB + DB;
+  constexpr int KT = KS * KS * CIN;                 // valid k
+  constexpr int MTT = (KT + 15) / 16;               // m-tiles (16 k rows)
+  constexpr int WPN = 8 / NT;                       // waves per n-tile
+  constexpr int RMW = (MTT + WPN - 1) / WPN;        // m-tiles per wave (max)
+  constexpr int NKG = TR * TW / 32;                 // 32-pixel k-groups per tile
+  __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nt = wave % NT, mw = wave / NT;
+  const int li = lane & 15, g = lane >> 4, q4 = li >> 2, pp = li & 3;
+  const int tiles_w = a.W / TW, tiles_h = a.H / TR;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), 0, (int)a.dybytes, 0x00020000);
+
+  auto issue = [&](int tile, int buf) {
+    const int n = tile / (tiles_h * tiles_w);
+    const int rem = tile - n * tiles_h * tiles_w;
+    const int h0 = (rem / tiles_w) * TR, w0 = (rem % tiles_w) * TW;
+    char* halo = smem + buf * BUF;
+    char* dys = halo + HB;
+    for (int q = wave; q < HQ; q += 8) {
+      const int L = q * 64 + lane;
+      const int hp = L / CPP, ch = L - (L / CPP) * CPP;
+      const int hr = hp / HW, hc = hp - (hp / HW) * HW;
+      const int hh = h0 + hr - PAD, ww = w0 + hc - PAD;
+      const int sc = ch ^ (hp & (CPP - 1));
+      const bool ok = L < HCH && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+      const unsigned off = ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * CIN + sc * 8) * 2) : 0x80000000u;
+      dma16(xr, halo + q * 1024, off);
+    }
+    for (int q = wave; q < DQ; q += 8) {
+      const int L = q * 64 + lane;
+      constexpr int CPR = LDD / 8;
+      const int row = L / CPR, dch = L - (L / CPR) * CPR;
+      const int sc = CPR >= 4 ? ((((dch >> 1) ^ tswz<LDD>(row)) << 1) | (dch & 1)) : dch;
+      const int p = (n * a.H + h0 + row / TW) * a.W + w0 + (row % TW);
+      const bool ok = L < DCH && sc * 8 < a.ldd;
+      const unsigned off = ok ? (unsigned)((p * a.ldd + sc * 8) * 2) : 0x80000000u;
+      dma16(dr, dys + q * 1024, off);
+    }
+  };
+
+  // this lane's constant part of each A fragment: (tap offset, byte offset in the pixel)
+  int aoff[RMW], akx[RMW];
+  bool aok[RMW];
+#pragma unroll
+  for (int j = 0; j < RMW; ++j) {
+    const int mt = mw + j * WPN;
+    const int k = mt * 16 + 4 * pp;                 // first of this lane's 4 k (same tap, same chunk)
+    const int tap = k / CIN, ci = k - (k / CIN) * CIN;
+    const int r = tap / KS, s = tap - (tap / KS) * KS;
+    aok[j] = mt < MTT;                              // wave-uniform (transposed reads need EXEC = all)
+    aoff[j] = k < KT ? r * HW + s : 0;              // k >= K rows: finite junk, never stored
+    akx[j] = k < KT ? ci : 0;
+  }
+  f32x4 acc[RMW];
+#pragma unroll
+  for (int j = 0; j < RMW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bslab && wave < NT;
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+
+  auto compute = [&](int buf) {
+    const char* halo = smem + buf * BUF;
+    const char* dys = halo + HB;
+    FV_LDS char* hl = (FV_LDS char*)(halo);
+    for (int kg = 0; kg < NKG; ++kg) {
+      // B: dy[32 px][16 co] of n-tile nt
+      const bf16x8 bfr = tfrag<LDD>(dys, kg * 32, nt * 16, lane);   // co >= LDD lanes: ignored
+      // pixel rows 8g+q4 and 8g+4+q4 of this k-group -> halo pixel at tap (0,0)
+      const int p0 = kg * 32 + 8 * g + q4, p1 = p0 + 4;
+      const int hb0 = (p0 / TW) * HW + (p0 % TW), hb1 = (p1 / TW) * HW + (p1 % TW);
+#pragma unroll
+      for (int j = 0; j < RMW; ++j) {
+        bf16x8 af = bf16x8{};
+        if (aok[j]) {
+          const int ha = hb0 + aoff[j], hb = hb1 + aoff[j];
+          const int ca = ((akx[j] >> 3) ^ (ha & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
+          const int cb = ((akx[j] >> 3) ^ (hb & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
+          const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + ha * CIN * 2 + ca));
+          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + hb * CIN * 2 + cb));
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+          af = __builtin_bit_cast(bf16x8, v);
+        }
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[j], 0, 0, 0);
+      }
+      if (do_bias) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr, accb, 0, 0, 0);
+    }
+  };
+
+  int tile = blockIdx.x;
+  if (tile < a.ntiles) issue(tile, 0);
+  for (int it = 0; tile < a.ntiles; ++it, tile += gridDim.x) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (tile + (int)gridDim.x < a.ntiles) issue(tile + gridDim.x, (it + 1) & 1);
+    compute(it & 1);
+  }
+
+  // D[k][co]: lane holds k = mt*16 + 4*(lane>>4) + i for co = nt*16 + (lane & 15)
+  float* slab = a.slab + (long)blockIdx.x * a.CW * a.KW;
+  const int co = nt * 16 + li;
+  if (co < a.cout) {
+#pragma unroll
+    for (int j = 0; j < RMW; ++j) {
+      const int mt = mw + j * WPN;
+      if (mt < MTT)
+        *reinterpret_cast<float4*>(slab + (long)co * a.KW + mt * 16 + g * 4) =
+            make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    }
+    if (do_bias && g == 0) a.bslab[(long)blockIdx.x * a.CW + co] = accb[0];
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // weight re-layout (+ 1/sigma) and slab reduction
 // ----------------------------------------------------------------------------------------
 template <typename T>
@@ -1042,25 +1350,53 @@ __global__ void weight_prep_kernel(const float* __restrict__ wp, const float* si
   }
 }
 
+// sum of the per-split slabs -> dW in the reference layout [co][ci][r][s] (+ db).  Block =
+// 64 consecutive outputs x 4 split lanes (4 independent partial sums each), so that large
+// split counts do not serialise on load latency; blocks >= nb_main reduce the bias slab.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
                                     float* dw, float* db, int nsplit, int CW, int KW, int K,
-                                    int cout, int cin_valid, int lgCin, int KS) {
-  const long total = (long)cout * K;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(e / K), k = (int)(e - (long)co * K);
+                                    int cout, int cin_valid, int lgCin, int KS, int nb_main) {
+  const int sg = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __shared__ float red[4][64];
+  float g = 0.f;
+  bool valid;
+  long dst = 0;
+  const float* p = nullptr;
+  long stride;
+  if ((int)blockIdx.x < nb_main) {
+    const long e = (long)blockIdx.x * 64 + l;
+    const int co = (int)(e / K), k = (int)(e - (e / K) * K);
     const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
-    if (c >= cin_valid) continue;
-    float g = 0.f;
-    for (int s = 0; s < nsplit; ++s) g += slab[((long)s * CW + co) * KW + k];
+    valid = e < (long)cout * K && c < cin_valid;
     const int r = tap / KS, sx = tap - (tap / KS) * KS;
-    dw[(((long)co * cin_valid + c) * KS + r) * KS + sx] = g;
+    dst = (((long)co * cin_valid + c) * KS + r) * KS + sx;
+    p = slab + (long)co * KW + k;
+    stride = (long)CW * KW;
+  } else {
+    const int co = ((int)blockIdx.x - nb_main) * 64 + l;
+    valid = db != nullptr && co < cout;
+    dst = co;
+    p = bslab + co;
+    stride = CW;
   }
-  if (db && blockIdx.x == 0) {
-    for (int co = threadIdx.x; co < cout; co += blockDim.x) {
-      float g = 0.f;
-      for (int s = 0; s < nsplit; ++s) g += bslab[(long)s * CW + co];
-      db[co] = g;
+  if (valid) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = sg;
+    for (; s + 12 < nsplit; s += 16) {
+      a0 += p[(long)s * stride];
+      a1 += p[(long)(s + 4) * stride];
+      a2 += p[(long)(s + 8) * stride];
+      a3 += p[(long)(s + 12) * stride];
     }
+    for (; s < nsplit; s += 4) a0 += p[(long)s * stride];
+    g = (a0 + a1) + (a2 + a3);
+  }
+  red[sg][l] = g;
+  __syncthreads();
+  if (sg == 0 && valid) {
+    const float t = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    if ((int)blockIdx.x < nb_main) dw[dst] = t;
+    else db[dst] = t;
   }
 }
 
@@ -1205,7 +1541,16 @@ int check_desc(const fv_conv_desc* d) {
 
 int kpad_of(int ks, int cin) { return fv_cdiv((long)ks * ks * cin, BK) * BK; }
 
-// wgrad plan: v2 (bf16 DMA-fed, 8 waves) or the register-staged v1 (fp32 / BN prologue)
+// 7x7 halo wgrad: in_conv (cin 8 -> 64, dy stride 64) or out_conv (cin 64 -> cout <= 8, dy stride 8)
+static int halo_wg_tr(const fv_conv_desc* d) {
+  if (d->ksize != 7 || d->upsample || d->pro_act || d->w % 64) return 0;
+  int tr = 0;
+  if (d->cin == 8 && d->cout == 64) tr = 4;
+  else if (d->cin == 64 && d->cout <= 8) tr = 2;
+  return (tr && d->h % tr == 0) ? tr : 0;
+}
+
+// wgrad plan: v2 (bf16 DMA-fed, 8 waves), halo (7x7), or the register-staged v1 (fp32 / BN prologue)
 struct WgPlan {
   int v2, bkt, bc, px, ntk, ntc, nsplit, nsteps, sps, KW, CW;
 };
@@ -1221,6 +1566,23 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
   p.v2 = !g_disable_wg2 && d->dtype == FV_BF16 && !d->pro_act && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
          P * 256 * 2 < (1L << 31);
+  // 7x7 halo path (v2 == 2): one persistent block per CU, ntk = 1 (all k in one tile)
+  const int htr = halo_wg_tr(d);
+  if (p.v2 && htr) {
+    const int nt = d->cin == 8 ? 4 : 1;
+    p.v2 = 2;
+    p.bkt = fv_cdiv(K, 16) * 16;
+    p.bc = nt * 16;
+    p.px = htr * 64;
+    p.ntk = 1;
+    p.ntc = 1;
+    p.nsteps = (int)(P / p.px);                  // pixel tiles
+    p.nsplit = p.nsteps < 256 ? p.nsteps : 256;  // persistent blocks
+    p.sps = fv_cdiv(p.nsteps, p.nsplit);
+    p.KW = p.bkt;
+    p.CW = p.bc;
+    return p;
+  }
   if (p.v2) {
     p.bc = d->cout > 128 ? 256 : d->cout > 64 ? 128 : d->cout > 16 ? 64 : 16;
     if (p.bc == 64) p.bkt = 128;
@@ -1237,6 +1599,7 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   p.nsteps = fv_cdiv(P, p.px);
   const int ntile = p.ntk * p.ntc;
   int ns = p.v2 ? (256 + ntile / 2) / ntile : 768 / ntile;
+  if (p.v2 && ns > 64 && (long)p.bc * p.bkt * ntile * ns * 4 > (32L << 20)) ns = 64;   // slab <= ~32 MB
   if (ns < 1) ns = 1;
   if (ns > p.nsteps) ns = p.nsteps;
   p.sps = fv_cdiv(p.nsteps, ns);
@@ -1329,7 +1692,27 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   return (size_t)fv_cdiv(d->cin, t.bn) * t.bn * kpad_of(d->ksize, cin_t);
 }
 
-static FwdTile plan_tile(const fv_conv_desc* d) { return use_v2(d) ? fwd_tile_v2(d->cout) : fwd_tile(d->cout); }
+// 7x7 halo path: (cin 8 -> cout 64, TR 8, weights in LDS) or (cin 64 -> cout <= 16, TR 2)
+static int g_disable_halo = -1;
+static int halo_tr(const fv_conv_desc* d) {
+  if (g_disable_halo < 0) {
+    const char* e = getenv("FV_DISABLE_HALO");
+    g_disable_halo = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_disable_halo || d->dtype != FV_BF16 || d->ksize != 7 || d->pro_act || d->upsample || d->w % 64) return 0;
+  int tr = 0;
+  if (d->cin == 8 && d->cout == 64) tr = 4;
+  else if (d->cin == 64 && d->cout <= 16) tr = 2;
+  if (!tr || d->h % tr) return 0;
+  if ((long)d->n * d->h * d->w * d->cin * 2 >= (1L << 31)) return 0;
+  return tr;
+}
+
+static FwdTile plan_tile(const fv_conv_desc* d) {
+  const int tr = halo_tr(d);
+  if (tr) return {d->cout <= 16 ? 16 : 64, tr * 64};
+  return use_v2(d) ? fwd_tile_v2(d->cout) : fwd_tile(d->cout);
+}
 
 int fv_conv2d_stats_block_pixels(const fv_conv_desc* d) { return plan_tile(d).bm; }
 
@@ -1391,6 +1774,16 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   a.sigmoid = d->epi_sigmoid; a.nchw = d->out_nchw_f32;
   a.ntn = fv_cdiv(d->cout, t.bn);
   int st;
+  if (const int tr = halo_tr(d)) {
+    a.lgtw = 6;
+    const int nblk = d->n * (d->h / tr) * (d->w / 64);
+    const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
+    if (d->cin == 8)
+      hipLaunchKernelGGL((conv_halo_fwd<7, 8, 4, 4, true, false>), dim3(nblk), dim3(512), 0, s, a, xb);
+    else
+      hipLaunchKernelGGL((conv_halo_fwd<7, 64, 1, 2, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
+    return fv_check_launch("conv2d_fwd_halo");
+  }
   if (use_v2(d)) {
     const FwdTile t2 = fwd_tile_v2(d->cout);
     a.ntn = fv_cdiv(d->cout, t2.bn);
@@ -1471,6 +1864,21 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
   const WgPlan t = plan_wgrad(d);
   const int Hin = d->upsample ? d->h / 2 : d->h, Win = d->upsample ? d->w / 2 : d->w;
   const long P = (long)d->n * d->h * d->w;
+  if (t.v2 == 2) {
+    const int ldd_need = d->cin == 8 ? 64 : 8;
+    FV_REQUIRE(ldy_dy == ldd_need, "wgrad (7x7 halo): dy channel stride must be %d (got %d)", ldd_need, ldy_dy);
+    HaloWgArgs a{};
+    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+    a.H = d->h; a.W = d->w; a.ldd = ldy_dy; a.K = d->ksize * d->ksize * d->cin;
+    a.KW = t.KW; a.CW = t.CW; a.ntiles = t.nsteps; a.cout = d->cout;
+    a.xbytes = (unsigned)(P * d->cin * 2);
+    a.dybytes = (unsigned)(P * ldy_dy * 2);
+    if (d->cin == 8)
+      hipLaunchKernelGGL((conv_halo_wgrad<7, 8, 4, 4>), dim3(t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL((conv_halo_wgrad<7, 64, 1, 2>), dim3(t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    return fv_check_launch("conv2d_bwd_weight_halo");
+  }
   if (t.v2) {
     FV_REQUIRE(P * ldy_dy * 2 < (1L << 31), "wgrad: dy larger than 2 GB");
     Wg2Args a{};
@@ -1525,10 +1933,11 @@ int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float
   const WgPlan t = plan_wgrad(d);
   const int K = d->ksize * d->ksize * d->cin;
   const long tot = (long)d->cout * K;
-  const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 8192);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, slab, bias_slab,
-                     dw_param, db, t.nsplit, t.CW, t.KW, K, d->cout, d->cin_valid, fv_ilog2(d->cin),
-                     d->ksize);
+  const int nb_main = fv_cdiv(tot, 64);
+  const int nb_bias = db ? fv_cdiv(d->cout, 64) : 0;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb_main + nb_bias), dim3(256), 0, (hipStream_t)stream, slab,
+                     bias_slab, dw_param, db, t.nsplit, t.CW, t.KW, K, d->cout, d->cin_valid, fv_ilog2(d->cin),
+                     d->ksize, nb_main);
   return fv_check_launch("wgrad_reduce");
 }
 

@@ -56,6 +56,9 @@ CONV_CASES = [
     (3, 128, 64, 10, 6, True, False),
     (7, 64, 3, 9, 13, False, False),
     (1, 512, 256, 6, 10, False, False),
+    # 7x7 halo path (bf16, W % 64 == 0): in_conv shape, out_conv shape (+ its dgrad)
+    (7, 3, 64, 16, 64, False, False),
+    (7, 64, 3, 8, 128, False, False),
 ]
 
 

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU tests + bench + rocprofv3 kernel-trace summary of the bench.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-it}
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+echo "pytest exit $?" >> gpurun_out/pytest_gpu.log
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || exit 1
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --cpu-seconds 0 > $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log 2>&1
