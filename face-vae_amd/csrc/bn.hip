@@ -158,101 +158,109 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
   if (shift) shift[c] = b - (float)mean * sc;
 }
 
-// out = [pool](act(y*scale+shift)); one thread per (out pixel, 8-channel chunk)
+// out = [pool](act(y*scale+shift)).  grid.y = output row (n*Ho + i), grid.x covers the row's
+// (pixel, 8-channel chunk) pairs: 32-bit shift/mask indexing only.
 template <typename T>
-__global__ void act_fwd_kernel(const T* __restrict__ y, int N, int H, int W, int C, int ldc,
+__global__ void act_fwd_kernel(const T* __restrict__ y, int W, int C, int ldc, int lgcpc,
                                const float* __restrict__ scale, const float* __restrict__ shift,
-                               float slope, int pool, T* out) {
-  const int cpc = C / 8;
-  const int Ho = pool ? H / 2 : H, Wo = pool ? W / 2 : W;
-  const long total = (long)N * Ho * Wo * cpc;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(e % cpc);
-    const long po = e / cpc;
-    const int c = cg * 8;
-    float sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { sc[j] = scale[c + j]; sh[j] = shift[c + j]; }
-    float o[8];
-    if (!pool) {
-      float f[8];
-      ld8<T>(y + po * ldc + c, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = fv_act(f[j] * sc[j] + sh[j], slope);
-    } else {
-      const int n = (int)(po / (Ho * Wo));
-      const int rem = (int)(po - (long)n * Ho * Wo);
-      const int i = rem / Wo, jx = rem - i * Wo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = 0.f;
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          float f[8];
-          ld8<T>(y + ((long)(n * H + 2 * i + dy) * W + 2 * jx + dx) * ldc + c, f);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += fv_act(f[j] * sc[j] + sh[j], slope);
-        }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] *= 0.25f;
-    }
-    st8<T>(out + po * C + c, o);
+                               float slope, int pool, T* __restrict__ out) {
+  const int Wo = pool ? W >> 1 : W;
+  const int e = blockIdx.x * NTH + threadIdx.x;
+  if (e >= (Wo << lgcpc)) return;
+  const int row = blockIdx.y;
+  const int j = e >> lgcpc, c = (e & ((1 << lgcpc) - 1)) * 8;
+  float sc[8], sh[8];
+  {
+    const float4 a0 = *reinterpret_cast<const float4*>(scale + c), a1 = *reinterpret_cast<const float4*>(scale + c + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(shift + c), b1 = *reinterpret_cast<const float4*>(shift + c + 4);
+    sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+    sh[0] = b0.x; sh[1] = b0.y; sh[2] = b0.z; sh[3] = b0.w; sh[4] = b1.x; sh[5] = b1.y; sh[6] = b1.z; sh[7] = b1.w;
   }
+  float o[8];
+  if (!pool) {
+    float f[8];
+    ld8<T>(y + (size_t)(row * W + j) * ldc + c, f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = fv_act(f[q] * sc[q] + sh[q], slope);
+  } else {
+    float f0[8], f1[8], f2[8], f3[8];
+    const size_t r0 = (size_t)(2 * row) * W + 2 * j, r1 = r0 + W;
+    ld8<T>(y + r0 * ldc + c, f0);
+    ld8<T>(y + (r0 + 1) * ldc + c, f1);
+    ld8<T>(y + r1 * ldc + c, f2);
+    ld8<T>(y + (r1 + 1) * ldc + c, f3);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      o[q] = 0.25f * ((fv_act(f0[q] * sc[q] + sh[q], slope) + fv_act(f1[q] * sc[q] + sh[q], slope)) +
+                      (fv_act(f2[q] * sc[q] + sh[q], slope) + fv_act(f3[q] * sc[q] + sh[q], slope)));
+  }
+  st8<T>(out + (size_t)(row * Wo + j) * C + c, o);
 }
 
-// g at a full-resolution pixel (n,h,w), 8 channels; pooled dout is [N][H/2][W/2][C]
+// per-thread copy of one 8-channel chunk's BN parameters
+struct BnChunk {
+  float mean[8], inv[8], gam[8], bet[8];
+  __device__ __forceinline__ void load(const float* m, const float* iv, const float* g, const float* b, int c) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      mean[q] = m[c + q];
+      inv[q] = iv[c + q];
+      gam[q] = g[c + q];
+      bet[q] = b[c + q];
+    }
+  }
+};
+
+// g = dout_full * act'(gamma*yhat + beta) at pixel p (pooled dout: [P/4][C], 0.25 per tap)
 template <typename T>
-__device__ __forceinline__ void grad_g(const T* dout, const T* y, long p, int n, int h, int w, int H,
-                                       int W, int C, int ldc, int c, int pool, const float* mean,
-                                       const float* invstd, const float* gamma, const float* beta,
-                                       float slope, float* g, float* yh) {
+__device__ __forceinline__ void grad_g(const T* dout, const T* y, int p, FastDiv fw, int W, int C, int ldc,
+                                       int c, int pool, const BnChunk& bp, float slope, float* g, float* yh) {
   float d[8], v[8];
   if (pool) {
-    ld8<T>(dout + ((long)(n * (H / 2) + h / 2) * (W / 2) + w / 2) * C + c, d);
+    const int hr = (int)fdiv((uint32_t)p, fw);            // n*H + h
+    const int w = p - hr * W;
+    ld8<T>(dout + (size_t)((hr >> 1) * (W >> 1) + (w >> 1)) * C + c, d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] *= 0.25f;
+    for (int q = 0; q < 8; ++q) d[q] *= 0.25f;
   } else {
-    ld8<T>(dout + p * ldc + c, d);
+    ld8<T>(dout + (size_t)p * ldc + c, d);
   }
-  ld8<T>(y + p * ldc + c, v);
+  ld8<T>(y + (size_t)p * ldc + c, v);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    yh[j] = (v[j] - mean[c + j]) * invstd[c + j];
-    const float z = gamma[c + j] * yh[j] + beta[c + j];
-    g[j] = z > 0.f ? d[j] : d[j] * slope;
+  for (int q = 0; q < 8; ++q) {
+    yh[q] = (v[q] - bp.mean[q]) * bp.inv[q];
+    const float z = bp.gam[q] * yh[q] + bp.bet[q];
+    g[q] = z > 0.f ? d[q] : d[q] * slope;
   }
 }
 
 template <typename T>
-__global__ void act_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ y, int N, int H,
+__global__ void act_bwd_reduce_kernel(const T* __restrict__ dout, const T* __restrict__ y, int P, FastDiv fw,
                                       int W, int C, int ldc, const float* mean, const float* invstd,
                                       const float* gamma, const float* beta, float slope, int pool,
                                       double* ws) {
   const int tpp = C / 8;
   const int rows = NTH / tpp;
   const int cg = threadIdx.x % tpp, row = threadIdx.x / tpp;
-  const long P = (long)N * H * W;
-  float s[8], q[8];
+  BnChunk bp;
+  bp.load(mean, invstd, gamma, beta, cg * 8);
+  float s[8], q2[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
-  for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
-    const int n = (int)(p / ((long)H * W));
-    const int rem = (int)(p - (long)n * H * W);
-    const int h = rem / W, w = rem - h * W;
+  for (int j = 0; j < 8; ++j) s[j] = q2[j] = 0.f;
+  for (int p = blockIdx.x * rows + row; p < P; p += gridDim.x * rows) {
     float g[8], yh[8];
-    grad_g<T>(dout, y, p, n, h, w, H, W, C, ldc, cg * 8, pool, mean, invstd, gamma, beta, slope, g, yh);
+    grad_g<T>(dout, y, p, fw, W, C, ldc, cg * 8, pool, bp, slope, g, yh);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       s[j] += g[j];
-      q[j] += g[j] * yh[j];
+      q2[j] += g[j] * yh[j];
     }
   }
   __shared__ float ss[2][NTH * 8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     ss[0][row * C + cg * 8 + j] = s[j];
-    ss[1][row * C + cg * 8 + j] = q[j];
+    ss[1][row * C + cg * 8 + j] = q2[j];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += NTH) {
@@ -277,30 +285,37 @@ __global__ void bwd_finalize_kernel(const double* red, int C, double count, floa
   k[C + c] = (float)(sgy / count);
 }
 
+// dx = gamma*invstd*(g - k0 - yhat*k1) [+ addend]; thread = (pixel, 8-channel chunk), the
+// grid stride is a multiple of C/8 so each thread keeps one chunk's parameters in registers
 template <typename T>
-__global__ void act_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ y, int N, int H,
-                                     int W, int C, int ldc, const float* mean, const float* invstd,
+__global__ void act_bwd_apply_kernel(const T* __restrict__ dout, const T* __restrict__ y, int P, FastDiv fw,
+                                     int W, int C, int ldc, int lgcpc, const float* mean, const float* invstd,
                                      const float* gamma, const float* beta, float slope, int pool,
-                                     const float* __restrict__ k, const T* addend, T* dx) {
-  const int cpc = C / 8;
-  const long total = (long)N * H * W * cpc;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(e % cpc);
-    const long p = e / cpc;
-    const int c = cg * 8;
-    const int n = (int)(p / ((long)H * W));
-    const int rem = (int)(p - (long)n * H * W);
-    const int h = rem / W, w = rem - h * W;
-    float g[8], yh[8], o[8];
-    grad_g<T>(dout, y, p, n, h, w, H, W, C, ldc, c, pool, mean, invstd, gamma, beta, slope, g, yh);
-    float ad[8];
-    if (addend) ld8<T>(addend + p * ldc + c, ad);
+                                     const float* __restrict__ k, const T* __restrict__ addend, T* __restrict__ dx) {
+  const int total = P << lgcpc;
+  const int e0 = blockIdx.x * NTH + threadIdx.x;
+  const int c = (e0 & ((1 << lgcpc) - 1)) * 8;
+  BnChunk bp;
+  bp.load(mean, invstd, gamma, beta, c);
+  float k0[8], k1[8], gi[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      o[j] = gamma[c + j] * invstd[c + j] * (g[j] - k[c + j] - yh[j] * k[C + c + j]);
-      if (addend) o[j] += ad[j];
+  for (int q = 0; q < 8; ++q) {
+    k0[q] = k[c + q];
+    k1[q] = k[C + c + q];
+    gi[q] = bp.gam[q] * bp.inv[q];
+  }
+  for (int e = e0; e < total; e += gridDim.x * NTH) {
+    const int p = e >> lgcpc;
+    float g[8], yh[8], o[8];
+    grad_g<T>(dout, y, p, fw, W, C, ldc, c, pool, bp, slope, g, yh);
+    float ad[8];
+    if (addend) ld8<T>(addend + (size_t)p * ldc + c, ad);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[q] = gi[q] * (g[q] - k0[q] - yh[q] * k1[q]);
+      if (addend) o[q] += ad[q];
     }
-    st8<T>(dx + p * ldc + c, o);
+    st8<T>(dx + (size_t)p * ldc + c, o);
   }
 }
 
@@ -374,14 +389,18 @@ int fv_bn_act_fwd(int dtype, const void* y, int n, int h, int w, int c, int ldc,
   int st = check_c(c, ldc);
   if (st) return st;
   FV_REQUIRE(!pool || (h % 2 == 0 && w % 2 == 0), "pool needs even h, w");
-  const long work = (long)n * (pool ? h / 2 : h) * (pool ? w / 2 : w) * (c / 8);
+  FV_REQUIRE((long)n * h * w * ldc < (1L << 31), "bn: tensor too large for 32-bit indexing");
+  const int lgcpc = fv_ilog2(c / 8);
+  const int ho = pool ? h / 2 : h, wo = pool ? w / 2 : w;
+  FV_REQUIRE(n * ho <= 65535, "bn: too many rows");
+  const dim3 grid(fv_cdiv((long)wo << lgcpc, NTH), n * ho);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(act_fwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)y, n, h, w, c,
-                       ldc, scale, shift, slope, pool, (bf16*)out);
+    hipLaunchKernelGGL(act_fwd_kernel<bf16>, grid, dim3(NTH), 0, s, (const bf16*)y, w, c, ldc, lgcpc, scale, shift,
+                       slope, pool, (bf16*)out);
   else
-    hipLaunchKernelGGL(act_fwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)y, n, h, w, c,
-                       ldc, scale, shift, slope, pool, (float*)out);
+    hipLaunchKernelGGL(act_fwd_kernel<float>, grid, dim3(NTH), 0, s, (const float*)y, w, c, ldc, lgcpc, scale,
+                       shift, slope, pool, (float*)out);
   return fv_check_launch("bn_act_fwd");
 }
 
@@ -392,13 +411,16 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
   if (st) return st;
   FV_REQUIRE(!pool || ldc == c, "pooled bwd needs dense channels");
   hipStream_t s = (hipStream_t)stream;
+  FV_REQUIRE((long)n * h * w * ldc < (1L << 31), "bn: tensor too large for 32-bit indexing");
   const int nb = stream_blocks((long)n * h * w, c);
+  const int P = n * h * w;
+  const FastDiv fw = make_fastdiv((uint32_t)w);
   if (dtype == FV_BF16)
     hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
-                       (const bf16*)y, n, h, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+                       (const bf16*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   else
     hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
-                       (const float*)y, n, h, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+                       (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
   hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, 2, c,
                      red);
@@ -419,15 +441,18 @@ int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h
   int st = check_c(c, ldc);
   if (st) return st;
   FV_REQUIRE(!pool || ldc == c, "pooled bwd needs dense channels");
+  FV_REQUIRE((long)n * h * w * ldc < (1L << 31), "bn: tensor too large for 32-bit indexing");
   const long work = (long)n * h * w * (c / 8);
+  const int P = n * h * w, lgcpc = fv_ilog2(c / 8);
+  const FastDiv fw = make_fastdiv((uint32_t)w);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(act_bwd_apply_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)dout,
-                       (const bf16*)y, n, h, w, c, ldc, mean, invstd, gamma, beta, slope, pool, k,
+    hipLaunchKernelGGL(act_bwd_apply_kernel<bf16>, dim3(grid_for(work, 16384)), dim3(NTH), 0, s, (const bf16*)dout,
+                       (const bf16*)y, P, fw, w, c, ldc, lgcpc, mean, invstd, gamma, beta, slope, pool, k,
                        (const bf16*)addend, (bf16*)dx);
   else
-    hipLaunchKernelGGL(act_bwd_apply_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)dout,
-                       (const float*)y, n, h, w, c, ldc, mean, invstd, gamma, beta, slope, pool, k,
+    hipLaunchKernelGGL(act_bwd_apply_kernel<float>, dim3(grid_for(work, 16384)), dim3(NTH), 0, s, (const float*)dout,
+                       (const float*)y, P, fw, w, c, ldc, lgcpc, mean, invstd, gamma, beta, slope, pool, k,
                        (const float*)addend, (float*)dx);
   return fv_check_launch("bn_bwd_apply");
 }

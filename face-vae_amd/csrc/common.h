@@ -96,3 +96,17 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// ------------------------------------------------------------------------------------
+// unsigned division by a run-time constant (host precomputes m, s); exact for n < 2^31
+// ------------------------------------------------------------------------------------
+struct FastDiv {
+  uint32_t m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t s = 0;
+  while ((1u << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return {(uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (__umulhi(n, f.m) + n) >> f.s; }

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -453,7 +454,12 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
   const int lrow = lane >> 3, lchk = lane & 7;
-  int rh[JA], rw[JA], rb[JA];
+  // per-piece constants.  Non-upsampled: the element offset of this lane's chunk at tap
+  // (0,0) plus a bitmask of the taps that stay inside the image, so a k-step costs one add
+  // and one bit test per piece (the tap offset is wave-uniform).
+  typedef typename std::conditional<(KS * KS > 32), unsigned long long, unsigned>::type TapMask;
+  int rh[JA], rw[JA], rb[JA], pbase[JA];
+  TapMask tmask[JA];
   bool rv[JA];
 #pragma unroll
   for (int j = 0; j < JA; ++j) {
@@ -464,44 +470,56 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     rh[j] = rem / a.W;
     rw[j] = rem - rh[j] * a.W;
     rb[j] = n * a.Hin * a.Win;
+    const int row = q * 8 + lrow;
+    pbase[j] = ((rb[j] + rh[j] * a.Win + rw[j]) << a.lgCin) + ((lchk ^ swz8(row)) << 3);
+    TapMask m = 0;
+    if (!UPS && rv[j]) {
+#pragma unroll
+      for (int r = 0; r < KS; ++r)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int hh = rh[j] + r - PAD, ww = rw[j] + s - PAD;
+          if (hh >= 0 && hh < a.Hin && ww >= 0 && ww < a.Win) m |= (TapMask)1 << (r * KS + s);
+        }
+    }
+    tmask[j] = m;
+  }
+  int wbase[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    const int row = (wave + j * NW) * 8 + lrow;
+    wbase[j] = ((co0 + row) * a.Kpad + ((lchk ^ swz8(row)) << 3)) * 2;
   }
 
   auto issue = [&](int ks, int buf) {
     const int k0 = ks * BK2;
     const int tap = k0 >> a.lgCin, ci0 = k0 & (a.Cin - 1);
     const int r = tap / KS, s = tap - (tap / KS) * KS;
+    const int tapoff = (((r - PAD) * a.Win + (s - PAD)) << a.lgCin) + ci0;
     char* As = smem + buf * STAGE;
     char* Bs = As + BM * ROWB;
 #pragma unroll
     for (int j = 0; j < JA; ++j) {
       const int q = wave + j * NW;
       if (QA % NW == 0 || q < QA) {
-        const int row = q * 8 + lrow;
-        const int ci = ci0 + ((lchk ^ swz8(row)) << 3);
-        const int hh = rh[j] + r - PAD, ww = rw[j] + s - PAD;
-        bool ok = rv[j];
-        int hs, ws;
+        unsigned off;
         if constexpr (UPS) {
-          ok = ok && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-          hs = hh >> 1;
-          ws = ww >> 1;
+          const int row = q * 8 + lrow;
+          const int ci = ci0 + ((lchk ^ swz8(row)) << 3);
+          const int hh = rh[j] + r - PAD, ww = rw[j] + s - PAD;
+          const bool ok = rv[j] && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+          off = ok ? ((unsigned)((rb[j] + (hh >> 1) * a.Win + (ww >> 1)) << a.lgCin) + (unsigned)ci) * 2u
+                   : 0x80000000u;
         } else {
-          ok = ok && hh >= 0 && hh < a.Hin && ww >= 0 && ww < a.Win;
-          hs = hh;
-          ws = ww;
+          off = ((tmask[j] >> tap) & 1) ? (unsigned)(pbase[j] + tapoff) * 2u : 0x80000000u;
         }
-        const unsigned off = ok ? ((unsigned)((rb[j] + hs * a.Win + ws) << a.lgCin) + (unsigned)ci) * 2u : 0x80000000u;
         dma16(xr, As + q * 1024, off);
       }
     }
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
       const int q = wave + j * NW;
-      if (QB % NW == 0 || q < QB) {
-        const int row = q * 8 + lrow;
-        const unsigned woff = (unsigned)(((co0 + row) * a.Kpad + k0 + ((lchk ^ swz8(row)) << 3)) * 2);
-        dma16(wr, Bs + q * 1024, woff);
-      }
+      if (QB % NW == 0 || q < QB) dma16(wr, Bs + q * 1024, (unsigned)(wbase[j] + k0 * 2));
     }
   };
 
@@ -944,17 +962,6 @@ conv_wgrad_kernel(WgArgs a) {
 // The bias gradient sum_p dy[p][co] rides along as one extra MFMA per co tile with an
 // all-ones A operand (k-tile-0 blocks, k-wave 0 only).  Output: per-split fp32 slabs.
 // ----------------------------------------------------------------------------------------
-struct FastDiv {
-  uint32_t m, s;
-};
-FastDiv make_fastdiv(uint32_t d) {  // host side; exact for numerators < 2^31
-  uint32_t s = 0;
-  while ((1u << s) < d) ++s;
-  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
-  return {(uint32_t)m, s};
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (__umulhi(n, f.m) + n) >> f.s; }
-
 struct Wg2Args {
   const void* x;
   const void* dy;
@@ -963,8 +970,9 @@ struct Wg2Args {
   int H, W, Hin, Win, P;
   int lgCin, K, KW, ldd, CW;
   int ntk, ntc, nsteps, sps;
-  FastDiv fhw, fw;
+  FastDiv fhw, fw, fh;
   unsigned xbytes, dybytes;
+  int rowal;   // W % PX == 0: each stage lies in one image row
 };
 
 // 32-B-block XOR of a [row][NCOL] bf16 image: the 8 rows {0-3, 8-11} (and {4-7, 12-15}) one
@@ -1065,15 +1073,31 @@ conv_wgrad_v2(Wg2Args a) {
     const int pbase = (s_begin + st) * PX;
     char* As = smem + buf * STAGE;
     char* Bs = As + SA;
+    // row-aligned stages (W % PX == 0): the whole stage is one image row segment, so the
+    // pixel decode is wave-uniform scalar work
+    int sn = 0, sh = 0, sw0 = 0;
+    if (a.rowal) {
+      const int hrow = (int)fdiv((uint32_t)pbase, a.fw);
+      sw0 = pbase - hrow * a.W;
+      sn = (int)fdiv((uint32_t)hrow, a.fh);
+      sh = hrow - sn * a.H;
+    }
 #pragma unroll
     for (int j = 0; j < JA; ++j) {
       const int q = wave + j * 8;
       if (QA % 8 == 0 || q < QA) {
         const int p = pbase + arow[j];
-        const int n = (int)fdiv((uint32_t)p, a.fhw);
-        const int rem = p - n * a.H * a.W;
-        const int h = (int)fdiv((uint32_t)rem, a.fw);
-        const int w = rem - h * a.W;
+        int n, h, w;
+        if (a.rowal) {
+          n = sn;
+          h = sh;
+          w = sw0 + arow[j];
+        } else {
+          n = (int)fdiv((uint32_t)p, a.fhw);
+          const int rem = p - n * a.H * a.W;
+          h = (int)fdiv((uint32_t)rem, a.fw);
+          w = rem - h * a.W;
+        }
         const int hh = h + adh[j], ww = w + adw[j];
         bool ok = akin[j] && p < a.P && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
         const int hs = UPS ? (hh >> 1) : hh, ws = UPS ? (ww >> 1) : ww;
@@ -1484,6 +1508,7 @@ int v2_cfg(int rows_needed) {
     g_v2_force = e ? atoi(e) : -1;
   }
   if (g_v2_force >= 0 && rows_needed % kV2Cfg[g_v2_force].bn == 0) return g_v2_force;
+  if (rows_needed % 256 == 0) return 3;
   if (rows_needed > 64) return 0;
   if (rows_needed > 16) return 1;
   return 2;
@@ -1599,7 +1624,6 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   p.nsteps = fv_cdiv(P, p.px);
   const int ntile = p.ntk * p.ntc;
   int ns = p.v2 ? (256 + ntile / 2) / ntile : 768 / ntile;
-  if (p.v2 && ns > 64 && (long)p.bc * p.bkt * ntile * ns * 4 > (32L << 20)) ns = 64;   // slab <= ~32 MB
   if (ns < 1) ns = 1;
   if (ns > p.nsteps) ns = p.nsteps;
   p.sps = fv_cdiv(p.nsteps, ns);
@@ -1890,6 +1914,8 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.ntk = t.ntk; a.ntc = t.ntc; a.nsteps = t.nsteps; a.sps = t.sps;
     a.fhw = make_fastdiv((uint32_t)(d->h * d->w));
     a.fw = make_fastdiv((uint32_t)d->w);
+    a.fh = make_fastdiv((uint32_t)d->h);
+    a.rowal = (d->w % t.px) == 0;
     a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
     const int nblk = t.ntk * t.ntc * t.nsplit;

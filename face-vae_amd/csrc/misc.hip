@@ -75,30 +75,26 @@ __global__ void cast_kernel(const TI* __restrict__ x, TO* y, long n) {
     y[i] = Elt<TO>::from_f(Elt<TI>::to_f(x[i]));
 }
 
+// grid.y = source row (n*h + i), grid.x = (column j, 8-channel chunk) of that row
 template <typename T>
-__global__ void upsample_bwd_kernel(const T* __restrict__ g, int N, int h, int w, int C, T* out) {
-  const int cpc = C / 8;
-  const long total = (long)N * h * w * cpc;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(e % cpc);
-    const long p = e / cpc;
-    const int n = (int)(p / ((long)h * w));
-    const int rem = (int)(p - (long)n * h * w);
-    const int i = rem / w, j = rem - i * w;
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+__global__ void upsample_bwd_kernel(const T* __restrict__ g, int w, int C, int lgcpc, T* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (w << lgcpc)) return;
+  const int row = blockIdx.y;
+  const int j = e >> lgcpc, c = (e & ((1 << lgcpc) - 1)) * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        Chunk8<T> c;
-        c.load(g + ((long)(n * 2 * h + 2 * i + a) * (2 * w) + 2 * j + b) * C + cg * 8);
+    for (int b = 0; b < 2; ++b) {
+      Chunk8<T> v;
+      v.load(g + ((size_t)(2 * row + a) * (2 * w) + 2 * j + b) * C + c);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += c.get(k);
-      }
-    Chunk8<T> o;
-    o.set8(acc);
-    o.store(out + p * C + cg * 8);
-  }
+      for (int k = 0; k < 8; ++k) acc[k] += v.get(k);
+    }
+  Chunk8<T> o;
+  o.set8(acc);
+  o.store(out + ((size_t)row * w + j) * C + c);
 }
 
 template <typename T>
@@ -121,60 +117,52 @@ __global__ void sigmoid_bwd_kernel(const float* __restrict__ dy, const float* __
 }
 
 // ----------------------------------------------------------------- latent / losses
-// thread per (n, 8-channel group, hw) with hw fastest: eps (NCHW) reads coalesce
+// grid.y = (n, 8-channel group), grid.x = hw (fastest: eps NCHW reads coalesce)
 template <typename T>
-__global__ void reparam_fwd_kernel(const T* __restrict__ h, const float* __restrict__ eps, int N, int L,
-                                   int HW, T* mu, T* ls, T* z) {
-  const int cpc = L / 8;
-  const long total = (long)N * cpc * HW;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int hw = (int)(e % HW);
-    const long r = e / HW;
-    const int cg = (int)(r % cpc), n = (int)(r / cpc);
-    const long p = (long)n * HW + hw;
-    Chunk8<T> m, s;
-    m.load(h + p * 2 * L + cg * 8);
-    s.load(h + p * 2 * L + L + cg * 8);
-    float fz[8];
+__global__ void reparam_fwd_kernel(const T* __restrict__ h, const float* __restrict__ eps, int L, int HW,
+                                   int cpc, T* __restrict__ mu, T* __restrict__ ls, T* __restrict__ z) {
+  const int hw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (hw >= HW) return;
+  const int n = blockIdx.y / cpc, cg = blockIdx.y - (blockIdx.y / cpc) * cpc;
+  const size_t p = (size_t)n * HW + hw;
+  Chunk8<T> m, s;
+  m.load(h + p * 2 * L + cg * 8);
+  s.load(h + p * 2 * L + L + cg * 8);
+  const float* ep = eps + ((size_t)n * L + cg * 8) * HW + hw;
+  float fz[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      fz[j] = m.get(j) + expf(s.get(j)) * eps[((long)n * L + cg * 8 + j) * HW + hw];
-    m.store(mu + p * L + cg * 8);
-    s.store(ls + p * L + cg * 8);
-    Chunk8<T> o;
-    o.set8(fz);
-    o.store(z + p * L + cg * 8);
-  }
+  for (int j = 0; j < 8; ++j) fz[j] = m.get(j) + expf(s.get(j)) * ep[(size_t)j * HW];
+  m.store(mu + p * L + cg * 8);
+  s.store(ls + p * L + cg * 8);
+  Chunk8<T> o;
+  o.set8(fz);
+  o.store(z + p * L + cg * 8);
 }
 
 template <typename T>
-__global__ void reparam_bwd_kernel(const T* __restrict__ h, const float* __restrict__ eps, int N, int L,
-                                   int HW, const T* dz, const T* dmu, const T* dls, T* dh) {
-  const int cpc = L / 8;
-  const long total = (long)N * cpc * HW;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int hw = (int)(e % HW);
-    const long r = e / HW;
-    const int cg = (int)(r % cpc), n = (int)(r / cpc);
-    const long p = (long)n * HW + hw;
-    Chunk8<T> s, gz, gm, gs;
-    s.load(h + p * 2 * L + L + cg * 8);
-    if (dz) gz.load(dz + p * L + cg * 8); else gz.zero();
-    if (dmu) gm.load(dmu + p * L + cg * 8); else gm.zero();
-    if (dls) gs.load(dls + p * L + cg * 8); else gs.zero();
-    float om[8], os[8];
+__global__ void reparam_bwd_kernel(const T* __restrict__ h, const float* __restrict__ eps, int L, int HW, int cpc,
+                                   const T* dz, const T* dmu, const T* dls, T* __restrict__ dh) {
+  const int hw = blockIdx.x * blockDim.x + threadIdx.x;
+  if (hw >= HW) return;
+  const int n = blockIdx.y / cpc, cg = blockIdx.y - (blockIdx.y / cpc) * cpc;
+  const size_t p = (size_t)n * HW + hw;
+  Chunk8<T> s, gz, gm, gs;
+  s.load(h + p * 2 * L + L + cg * 8);
+  if (dz) gz.load(dz + p * L + cg * 8); else gz.zero();
+  if (dmu) gm.load(dmu + p * L + cg * 8); else gm.zero();
+  if (dls) gs.load(dls + p * L + cg * 8); else gs.zero();
+  const float* ep = eps + ((size_t)n * L + cg * 8) * HW + hw;
+  float om[8], os[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float ep = eps[((long)n * L + cg * 8 + j) * HW + hw];
-      om[j] = gz.get(j) + gm.get(j);
-      os[j] = gz.get(j) * expf(s.get(j)) * ep + gs.get(j);
-    }
-    Chunk8<T> a, b;
-    a.set8(om);
-    b.set8(os);
-    a.store(dh + p * 2 * L + cg * 8);
-    b.store(dh + p * 2 * L + L + cg * 8);
+  for (int j = 0; j < 8; ++j) {
+    om[j] = gz.get(j) + gm.get(j);
+    os[j] = gz.get(j) * expf(s.get(j)) * ep[(size_t)j * HW] + gs.get(j);
   }
+  Chunk8<T> a, b;
+  a.set8(om);
+  b.set8(os);
+  a.store(dh + p * 2 * L + cg * 8);
+  b.store(dh + p * 2 * L + L + cg * 8);
 }
 
 // generic two-stage scalar mean: kind 0 = KL(mu, logstd), 1 = (a-b)^2, 2 = |a-b|
@@ -401,15 +389,16 @@ int fv_cast(int dtype_in, const void* x, int dtype_out, void* y, long count, voi
 }
 
 int fv_upsample2x_bwd(int dtype, const void* g, int n, int h_src, int w_src, int c, void* out, void* stream) {
-  FV_REQUIRE(g && out && c % 8 == 0, "upsample bwd: channels must be a multiple of 8");
-  const long work = (long)n * h_src * w_src * (c / 8);
+  FV_REQUIRE(g && out && c % 8 == 0 && fv_ilog2(c / 8) >= 0, "upsample bwd: channels must be 8 * a power of two");
+  FV_REQUIRE(n * h_src <= 65535 && (long)n * h_src * w_src * 4 * c < (1L << 31), "upsample bwd: too large");
+  const int lgcpc = fv_ilog2(c / 8);
+  const dim3 grid(fv_cdiv((long)w_src << lgcpc, NTH), n * h_src);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(upsample_bwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)g, n, h_src,
-                       w_src, c, (bf16*)out);
+    hipLaunchKernelGGL(upsample_bwd_kernel<bf16>, grid, dim3(NTH), 0, s, (const bf16*)g, w_src, c, lgcpc, (bf16*)out);
   else
-    hipLaunchKernelGGL(upsample_bwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)g, n, h_src,
-                       w_src, c, (float*)out);
+    hipLaunchKernelGGL(upsample_bwd_kernel<float>, grid, dim3(NTH), 0, s, (const float*)g, w_src, c, lgcpc,
+                       (float*)out);
   return fv_check_launch("upsample2x_bwd");
 }
 
@@ -432,28 +421,30 @@ size_t fv_loss_ws_bytes(void) { return RED_BLOCKS * sizeof(double); }
 int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu, void* logstd,
                    void* z, void* stream) {
   FV_REQUIRE(h && eps && mu && logstd && z && L % 8 == 0, "reparam: bad args (L %% 8 == 0)");
-  const long work = (long)n * (L / 8) * hw;
+  FV_REQUIRE(n * (L / 8) <= 65535, "reparam: too many (image, channel-group) rows");
+  const dim3 grid(fv_cdiv(hw, NTH), n * (L / 8));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(reparam_fwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)h, eps, n, L, hw,
+    hipLaunchKernelGGL(reparam_fwd_kernel<bf16>, grid, dim3(NTH), 0, s, (const bf16*)h, eps, L, hw, L / 8,
                        (bf16*)mu, (bf16*)logstd, (bf16*)z);
   else
-    hipLaunchKernelGGL(reparam_fwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)h, eps, n, L,
-                       hw, (float*)mu, (float*)logstd, (float*)z);
+    hipLaunchKernelGGL(reparam_fwd_kernel<float>, grid, dim3(NTH), 0, s, (const float*)h, eps, L, hw, L / 8,
+                       (float*)mu, (float*)logstd, (float*)z);
   return fv_check_launch("reparam_fwd");
 }
 
 int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw, const void* dz,
                    const void* dmu, const void* dlogstd, void* dh, void* stream) {
   FV_REQUIRE(h && eps && dh && L % 8 == 0, "reparam bwd: bad args");
-  const long work = (long)n * (L / 8) * hw;
+  FV_REQUIRE(n * (L / 8) <= 65535, "reparam: too many (image, channel-group) rows");
+  const dim3 grid(fv_cdiv(hw, NTH), n * (L / 8));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(reparam_bwd_kernel<bf16>, dim3(grid_for(work)), dim3(NTH), 0, s, (const bf16*)h, eps, n, L, hw,
+    hipLaunchKernelGGL(reparam_bwd_kernel<bf16>, grid, dim3(NTH), 0, s, (const bf16*)h, eps, L, hw, L / 8,
                        (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, (bf16*)dh);
   else
-    hipLaunchKernelGGL(reparam_bwd_kernel<float>, dim3(grid_for(work)), dim3(NTH), 0, s, (const float*)h, eps, n, L,
-                       hw, (const float*)dz, (const float*)dmu, (const float*)dlogstd, (float*)dh);
+    hipLaunchKernelGGL(reparam_bwd_kernel<float>, grid, dim3(NTH), 0, s, (const float*)h, eps, L, hw, L / 8,
+                       (const float*)dz, (const float*)dmu, (const float*)dlogstd, (float*)dh);
   return fv_check_launch("reparam_bwd");
 }
 
