@@ -39,6 +39,7 @@ struct ConvArgs {
   int K, Kpad, nks;
   int sigmoid, nchw;
   int ntn;
+  int dbg;       // experiment knob (FV_CONV_DBG): bit0 skip MFMA, bit1 skip DMA after stage 0
   int lgtw;       // > 0: a block's pixels are a (BM >> lgtw) x (1 << lgtw) rectangle at p0
 };
 
@@ -104,7 +105,10 @@ __device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b,
 }
 
 // shared epilogue: bias [+ residual] -> BN partials -> [sigmoid] -> store (NHWC T or NCHW f32)
-template <typename T, int WN, int WM, int RN, int RM>
+// STAGED (bf16 NHWC only): after bias and BN partials the tile is rounded to bf16, written
+// to LDS (16-B chunks XOR-swizzled by pixel row) and stored with coalesced 16-B row
+// segments; the residual (if any) is added in that pass.  smem must hold BM*BN*2 bytes.
+template <typename T, int WN, int WM, int RN, int RM, bool STAGED = false>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN][RM], char* smem, int co0, int p0,
                                               int tm, int wn, int wm, int lane, int tid) {
   constexpr int NT = 64 * WN * WM;
@@ -135,7 +139,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     for (int m = 0; m < RM; ++m) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[n][m][i] += bv[n][i];
-      if (a.res && pv[m]) {
+      if (!STAGED && a.res && pv[m]) {
         const T* rp = reinterpret_cast<const T*>(a.res) + (long)pix_of[m] * a.ldy + cb;
         if (cb + 3 < a.Cout) {
           float f[4];
@@ -218,6 +222,42 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     }
   }
 
+  if constexpr (STAGED) {
+    static_assert(sizeof(T) == 2, "staged epilogue is bf16 NHWC");
+    constexpr int CPR = BN / 8;                         // 16-B chunks per pixel row
+    __syncthreads();                                    // stats scratch / last k-step reads done
+#pragma unroll
+    for (int n = 0; n < RN; ++n) {
+      const int cl = wn * RN * 16 + n * 16 + lh * 4;    // local channel of this lane's 4 values
+#pragma unroll
+      for (int m = 0; m < RM; ++m) {
+        const int pl = wm * RM * 16 + m * 16 + lr;
+        bf16 t4[4] = {(bf16)acc[n][m][0], (bf16)acc[n][m][1], (bf16)acc[n][m][2], (bf16)acc[n][m][3]};
+        char* dst = smem + pl * BN * 2 + (((cl >> 3) ^ (pl & (CPR - 1))) << 4) + ((cl & 4) << 1);
+        *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(t4);
+      }
+    }
+    __syncthreads();
+    for (int idx = tid; idx < BM * CPR; idx += NT) {
+      const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
+      const int pix = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
+      const int co = co0 + ch * 8;
+      if (pix >= a.P || co >= a.Cout) continue;
+      Chunk8<bf16> v;
+      v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+      T* yp = reinterpret_cast<T*>(a.y) + (long)pix * a.ldy + co;
+      if (a.res) {
+        Chunk8<bf16> r;
+        r.load(reinterpret_cast<const bf16*>(a.res) + (long)pix * a.ldy + co);
+        float f[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = v.get(j) + r.get(j);
+        v.set8(f);
+      }
+      v.store(reinterpret_cast<bf16*>(yp));
+    }
+    return;
+  }
 #pragma unroll
   for (int n = 0; n < RN; ++n) {
     const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
@@ -491,17 +531,18 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     wbase[j] = ((co0 + row) * a.Kpad + ((lchk ^ swz8(row)) << 3)) * 2;
   }
 
-  auto issue = [&](int ks, int buf) {
+  constexpr int PW = JA + JB;      // DMA pieces this wave issues per stage (upper bound)
+  // one DMA piece p of stage ks into buffer buf (p < JA: activation rows, else weight rows)
+  auto issue_piece = [&](int ks, int buf, int p) {
     const int k0 = ks * BK2;
-    const int tap = k0 >> a.lgCin, ci0 = k0 & (a.Cin - 1);
-    const int r = tap / KS, s = tap - (tap / KS) * KS;
-    const int tapoff = (((r - PAD) * a.Win + (s - PAD)) << a.lgCin) + ci0;
     char* As = smem + buf * STAGE;
     char* Bs = As + BM * ROWB;
-#pragma unroll
-    for (int j = 0; j < JA; ++j) {
+    if (p < JA) {
+      const int j = p;
       const int q = wave + j * NW;
       if (QA % NW == 0 || q < QA) {
+        const int tap = k0 >> a.lgCin, ci0 = k0 & (a.Cin - 1);
+        const int r = tap / KS, s = tap - (tap / KS) * KS;
         unsigned off;
         if constexpr (UPS) {
           const int row = q * 8 + lrow;
@@ -511,16 +552,20 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
           off = ok ? ((unsigned)((rb[j] + (hh >> 1) * a.Win + (ww >> 1)) << a.lgCin) + (unsigned)ci) * 2u
                    : 0x80000000u;
         } else {
+          const int tapoff = (((r - PAD) * a.Win + (s - PAD)) << a.lgCin) + ci0;
           off = ((tmask[j] >> tap) & 1) ? (unsigned)(pbase[j] + tapoff) * 2u : 0x80000000u;
         }
         dma16(xr, As + q * 1024, off);
       }
-    }
-#pragma unroll
-    for (int j = 0; j < JB; ++j) {
+    } else {
+      const int j = p - JA;
       const int q = wave + j * NW;
       if (QB % NW == 0 || q < QB) dma16(wr, Bs + q * 1024, (unsigned)(wbase[j] + k0 * 2));
     }
+  };
+  auto issue = [&](int ks, int buf) {
+#pragma unroll
+    for (int p = 0; p < PW; ++p) issue_piece(ks, buf, p);
   };
 
   f32x4 acc[RN][RM];
@@ -530,9 +575,12 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     for (int m = 0; m < RM; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lh = lane >> 4;
-  auto compute = [&](int buf) {
+  // compute stage `buf`; when nks_next >= 0 the pieces of that stage are issued one by one
+  // between the MFMA groups (2*RN slots) instead of in one burst after the barrier
+  auto compute = [&](int buf, int ks_next) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + BM * ROWB;
+    constexpr int SLOTS = 2 * RN;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       Frag<bf16> af[RN], bfm[RM];
@@ -547,9 +595,19 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
         bfm[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
       }
 #pragma unroll
-      for (int n = 0; n < RN; ++n)
+      for (int n = 0; n < RN; ++n) {
 #pragma unroll
         for (int m = 0; m < RM; ++m) acc[n][m] = mma(af[n], bfm[m], acc[n][m]);
+        if (ks_next >= 0) {
+          const int slot = kk * RN + n;
+#pragma unroll
+          for (int p = slot * PW / SLOTS; p < (slot + 1) * PW / SLOTS; ++p) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue_piece(ks_next, ks_next & 1, p);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
     }
   };
 
@@ -557,11 +615,18 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   for (int ks = 0; ks < a.nks; ++ks) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (ks + 1 < a.nks) issue(ks + 1, (ks + 1) & 1);
-    compute(ks & 1);
+    const int nxt = (ks + 1 < a.nks && !(a.dbg & 2)) ? ks + 1 : -1;
+    // burst issue after the barrier measured faster than pieces interleaved between the
+    // MFMA groups (the sched_barriers cost the ds_read/MFMA schedule more than they hide)
+    if (nxt >= 0) issue(nxt, nxt & 1);
+    if (!(a.dbg & 1)) compute(ks & 1, -1);
   }
   __syncthreads();
-  conv_epilogue<bf16, WN, WM, RN, RM>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+  if (a.dbg & 4) {   // experiment: skip the epilogue (keep one store so the MFMAs stay live)
+    if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.y)[tid] = acc[RN - 1][RM - 1][3];
+    return;
+  }
+  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1487,6 +1552,7 @@ bool use_v2(const fv_conv_desc* d) {
   }
   if (g_disable_v2) return false;
   if (d->dtype != FV_BF16 || d->pro_act || d->cin % 64) return false;
+  if (d->out_nchw_f32 || d->epi_sigmoid || d->cout % 8 || d->ldy % 8) return false;   // staged NHWC epilogue
   const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
@@ -1781,6 +1847,7 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   return FV_OK;
 }
 
+static int g_conv_dbg = -1;
 static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
                     const float* psc, const float* psh, const void* res, void* y, float* stats,
                     hipStream_t s) {
@@ -1797,6 +1864,11 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   a.K = d->ksize * d->ksize * d->cin; a.Kpad = kpad_of(d->ksize, d->cin); a.nks = a.Kpad / BK;
   a.sigmoid = d->epi_sigmoid; a.nchw = d->out_nchw_f32;
   a.ntn = fv_cdiv(d->cout, t.bn);
+  if (g_conv_dbg < 0) {
+    const char* e = getenv("FV_CONV_DBG");
+    g_conv_dbg = e ? atoi(e) : 0;
+  }
+  a.dbg = g_conv_dbg;
   int st;
   if (const int tr = halo_tr(d)) {
     a.lgtw = 6;
@@ -1809,6 +1881,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     return fv_check_launch("conv2d_fwd_halo");
   }
   if (use_v2(d)) {
+    FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");
     const FwdTile t2 = fwd_tile_v2(d->cout);
     a.ntn = fv_cdiv(d->cout, t2.bn);
     a.nks = a.Kpad / BK2;
