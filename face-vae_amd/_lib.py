@@ -27,6 +27,11 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class SnLayer(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("u", c_void_p), ("v", c_void_p), ("sigma", c_void_p), ("usnap", c_void_p),
+                ("vsnap", c_void_p), ("rows", c_int), ("cols", c_int)]
+
+
 class AdamTensor(ctypes.Structure):
     _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p),
                 ("exp_avg_sq", c_void_p), ("numel", c_long)]
@@ -53,6 +58,10 @@ _SIGS = {
     "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),
     "fv_spectral_norm_fwd": (c_int, [P, c_int, c_int, P, P, P, c_int, P, P]),
     "fv_spectral_norm_bwd": (c_int, [P, P, c_int, c_int, P, P, P, P, P, P]),
+    "fv_spectral_norm_batch_ws_floats": (c_size_t, [P, c_int]),
+    "fv_spectral_norm_batch_table_bytes": (c_size_t, [c_int]),
+    "fv_spectral_norm_batch_build": (c_int, [P, c_int, P, P, P]),
+    "fv_spectral_norm_fwd_batch": (c_int, [P, c_int, P, c_int, P]),
     "fv_bn_ws_bytes": (c_size_t, [c_int]),
     "fv_bn_stats_from_partials": (c_int, [P, c_int, c_int, c_long, c_int, P, P, P]),
     "fv_bn_stats_tensor": (c_int, [c_int, P, c_long, c_int, c_int, P, P, P]),

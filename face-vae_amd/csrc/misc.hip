@@ -328,6 +328,129 @@ __global__ void sn_bwd_apply_kernel(const float* __restrict__ g, int rows, int c
   }
 }
 
+// ---------------------------------------------------- batched spectral norm (all layers)
+// One power iteration + sigma for every spectral-normed conv of the model in 4 launches
+// (torch/nn/utils/spectral_norm.py:62-113 per layer): K1 partial W^T u over 64-row slices,
+// K2 column sums -> t and |t|^2 partials, K3 s = W (t/|t|) one wave per row, K4 u = s/|s|,
+// sigma = u.s (+ snapshots of u, v for the backward).  Layer descriptors live in a DEVICE
+// table built once by the caller; blocks map to (layer, tile) through per-layer offsets.
+struct SnDev {
+  const float* w;
+  float* u;
+  float* v;
+  float* sigma;
+  float* usnap;
+  float* vsnap;
+  float* tp;      // [rs][cols] partials of W^T u
+  float* t;       // [cols]
+  float* part;    // [cdiv(cols, 256)] partial |t|^2
+  float* s;       // [rows]
+  int rows, cols;
+  int b1, b2, b3; // first block of this layer in K1, K2, K3
+};
+
+__device__ __forceinline__ int sn_layer_of(const SnDev* L, int nl, int b, int which) {
+  int l = 0;
+  for (int i = 1; i < nl; ++i) {
+    const int bi = which == 1 ? L[i].b1 : which == 2 ? L[i].b2 : L[i].b3;
+    if (b >= bi) l = i;
+  }
+  return l;
+}
+
+__global__ void snb_wtu_kernel(const SnDev* __restrict__ L, int nl) {
+  const int l = sn_layer_of(L, nl, blockIdx.x, 1);
+  const SnDev d = L[l];
+  const int ncb = (d.cols + 63) / 64;
+  const int b = blockIdx.x - d.b1;
+  const int rs = b / ncb, cb = b - rs * ncb;
+  const int j = cb * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (j < d.cols) {
+    const int r0 = rs * 64 + rg * 16;
+#pragma unroll 4
+    for (int i = r0; i < min(d.rows, r0 + 16); ++i) acc += d.w[(long)i * d.cols + j] * d.u[i];
+  }
+  __shared__ float sh[4][64];
+  sh[rg][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (rg == 0 && j < d.cols)
+    d.tp[(long)rs * d.cols + j] = (sh[0][threadIdx.x] + sh[1][threadIdx.x]) + (sh[2][threadIdx.x] + sh[3][threadIdx.x]);
+}
+
+__global__ void snb_colsum_kernel(const SnDev* __restrict__ L, int nl) {
+  const int l = sn_layer_of(L, nl, blockIdx.x, 2);
+  const SnDev d = L[l];
+  const int b = blockIdx.x - d.b2;
+  const int j = b * NTH + threadIdx.x;
+  const int nrs = (d.rows + 63) / 64;
+  float t = 0.f;
+  if (j < d.cols) {
+    for (int rs = 0; rs < nrs; ++rs) t += d.tp[(long)rs * d.cols + j];
+    d.t[j] = t;
+  }
+  float sq = wave_sum(t * t);
+  __shared__ float sh[NTH / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) d.part[b] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+__global__ void snb_wv_kernel(const SnDev* __restrict__ L, int nl, int power_iter) {
+  const int l = sn_layer_of(L, nl, blockIdx.x, 3);
+  const SnDev d = L[l];
+  const int b = blockIdx.x - d.b3;
+  float inv = 1.f;
+  const float* vv = d.v;
+  if (power_iter) {
+    float n2 = 0.f;
+    for (int i = 0; i < (d.cols + NTH - 1) / NTH; ++i) n2 += d.part[i];
+    inv = 1.f / fmaxf(sqrtf(n2), 1e-12f);
+    vv = d.t;
+    if (b == 0)
+      for (int j = threadIdx.x; j < d.cols; j += NTH) {
+        const float vj = d.t[j] * inv;
+        d.v[j] = vj;
+        d.vsnap[j] = vj;
+      }
+  } else if (b == 0) {
+    for (int j = threadIdx.x; j < d.cols; j += NTH) d.vsnap[j] = d.v[j];
+  }
+  const int lane = threadIdx.x & 63;
+  const int row = b * (NTH / 64) + (threadIdx.x >> 6);
+  if (row >= d.rows) return;
+  float acc = 0.f;
+  for (int j = lane; j < d.cols; j += 64) acc += d.w[(long)row * d.cols + j] * vv[j];
+  acc = wave_sum(acc) * inv;
+  if (lane == 0) d.s[row] = acc;
+}
+
+__global__ void snb_fin_kernel(const SnDev* __restrict__ L, int power_iter) {
+  const SnDev d = L[blockIdx.x];
+  __shared__ float sh[NTH / 64];
+  __shared__ float bc;
+  float n2 = 0.f;
+  for (int i = threadIdx.x; i < d.rows; i += NTH) n2 += d.s[i] * d.s[i];
+  n2 = wave_sum(n2);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = n2;
+  __syncthreads();
+  if (threadIdx.x == 0) bc = 1.f / fmaxf(sqrtf((sh[0] + sh[1]) + (sh[2] + sh[3])), 1e-12f);
+  __syncthreads();
+  const float inv = bc;
+  float dd = 0.f;
+  for (int i = threadIdx.x; i < d.rows; i += NTH) {
+    const float uu = power_iter ? d.s[i] * inv : d.u[i];
+    if (power_iter) d.u[i] = uu;
+    d.usnap[i] = uu;
+    dd += uu * d.s[i];
+  }
+  __syncthreads();
+  dd = wave_sum(dd);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = dd;
+  __syncthreads();
+  if (threadIdx.x == 0) d.sigma[0] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
 // ------------------------------------------------------------------------------ Adam
 __global__ void adam_kernel(const fv_adam_tensor* __restrict__ ts, const int* __restrict__ blocks, float omb1,
                             float b2, float omb2, float eps, float step_size, float bc2_sqrt) {
@@ -544,6 +667,63 @@ int fv_spectral_norm_bwd(const float* w, const float* g_sn, int rows, int cols, 
   hipLaunchKernelGGL(sn_bwd_apply_kernel, dim3(grid_for(n, 2048)), dim3(NTH), 0, s, g_sn, rows, cols, u, v, sigma,
                      part, nb, g_orig);
   return fv_check_launch("sn_bwd");
+}
+
+size_t fv_spectral_norm_batch_ws_floats(const fv_sn_layer* layers, int nlayers) {
+  size_t n = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    const int r = layers[i].rows, c = layers[i].cols;
+    n += (size_t)((r + 63) / 64) * c + c + (c + NTH - 1) / NTH + r;
+  }
+  return n;
+}
+
+size_t fv_spectral_norm_batch_table_bytes(int nlayers) { return (size_t)nlayers * sizeof(SnDev); }
+
+int fv_spectral_norm_batch_build(const fv_sn_layer* layers, int nlayers, float* ws, void* table_host,
+                                 int* nblocks3) {
+  FV_REQUIRE(layers && nlayers > 0 && ws && table_host && nblocks3, "sn batch build: bad args");
+  SnDev* T = (SnDev*)table_host;
+  int b1 = 0, b2 = 0, b3 = 0;
+  float* p = ws;
+  for (int i = 0; i < nlayers; ++i) {
+    const fv_sn_layer& s = layers[i];
+    FV_REQUIRE(s.w && s.u && s.v && s.sigma && s.usnap && s.vsnap && s.rows > 0 && s.cols > 0, "sn layer %d", i);
+    SnDev d{};
+    d.w = s.w; d.u = s.u; d.v = s.v; d.sigma = s.sigma; d.usnap = s.usnap; d.vsnap = s.vsnap;
+    d.rows = s.rows; d.cols = s.cols;
+    const int nrs = (s.rows + 63) / 64;
+    d.tp = p; p += (size_t)nrs * s.cols;
+    d.t = p; p += s.cols;
+    d.part = p; p += (s.cols + NTH - 1) / NTH;
+    d.s = p; p += s.rows;
+    d.b1 = b1; b1 += nrs * ((s.cols + 63) / 64);
+    d.b2 = b2; b2 += (s.cols + NTH - 1) / NTH;
+    d.b3 = b3; b3 += (s.rows + NTH / 64 - 1) / (NTH / 64);
+    T[i] = d;
+  }
+  nblocks3[0] = b1;
+  nblocks3[1] = b2;
+  nblocks3[2] = b3;
+  return FV_OK;
+}
+
+int fv_spectral_norm_fwd_batch(const void* table_dev, int nlayers, const int* nblocks3, int power_iter,
+                               void* stream) {
+  FV_REQUIRE(table_dev && nlayers > 0 && nblocks3, "sn batch: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  const SnDev* L = (const SnDev*)table_dev;
+  int st;
+  if (power_iter) {
+    hipLaunchKernelGGL(snb_wtu_kernel, dim3(nblocks3[0]), dim3(NTH), 0, s, L, nlayers);
+    if ((st = fv_check_launch("snb_wtu"))) return st;
+    hipLaunchKernelGGL(snb_colsum_kernel, dim3(nblocks3[1]), dim3(NTH), 0, s, L, nlayers);
+    if ((st = fv_check_launch("snb_colsum"))) return st;
+  }
+  hipLaunchKernelGGL(snb_wv_kernel, dim3(nblocks3[2]), dim3(NTH), 0, s, L, nlayers, power_iter);
+  if ((st = fv_check_launch("snb_wv"))) return st;
+  hipLaunchKernelGGL(snb_fin_kernel, dim3(nlayers), dim3(NTH), 0, s, L, power_iter);
+  return fv_check_launch("snb_fin");
 }
 
 int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, double lr, double beta1,

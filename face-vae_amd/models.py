@@ -81,7 +81,18 @@ class FaceVAE(_Block):
         self.afe = AFE(False, list(cfg.down_seq), 0, C=2 * cfg.latent, D=1)
         self.generator = Generator(True, cfg.n_res, list(cfg.up_seq), D=1, C=cfg.latent)
 
+    def _sn_batch(self):
+        sb = getattr(self, "_snb", None)
+        if sb is None:
+            from .modules import _Conv
+            convs = [c for c in self.modules() if isinstance(c, _Conv) and c.sn]
+            sb = ops.SNBatch(convs)
+            object.__setattr__(self, "_snb", sb)
+        return sb
+
     def forward(self, x, eps):
+        if x.is_cuda:
+            self._sn_batch().run(self.training)   # all 15 power iterations in 4 launches
         h = self.afe.forward_2d(x)
         mu, logstd, z = ops.reparameterise(h, eps, self.compute_dtype())
         y = self.generator.forward_2d(z)

@@ -134,6 +134,48 @@ def spectral_norm_bwd(w, g, u, v, sigma):
     return g
 
 
+class SNBatch:
+    """One batched power iteration (4 launches) for every spectral-normed conv of a model,
+    run at the start of its forward; each conv then picks up its sigma and (u, v) snapshot
+    instead of running spectral_norm_fwd itself (torch/nn/utils/spectral_norm.py:62-113)."""
+
+    def __init__(self, convs):
+        self.convs = list(convs)
+        self.n = len(self.convs)
+        self.ws = None
+        self.nb = (ctypes.c_int * 3)()
+        self.tb = query("fv_spectral_norm_batch_table_bytes", self.n)
+        self._host = None
+        self._keep = None
+
+    def run(self, training: bool):
+        if self.n == 0:
+            return
+        dev = self.convs[0].weight_param().device
+        sigma = torch.empty(self.n, dtype=F32, device=dev)
+        snaps = [(torch.empty_like(c.weight_u), torch.empty_like(c.weight_v)) for c in self.convs]
+        layers = (L.SnLayer * self.n)()
+        for i, c in enumerate(self.convs):
+            w = c.weight_param()
+            if w.dtype != F32 or not w.is_contiguous():
+                raise RuntimeError("conv weights must be contiguous fp32")
+            layers[i] = L.SnLayer(w.data_ptr(), c.weight_u.data_ptr(), c.weight_v.data_ptr(),
+                                  sigma.data_ptr() + 4 * i, snaps[i][0].data_ptr(), snaps[i][1].data_ptr(),
+                                  w.shape[0], w.numel() // w.shape[0])
+        if self.ws is None or self.ws.device != dev:
+            self.ws = _empty(query("fv_spectral_norm_batch_ws_floats", ctypes.addressof(layers), self.n), F32, dev)
+        host = (ctypes.c_uint8 * self.tb)()
+        call("fv_spectral_norm_batch_build", ctypes.addressof(layers), self.n, ptr(self.ws), ctypes.addressof(host),
+             ctypes.addressof(self.nb))
+        hb = torch.frombuffer(bytearray(bytes(host)), dtype=torch.uint8).pin_memory()
+        table = hb.to(dev, non_blocking=True)
+        call("fv_spectral_norm_fwd_batch", table.data_ptr(), self.n, ctypes.addressof(self.nb), int(training),
+             stream())
+        self._keep = (hb, table)          # alive until the launches have consumed them
+        for i, c in enumerate(self.convs):
+            c._sn_pre = (sigma[i:i + 1], snaps[i][0], snaps[i][1])
+
+
 class ConvState:
     """Per-forward state of one conv: descriptor, prepared weights, SN snapshot."""
 
@@ -146,9 +188,14 @@ class ConvState:
         self.w = w
         self.sigma = None
         if conv.sn:
-            self.sigma = spectral_norm_fwd(w, conv.weight_u, conv.weight_v, training)
-            self.u = conv.weight_u.clone()
-            self.v = conv.weight_v.clone()
+            pre = getattr(conv, "_sn_pre", None)
+            if pre is not None:           # computed by the model's SNBatch for this forward
+                self.sigma, self.u, self.v = pre
+                conv._sn_pre = None
+            else:
+                self.sigma = spectral_norm_fwd(w, conv.weight_u, conv.weight_v, training)
+                self.u = conv.weight_u.clone()
+                self.v = conv.weight_v.clone()
         self.wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
         self.wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if need_wt else None
         call("fv_conv_weight_prep", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),

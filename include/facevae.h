@@ -117,6 +117,27 @@ int fv_spectral_norm_bwd(const float* w, const float* g_sn, int rows, int cols, 
                          const float* v, const float* sigma, float* g_orig, void* ws,
                          void* stream);
 
+/* batched form for all spectral-normed convs of a model (4 launches).  The caller builds
+ * the table once on the host (fv_spectral_norm_batch_build writes it into table_host, which
+ * the caller copies to device memory of fv_spectral_norm_batch_table_bytes) and keeps the
+ * workspace (fv_spectral_norm_batch_ws_floats floats) alive.  usnap/vsnap receive the u, v
+ * used for sigma (what the backward needs). */
+typedef struct fv_sn_layer {
+  const float* w;
+  float* u;
+  float* v;
+  float* sigma;
+  float* usnap;
+  float* vsnap;
+  int rows, cols;
+} fv_sn_layer;
+size_t fv_spectral_norm_batch_ws_floats(const fv_sn_layer* layers, int nlayers);
+size_t fv_spectral_norm_batch_table_bytes(int nlayers);
+int fv_spectral_norm_batch_build(const fv_sn_layer* layers, int nlayers, float* ws, void* table_host,
+                                 int* nblocks3);
+int fv_spectral_norm_fwd_batch(const void* table_dev, int nlayers, const int* nblocks3, int power_iter,
+                               void* stream);
+
 /* ---------------------------------------------------------------- batch norm ---- */
 size_t fv_bn_ws_bytes(int c);
 /* (count, sum, centred-M2) conv partials -> stats [3][c] doubles (count, sum, sumsq) */

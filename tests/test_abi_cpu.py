@@ -44,7 +44,9 @@ def test_descriptor_queries(lib_built):
     from facevae_amd import _lib, ops
     d = ops.desc(torch.bfloat16, 2, 64, 64, 256, 256, 256, 256, 3)
     assert _lib.query("fv_conv_wk_elems", ctypes.byref(d)) == 256 * 9 * 256
-    assert _lib.query("fv_conv2d_stats_blocks", ctypes.byref(d)) == 2 * 64 * 64 // 128
+    bp = _lib.query("fv_conv2d_stats_block_pixels", ctypes.byref(d))
+    assert bp == 256   # 256x256 tiles for 256-channel 3x3 convs
+    assert _lib.query("fv_conv2d_stats_blocks", ctypes.byref(d)) == 2 * 64 * 64 // bp
     bad = ops.desc(torch.bfloat16, 2, 64, 64, 24, 24, 256, 256, 3)   # cin not a power of two
     assert _lib.query("fv_conv_wk_elems", ctypes.byref(bad)) == 0
     assert _lib.query("fv_conv2d_fwd", ctypes.byref(bad), None, None, None, None, None, None, None, None,
