@@ -120,6 +120,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+    t_host = time.perf_counter() - t0      # host time to issue K steps (launches are async)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -160,6 +161,7 @@ def main():
         "config": {"workload": f"FaceVAE step {cfg.H}x{cfg.H} (AFE trunk + reparam + Generator trunk, MSE+KL, Adam)",
                    "global_batch": B * world, "per_gpu_batch": B, "resolution": cfg.H,
                    "parallelism": f"dp{world}" + ("" if world == 1 else (" syncbn" if not args.no_syncbn else " local-bn"))},
+        "host_issue_ms_per_step": round(t_host / args.steps * 1e3, 3),
         "mfma_util_step": round(step_util, 4),
         "step_flop_per_image": f_img,
         "roofline": roof,

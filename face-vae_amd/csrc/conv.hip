@@ -465,6 +465,28 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds,
                : "v"(voff), "s"(r), "s"(la)
                : "memory");
 }
+// the same with an LDS byte address and a wave-uniform byte offset in soffset (offset = voffset + soffset; an
+// out-of-range voffset of 0x80000000 stays out of range for any soffset < 2^31)
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff, unsigned soff) {
+  // no asm outputs: hipcc models an inline asm that contains a VMEM op as writing its outputs
+  // asynchronously and then waits vmcnt before those registers are reused (M0 is clobbered)
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+               :
+               : "v"(voff), "s"(r), "s"(lds), "s"(soff)
+               : "memory", "m0");
+}
+
+// f(integral_constant<S>) for the run-time, wave-uniform s in [0, N): a scalar branch to
+// one of N instantiations, so register arrays are only ever indexed by constants
+template <int S, int N, typename F>
+__device__ __forceinline__ void with_const(int s, F&& f) {
+  if constexpr (S + 1 == N) {
+    f(std::integral_constant<int, S>{});
+  } else {
+    if (s == S) f(std::integral_constant<int, S>{});
+    else with_const<S + 1, N>(s, f);
+  }
+}
 
 template <int KS, int WN, int WM, int RN, int RM, bool UPS>
 __global__ void __launch_bounds__(64 * WN * WM, 2)
@@ -493,79 +515,68 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
   const int lrow = lane >> 3, lchk = lane & 7;
-  // per-piece constants.  Non-upsampled: the element offset of this lane's chunk at tap
-  // (0,0) plus a bitmask of the taps that stay inside the image, so a k-step costs one add
-  // and one bit test per piece (the tap offset is wave-uniform).
-  typedef typename std::conditional<(KS * KS > 32), unsigned long long, unsigned>::type TapMask;
-  int rh[JA], rw[JA], rb[JA], pbase[JA];
-  TapMask tmask[JA];
-  bool rv[JA];
+  // per-piece constants.  A piece is 8 consecutive pixels of ONE image row (W % 8 == 0, so
+  // p0 + 8q never straddles a row) x 8 16-B chunks: its image row (n, h) is wave-uniform and
+  // the row part of the source address goes to soffset (SALU only); the lane's column part
+  // for each tap column s is precomputed once, 0x80000000 marking a column outside the
+  // image (the buffer range check then returns 0).  A k-step costs no address VALU beyond
+  // selecting the tap column's register.
+  int prn[JA], prh[JA];
+  bool pok[JA];
+  unsigned vcol[JA][KS];
 #pragma unroll
   for (int j = 0; j < JA; ++j) {
     const int q = wave + j * NW;
-    const int pix = p0 + q * 8 + lrow;
-    rv[j] = q < QA && pix < a.P;
-    const int n = pix / HW, rem = pix - (pix / HW) * HW;
-    rh[j] = rem / a.W;
-    rw[j] = rem - rh[j] * a.W;
-    rb[j] = n * a.Hin * a.Win;
-    const int row = q * 8 + lrow;
-    pbase[j] = ((rb[j] + rh[j] * a.Win + rw[j]) << a.lgCin) + ((lchk ^ swz8(row)) << 3);
-    TapMask m = 0;
-    if (!UPS && rv[j]) {
+    const int pp = __builtin_amdgcn_readfirstlane(p0 + q * 8);
+    pok[j] = (QA % NW == 0 || q < QA) && pp < a.P;
+    const int n = pp / HW, rem = pp - n * HW;
+    const int h = rem / a.W, w0 = rem - h * a.W;
+    prn[j] = n * a.Hin;
+    prh[j] = h;
+    const unsigned chunk = (unsigned)((lchk ^ swz8(q * 8 + lrow)) << 3);
 #pragma unroll
-      for (int r = 0; r < KS; ++r)
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const int hh = rh[j] + r - PAD, ww = rw[j] + s - PAD;
-          if (hh >= 0 && hh < a.Hin && ww >= 0 && ww < a.Win) m |= (TapMask)1 << (r * KS + s);
-        }
+    for (int s = 0; s < KS; ++s) {
+      const int ww = w0 + lrow + s - PAD;
+      const int sc = UPS ? (ww >> 1) : ww;
+      vcol[j][s] = (ww >= 0 && ww < a.W) ? ((unsigned)(sc << a.lgCin) + chunk) * 2u : 0x80000000u;
     }
-    tmask[j] = m;
   }
-  int wbase[JB];
+  unsigned wbase[JB];
 #pragma unroll
   for (int j = 0; j < JB; ++j) {
     const int row = (wave + j * NW) * 8 + lrow;
-    wbase[j] = ((co0 + row) * a.Kpad + ((lchk ^ swz8(row)) << 3)) * 2;
+    wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ swz8(row)) << 3)) * 2);
   }
 
   constexpr int PW = JA + JB;      // DMA pieces this wave issues per stage (upper bound)
-  // one DMA piece p of stage ks into buffer buf (p < JA: activation rows, else weight rows)
-  auto issue_piece = [&](int ks, int buf, int p) {
-    const int k0 = ks * BK2;
-    char* As = smem + buf * STAGE;
-    char* Bs = As + BM * ROWB;
-    if (p < JA) {
-      const int j = p;
-      const int q = wave + j * NW;
-      if (QA % NW == 0 || q < QA) {
-        const int tap = k0 >> a.lgCin, ci0 = k0 & (a.Cin - 1);
-        const int r = tap / KS, s = tap - (tap / KS) * KS;
-        unsigned off;
-        if constexpr (UPS) {
-          const int row = q * 8 + lrow;
-          const int ci = ci0 + ((lchk ^ swz8(row)) << 3);
-          const int hh = rh[j] + r - PAD, ww = rw[j] + s - PAD;
-          const bool ok = rv[j] && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-          off = ok ? ((unsigned)((rb[j] + (hh >> 1) * a.Win + (ww >> 1)) << a.lgCin) + (unsigned)ci) * 2u
-                   : 0x80000000u;
-        } else {
-          const int tapoff = (((r - PAD) * a.Win + (s - PAD)) << a.lgCin) + ci0;
-          off = ((tmask[j] >> tap) & 1) ? (unsigned)(pbase[j] + tapoff) * 2u : 0x80000000u;
-        }
-        dma16(xr, As + q * 1024, off);
-      }
-    } else {
-      const int j = p - JA;
-      const int q = wave + j * NW;
-      if (QB % NW == 0 || q < QB) dma16(wr, Bs + q * 1024, (unsigned)(wbase[j] + k0 * 2));
-    }
-  };
   auto issue = [&](int ks, int buf) {
+    const int k0 = ks * BK2;
+    const unsigned As = sbase + buf * STAGE;
+    const unsigned Bs = As + BM * ROWB;
+    const int tap = k0 >> a.lgCin, ci0 = k0 & (a.Cin - 1);
+    const int r = tap / KS, s = tap - (tap / KS) * KS;
+    with_const<0, KS>(s, [&](auto sc) {
+      constexpr int S = decltype(sc)::value;
 #pragma unroll
-    for (int p = 0; p < PW; ++p) issue_piece(ks, buf, p);
+      for (int j = 0; j < JA; ++j) {
+        const int q = wave + j * NW;
+        if (QA % NW == 0 || q < QA) {
+          const int hh = prh[j] + r - PAD;
+          const int srow = UPS ? (hh >> 1) : hh;
+          if (pok[j] && hh >= 0 && hh < a.H)
+            dma16s(xr, As + q * 1024, vcol[j][S], (unsigned)((((prn[j] + srow) * a.Win) << a.lgCin) + ci0) * 2u);
+          else
+            dma16s(xr, As + q * 1024, 0x80000000u, 0u);
+        }
+      }
+    });
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int q = wave + j * NW;
+      if (QB % NW == 0 || q < QB) dma16s(wr, Bs + q * 1024, wbase[j], (unsigned)(k0 * 2));
+    }
   };
 
   f32x4 acc[RN][RM];
@@ -575,12 +586,10 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     for (int m = 0; m < RM; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lh = lane >> 4;
-  // compute stage `buf`; when nks_next >= 0 the pieces of that stage are issued one by one
-  // between the MFMA groups (2*RN slots) instead of in one burst after the barrier
-  auto compute = [&](int buf, int ks_next) {
+  // compute stage `buf` (the DMAs of the next stage were issued in one burst before it)
+  auto compute = [&](int buf) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + BM * ROWB;
-    constexpr int SLOTS = 2 * RN;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       Frag<bf16> af[RN], bfm[RM];
@@ -595,19 +604,9 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
         bfm[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
       }
 #pragma unroll
-      for (int n = 0; n < RN; ++n) {
+      for (int n = 0; n < RN; ++n)
 #pragma unroll
         for (int m = 0; m < RM; ++m) acc[n][m] = mma(af[n], bfm[m], acc[n][m]);
-        if (ks_next >= 0) {
-          const int slot = kk * RN + n;
-#pragma unroll
-          for (int p = slot * PW / SLOTS; p < (slot + 1) * PW / SLOTS; ++p) {
-            __builtin_amdgcn_sched_barrier(0);
-            issue_piece(ks_next, ks_next & 1, p);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
     }
   };
 
@@ -619,7 +618,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     // burst issue after the barrier measured faster than pieces interleaved between the
     // MFMA groups (the sched_barriers cost the ds_read/MFMA schedule more than they hide)
     if (nxt >= 0) issue(nxt, nxt & 1);
-    if (!(a.dbg & 1)) compute(ks & 1, -1);
+    if (!(a.dbg & 1)) compute(ks & 1);
   }
   __syncthreads();
   if (a.dbg & 4) {   // experiment: skip the epilogue (keep one store so the MFMAs stay live)
@@ -1553,6 +1552,7 @@ bool use_v2(const fv_conv_desc* d) {
   if (g_disable_v2) return false;
   if (d->dtype != FV_BF16 || d->pro_act || d->cin % 64) return false;
   if (d->out_nchw_f32 || d->epi_sigmoid || d->cout % 8 || d->ldy % 8) return false;   // staged NHWC epilogue
+  if (d->w % 8) return false;   // a DMA piece (8 pixels) must lie in one image row
   const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
