@@ -1133,35 +1133,75 @@ conv_wgrad_v2(Wg2Args a) {
     bok[j] = (QB % 8 == 0 || q < QB) && bco[j] < a.ldd;
   }
 
+  // row-aligned stages (W % PX == 0, so P % PX == 0 too): a stage is one image-row segment
+  // (n, h, w0 wave-uniform).  The lane's part of its im2col source offset is precomputed
+  // relative to (h, w0) -- per h parity when upsampling -- so a piece costs an add, two
+  // range compares and a select; the dy pieces are a fixed per-lane offset + soffset.
+  int cwA[JA], cA0[JA], cA1[JA];
+#pragma unroll
+  for (int j = 0; j < JA; ++j) {
+    const int cw = akin[j] ? arow[j] + adw[j] : 0x40000000;   // column relative to w0
+    cwA[j] = cw;
+    if (UPS) {
+      cA0[j] = (((((adh[j] >> 1) * a.Win) + (cw >> 1)) << a.lgCin) + aci[j]) * 2;
+      cA1[j] = (((((1 + adh[j]) >> 1) * a.Win + (cw >> 1)) << a.lgCin) + aci[j]) * 2;
+    } else {
+      cA0[j] = cA1[j] = (((adh[j] * a.Win + cw) << a.lgCin) + aci[j]) * 2;
+    }
+  }
+  unsigned cB[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) cB[j] = bok[j] ? (unsigned)(brow[j] * a.ldd + bco[j]) * 2u : 0x80000000u;
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+
+  auto issue_rowal = [&](int st, int buf) {
+    const int pbase = (s_begin + st) * PX;
+    const unsigned As = sbase + buf * STAGE;
+    const unsigned Bs = As + SA;
+    const int hrow = (int)fdiv((uint32_t)pbase, a.fw);
+    const int w0 = pbase - hrow * a.W;
+    const int n = (int)fdiv((uint32_t)hrow, a.fh);
+    const int h = hrow - n * a.H;
+    const bool sok = pbase < a.P;
+    const int S = UPS ? ((((n * a.Hin + (h >> 1)) * a.Win + (w0 >> 1)) << a.lgCin) * 2)
+                      : ((((n * a.Hin + h) * a.Win + w0) << a.lgCin) * 2);
+    const bool odd = UPS && (h & 1);
+#pragma unroll
+    for (int j = 0; j < JA; ++j) {
+      const int q = wave + j * 8;
+      if (QA % 8 == 0 || q < QA) {
+        const bool ok = sok && (unsigned)(h + adh[j]) < (unsigned)a.H && (unsigned)(w0 + cwA[j]) < (unsigned)a.W;
+        const int c = odd ? cA1[j] : cA0[j];
+        dma16s(xr, As + q * 1024, ok ? (unsigned)(S + c) : 0x80000000u, 0u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < JB; ++j) {
+      const int q = wave + j * 8;
+      if (QB % 8 == 0 || q < QB) {
+        if (sok) dma16s(dr, Bs + q * 1024, cB[j], (unsigned)pbase * (unsigned)a.ldd * 2u);
+        else dma16s(dr, Bs + q * 1024, 0x80000000u, 0u);
+      }
+    }
+  };
+
   auto issue = [&](int st, int buf) {
+    if (a.rowal) {
+      issue_rowal(st, buf);
+      return;
+    }
     const int pbase = (s_begin + st) * PX;
     char* As = smem + buf * STAGE;
     char* Bs = As + SA;
-    // row-aligned stages (W % PX == 0): the whole stage is one image row segment, so the
-    // pixel decode is wave-uniform scalar work
-    int sn = 0, sh = 0, sw0 = 0;
-    if (a.rowal) {
-      const int hrow = (int)fdiv((uint32_t)pbase, a.fw);
-      sw0 = pbase - hrow * a.W;
-      sn = (int)fdiv((uint32_t)hrow, a.fh);
-      sh = hrow - sn * a.H;
-    }
 #pragma unroll
     for (int j = 0; j < JA; ++j) {
       const int q = wave + j * 8;
       if (QA % 8 == 0 || q < QA) {
         const int p = pbase + arow[j];
-        int n, h, w;
-        if (a.rowal) {
-          n = sn;
-          h = sh;
-          w = sw0 + arow[j];
-        } else {
-          n = (int)fdiv((uint32_t)p, a.fhw);
-          const int rem = p - n * a.H * a.W;
-          h = (int)fdiv((uint32_t)rem, a.fw);
-          w = rem - h * a.W;
-        }
+        const int n = (int)fdiv((uint32_t)p, a.fhw);
+        const int rem = p - n * a.H * a.W;
+        const int h = (int)fdiv((uint32_t)rem, a.fw);
+        const int w = rem - h * a.W;
         const int hh = h + adh[j], ww = w + adw[j];
         bool ok = akin[j] && p < a.P && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
         const int hs = UPS ? (hh >> 1) : hh, ws = UPS ? (ww >> 1) : ww;
@@ -1643,8 +1683,45 @@ static int halo_wg_tr(const fv_conv_desc* d) {
 
 // wgrad plan: v2 (bf16 DMA-fed, 8 waves), halo (7x7), or the register-staged v1 (fp32 / BN prologue)
 struct WgPlan {
-  int v2, bkt, bc, px, ntk, ntc, nsplit, nsteps, sps, KW, CW;
+  int v2, bkt, bc, px, ntk, ntc, nsplit, nsteps, sps, KW, CW, cfg;
 };
+
+// wgrad v2 tile configs: k rows x co cols per block, 8 waves as wk x wc, pixels per stage,
+// LDS ring depth.  The 32-B-block XOR swizzle of the transposed images needs bkt % 128 == 0.
+struct Wg2Cfg { int bkt, bc, wk, wc, px, ns; };
+constexpr Wg2Cfg kWg2Cfg[] = {
+    {256, 256, 2, 4, 64, 2},   // 0  (64 KB stages)
+    {128, 256, 2, 4, 64, 3},   // 1
+    {256, 128, 4, 2, 64, 3},   // 2
+    {128, 128, 2, 4, 64, 4},   // 3
+    {128, 64, 8, 1, 64, 4},    // 4
+    {256, 16, 8, 1, 64, 2},    // 5
+    {256, 256, 2, 4, 32, 4},   // 6  (32 KB stages, 3 in flight)
+    {384, 64, 8, 1, 64, 2},    // 7
+    {384, 64, 4, 2, 64, 2},    // 8
+    {128, 128, 2, 4, 32, 4},   // 9
+    {256, 128, 4, 2, 32, 4},   // 10
+};
+constexpr int kNumWg2Cfg = sizeof(kWg2Cfg) / sizeof(kWg2Cfg[0]);
+static int g_wg2_force = -2;
+int wg2_cfg(const fv_conv_desc* d, int K) {
+  if (g_wg2_force == -2) {
+    const char* e = getenv("FV_WG2_CFG");
+    g_wg2_force = e ? atoi(e) : -1;
+  }
+  const int bc = d->cout > 128 ? 256 : d->cout > 64 ? 128 : d->cout > 16 ? 64 : 16;
+  if (g_wg2_force >= 0 && g_wg2_force < kNumWg2Cfg && kWg2Cfg[g_wg2_force].bc == bc &&
+      d->w % kWg2Cfg[g_wg2_force].px == 0 && (d->ksize == 3 || g_wg2_force <= 5))
+    return g_wg2_force;
+  // defaults from the FaceVAE-shape sweep (tools/gpu_wgsweep.sh): 384 x 64 tiles for the
+  // 64-channel layers (K = 1152 splits exactly), 32-pixel stages 3-deep when K is not a
+  // multiple of 256 at 256 channels
+  if (bc == 16) return 5;
+  if (bc == 64) return (K % 384 == 0 && d->w % 64 == 0) ? 7 : 4;
+  const bool k256 = fv_cdiv(K, 256) * 256 <= fv_cdiv(K, 128) * 128;
+  if (bc == 256) return K % 256 == 0 ? 0 : (d->ksize == 3 && d->w % 32 == 0 ? 6 : 1);
+  return k256 ? 2 : 3;
+}
 static int g_disable_wg2 = -1;
 WgPlan plan_wgrad(const fv_conv_desc* d) {
   if (g_disable_wg2 < 0) {
@@ -1675,11 +1752,11 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
     return p;
   }
   if (p.v2) {
-    p.bc = d->cout > 128 ? 256 : d->cout > 64 ? 128 : d->cout > 16 ? 64 : 16;
-    if (p.bc == 64) p.bkt = 128;
-    else if (p.bc == 16) p.bkt = 256;
-    else p.bkt = (fv_cdiv(K, 256) * 256 <= fv_cdiv(K, 128) * 128) ? 256 : 128;
-    p.px = 64;
+    p.cfg = wg2_cfg(d, K);
+    const Wg2Cfg& c = kWg2Cfg[p.cfg];
+    p.bkt = c.bkt;
+    p.bc = c.bc;
+    p.px = c.px;
   } else {
     p.bc = d->cout > 64 ? 128 : (d->cout > 16 ? 64 : 16);
     p.bkt = 128;
@@ -1699,25 +1776,26 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   return p;
 }
 
-template <int KS, int BKT, int BC, int WK, int WC, int NS>
+template <int KS, int CFG>
 int launch_wg2_t(const Wg2Args& a, int ups, int nblk, hipStream_t s) {
+  constexpr Wg2Cfg c = kWg2Cfg[CFG];
   if (ups) {
-    if constexpr (KS == 3) hipLaunchKernelGGL((conv_wgrad_v2<KS, BKT, BC, WK, WC, 64, NS, true>), dim3(nblk), dim3(512), 0, s, a);
+    if constexpr (KS == 3)
+      hipLaunchKernelGGL((conv_wgrad_v2<KS, c.bkt, c.bc, c.wk, c.wc, c.px, c.ns, true>), dim3(nblk), dim3(512), 0, s, a);
     else return FV_E_UNSUPPORTED;
   } else {
-    hipLaunchKernelGGL((conv_wgrad_v2<KS, BKT, BC, WK, WC, 64, NS, false>), dim3(nblk), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_wgrad_v2<KS, c.bkt, c.bc, c.wk, c.wc, c.px, c.ns, false>), dim3(nblk), dim3(512), 0, s, a);
   }
   return FV_OK;
 }
 
-template <int KS>
+template <int KS, int CFG = 0>
 int launch_wg2_ks(const Wg2Args& a, const WgPlan& p, int ups, int nblk, hipStream_t s) {
-  if (p.bkt == 256 && p.bc == 256) return launch_wg2_t<KS, 256, 256, 2, 4, 2>(a, ups, nblk, s);
-  if (p.bkt == 128 && p.bc == 256) return launch_wg2_t<KS, 128, 256, 2, 4, 3>(a, ups, nblk, s);
-  if (p.bkt == 256 && p.bc == 128) return launch_wg2_t<KS, 256, 128, 4, 2, 3>(a, ups, nblk, s);
-  if (p.bkt == 128 && p.bc == 128) return launch_wg2_t<KS, 128, 128, 2, 4, 4>(a, ups, nblk, s);
-  if (p.bkt == 128 && p.bc == 64) return launch_wg2_t<KS, 128, 64, 8, 1, 4>(a, ups, nblk, s);
-  if (p.bkt == 256 && p.bc == 16) return launch_wg2_t<KS, 256, 16, 8, 1, 2>(a, ups, nblk, s);
+  if constexpr (CFG < kNumWg2Cfg) {
+    if constexpr (KS != 3 && CFG > 5) return FV_E_UNSUPPORTED;   // experiment configs: 3x3 only
+    if (p.cfg == CFG) return launch_wg2_t<KS, CFG>(a, ups, nblk, s);
+    return launch_wg2_ks<KS, CFG + 1>(a, p, ups, nblk, s);
+  }
   return FV_E_UNSUPPORTED;
 }
 
