@@ -79,6 +79,8 @@ _SIGS = {
     "fv_sigmoid_bwd_to_nhwc": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, P, P]),
     "fv_loss_ws_bytes": (c_size_t, []),
     "fv_reparam_fwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P]),
+    "fv_reparam_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "fv_reparam_kl_fwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P, P, P]),
     "fv_reparam_bwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P, P]),
     "fv_kl_fwd": (c_int, [c_int, P, P, c_long, P, P, P]),
     "fv_kl_bwd": (c_int, [c_int, P, P, c_long, P, P, P, P]),

@@ -39,7 +39,8 @@ struct ConvArgs {
   int K, Kpad, nks;
   int sigmoid, nchw;
   int ntn;
-  int dbg;       // experiment knob (FV_CONV_DBG): bit0 skip MFMA, bit1 skip DMA after stage 0
+  int dbg;       // experiment knob (FV_CONV_DBG): bit0 skip MFMA (ref loop), bit1 skip DMA after
+                 // the prologue, bit2 skip epilogue, bit3 v2 fwd: reference (unpipelined) k loop
   int lgtw;       // > 0: a block's pixels are a (BM >> lgtw) x (1 << lgtw) rectangle at p0
 };
 
@@ -586,39 +587,73 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     for (int m = 0; m < RM; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lh = lane >> 4;
-  // compute stage `buf` (the DMAs of the next stage were issued in one burst before it)
-  auto compute = [&](int buf) {
+  // fragments of one 32-deep k half-step (kk) of LDS buffer `buf`
+  auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], int buf, int kk) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + BM * ROWB;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      Frag<bf16> af[RN], bfm[RM];
+    for (int n = 0; n < RN; ++n) {
+      const int row = wn * RN * 16 + n * 16 + lr;
+      fa[n].lds(Bs + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
+    }
 #pragma unroll
-      for (int n = 0; n < RN; ++n) {
-        const int row = wn * RN * 16 + n * 16 + lr;
-        af[n].lds(Bs + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
-      }
-#pragma unroll
-      for (int m = 0; m < RM; ++m) {
-        const int row = wm * RM * 16 + m * 16 + lr;
-        bfm[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
-      }
-#pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int m = 0; m < RM; ++m) acc[n][m] = mma(af[n], bfm[m], acc[n][m]);
+    for (int m = 0; m < RM; ++m) {
+      const int row = wm * RM * 16 + m * 16 + lr;
+      fb[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
     }
   };
+  auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[n][m] = mma(fa[n], fb[m], acc[n][m]);
+  };
 
-  issue(0, 0);
-  for (int ks = 0; ks < a.nks; ++ks) {
+  if (!(a.dbg & 8)) {
+    // Software-pipelined k loop: the fragments of the next half-step are read while the
+    // MFMAs of the current one run, and the per-step barrier sits between the two MFMA
+    // groups of a step, so after it the matrix pipe has the second group (already in
+    // registers) to work on while the next step's first fragments and DMAs are issued.
+    //   step ks:  read F1(ks) | MFMA F0(ks) | vmcnt(0)+lgkmcnt(0), barrier | DMA ks+2 -> buf,
+    //             read F0(ks+1) | MFMA F1(ks)
+    // The barrier publishes stage ks+1 (every wave waited for its own DMAs) and retires all
+    // reads of buffer ks&1 (each wave drained its reads first), which DMA ks+2 then refills.
+    Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
+    issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int nxt = (ks + 1 < a.nks && !(a.dbg & 2)) ? ks + 1 : -1;
-    // burst issue after the barrier measured faster than pieces interleaved between the
-    // MFMA groups (the sched_barriers cost the ds_read/MFMA schedule more than they hide)
-    if (nxt >= 0) issue(nxt, nxt & 1);
-    if (!(a.dbg & 1)) compute(ks & 1);
+    if (a.nks > 1) issue(1, 1);
+    load_frags(fa0, fb0, 0, 0);
+    for (int ks = 0; ks < a.nks; ++ks) {
+      const int buf = ks & 1;
+      load_frags(fa1, fb1, buf, 1);
+      mfma_all(fa0, fb0);
+      if (ks + 1 < a.nks) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (ks + 2 < a.nks && !(a.dbg & 2)) issue(ks + 2, buf);
+        load_frags(fa0, fb0, buf ^ 1, 0);
+      }
+      mfma_all(fa1, fb1);
+    }
+  } else {
+    // reference loop (FV_CONV_DBG bit 3): one barrier per step, fragments read per half-step
+    issue(0, 0);
+    for (int ks = 0; ks < a.nks; ++ks) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int nxt = (ks + 1 < a.nks && !(a.dbg & 2)) ? ks + 1 : -1;
+      if (nxt >= 0) issue(nxt, nxt & 1);
+      if (!(a.dbg & 1)) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          Frag<bf16> af[RN], bfm[RM];
+          load_frags(af, bfm, ks & 1, kk);
+          mfma_all(af, bfm);
+        }
+      }
+    }
   }
   __syncthreads();
   if (a.dbg & 4) {   // experiment: skip the epilogue (keep one store so the MFMAs stay live)

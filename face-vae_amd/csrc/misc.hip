@@ -165,6 +165,122 @@ __global__ void reparam_bwd_kernel(const T* __restrict__ h, const float* __restr
   b.store(dh + p * 2 * L + L + cg * 8);
 }
 
+// Tiled forms (hw % 32 == 0): a block owns 32 pixels of one image x all L channels.  The
+// eps tile [L][32] (NCHW fp32) is read coalesced into LDS and read back transposed, so the
+// NHWC h / mu / logstd / z rows are touched as whole contiguous pixel rows.  The forward also
+// writes the block's KL partial sum (losses.py:392, the sum before the mean) in fp64.
+constexpr int RP_PX = 32;
+template <typename T>
+__global__ void __launch_bounds__(NTH) reparam_fwd_tiled(const T* __restrict__ h, const float* __restrict__ eps,
+                                                          int L, int HW, T* __restrict__ mu, T* __restrict__ ls,
+                                                          T* __restrict__ z, double* __restrict__ klpart) {
+  extern __shared__ float es[];          // [L][RP_PX + 1]
+  const int tpb = HW / RP_PX;
+  const int n = blockIdx.x / tpb, hw0 = (blockIdx.x - n * tpb) * RP_PX;
+  const int tid = threadIdx.x;
+  const float* eb = eps + (size_t)n * L * HW + hw0;
+  for (int f = tid; f < L * (RP_PX / 4); f += NTH) {
+    const int c = f / (RP_PX / 4), px = (f - c * (RP_PX / 4)) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(eb + (size_t)c * HW + px);
+    float* d = es + c * (RP_PX + 1) + px;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+  const int G = L / 8;
+  float kl = 0.f;
+  for (int it = tid; it < RP_PX * G; it += NTH) {
+    const int px = it / G, g = it - px * G;
+    const size_t p = (size_t)n * HW + hw0 + px;
+    Chunk8<T> m, s;
+    m.load(h + p * 2 * L + g * 8);
+    s.load(h + p * 2 * L + L + g * 8);
+    float fz[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float mv = m.get(j), sv = s.get(j);
+      const float ex = expf(sv);
+      fz[j] = mv + ex * es[(g * 8 + j) * (RP_PX + 1) + px];
+      kl += -0.5f - sv + 0.5f * mv * mv + 0.5f * ex * ex;
+    }
+    m.store(mu + p * L + g * 8);
+    s.store(ls + p * L + g * 8);
+    Chunk8<T> o;
+    o.set8(fz);
+    o.store(z + p * L + g * 8);
+  }
+  if (klpart) {
+    double acc = wave_sum_d((double)kl);
+    __shared__ double sh[NTH / 64];
+    if ((tid & 63) == 0) sh[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0;
+      for (int i = 0; i < NTH / 64; ++i) t += sh[i];
+      klpart[blockIdx.x] = t;
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(NTH) reparam_bwd_tiled(const T* __restrict__ h, const float* __restrict__ eps,
+                                                          int L, int HW, const T* dz, const T* dmu, const T* dls,
+                                                          T* __restrict__ dh) {
+  extern __shared__ float es[];
+  const int tpb = HW / RP_PX;
+  const int n = blockIdx.x / tpb, hw0 = (blockIdx.x - n * tpb) * RP_PX;
+  const int tid = threadIdx.x;
+  const float* eb = eps + (size_t)n * L * HW + hw0;
+  for (int f = tid; f < L * (RP_PX / 4); f += NTH) {
+    const int c = f / (RP_PX / 4), px = (f - c * (RP_PX / 4)) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(eb + (size_t)c * HW + px);
+    float* d = es + c * (RP_PX + 1) + px;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+  }
+  __syncthreads();
+  const int G = L / 8;
+  for (int it = tid; it < RP_PX * G; it += NTH) {
+    const int px = it / G, g = it - px * G;
+    const size_t p = (size_t)n * HW + hw0 + px;
+    Chunk8<T> s, gz, gm, gs;
+    s.load(h + p * 2 * L + L + g * 8);
+    if (dz) gz.load(dz + p * L + g * 8); else gz.zero();
+    if (dmu) gm.load(dmu + p * L + g * 8); else gm.zero();
+    if (dls) gs.load(dls + p * L + g * 8); else gs.zero();
+    float om[8], os[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      om[j] = gz.get(j) + gm.get(j);
+      os[j] = gz.get(j) * expf(s.get(j)) * es[(g * 8 + j) * (RP_PX + 1) + px] + gs.get(j);
+    }
+    Chunk8<T> a, b;
+    a.set8(om);
+    b.set8(os);
+    a.store(dh + p * 2 * L + g * 8);
+    b.store(dh + p * 2 * L + L + g * 8);
+  }
+}
+
+// KL backward, 8 elements per thread: dmu = g mu / n, dlogstd = g (exp(2 logstd) - 1) / n
+template <typename T>
+__global__ void kl_bwd_vec_kernel(const T* __restrict__ mu, const T* __restrict__ ls, long n, const float* gout,
+                                  T* dmu, T* dls) {
+  const float g = gout[0] / (float)n;
+  const long n8 = n / 8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    Chunk8<T> m, s;
+    m.load(mu + i * 8);
+    s.load(ls + i * 8);
+    float a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = g * m.get(j);
+      b[j] = g * (expf(2.f * s.get(j)) - 1.f);
+    }
+    if (dmu) { Chunk8<T> o; o.set8(a); o.store(dmu + i * 8); }
+    if (dls) { Chunk8<T> o; o.set8(b); o.store(dls + i * 8); }
+  }
+}
+
 // generic two-stage scalar mean: kind 0 = KL(mu, logstd), 1 = (a-b)^2, 2 = |a-b|
 template <int KIND, typename T>
 __global__ void loss_partial_kernel(const T* __restrict__ a, const T* __restrict__ b, long n, double* part) {
@@ -541,27 +657,67 @@ int fv_sigmoid_bwd_to_nhwc(int dtype_out, const float* dy, const float* y, int n
 
 size_t fv_loss_ws_bytes(void) { return RED_BLOCKS * sizeof(double); }
 
-int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu, void* logstd,
-                   void* z, void* stream) {
+size_t fv_reparam_ws_bytes(int n, int L, int hw) {
+  (void)L;
+  return (size_t)(hw % RP_PX == 0 ? (long)n * (hw / RP_PX) : 1) * sizeof(double);
+}
+
+static size_t reparam_lds(int L) { return (size_t)L * (RP_PX + 1) * sizeof(float); }
+
+int fv_reparam_kl_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu, void* logstd,
+                      void* z, float* kl, void* ws, void* stream) {
   FV_REQUIRE(h && eps && mu && logstd && z && L % 8 == 0, "reparam: bad args (L %% 8 == 0)");
+  hipStream_t s = (hipStream_t)stream;
+  if (hw % RP_PX == 0 && reparam_lds(L) <= 64 * 1024) {
+    FV_REQUIRE(!kl || ws, "reparam: KL output needs the workspace");
+    const int nb = n * (hw / RP_PX);
+    double* part = kl ? (double*)ws : nullptr;
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(reparam_fwd_tiled<bf16>, dim3(nb), dim3(NTH), reparam_lds(L), s, (const bf16*)h, eps, L, hw,
+                         (bf16*)mu, (bf16*)logstd, (bf16*)z, part);
+    else
+      hipLaunchKernelGGL(reparam_fwd_tiled<float>, dim3(nb), dim3(NTH), reparam_lds(L), s, (const float*)h, eps, L,
+                         hw, (float*)mu, (float*)logstd, (float*)z, part);
+    int st = fv_check_launch("reparam_fwd_tiled");
+    if (st || !kl) return st;
+    hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(NTH), 0, s, part, nb, (double)n * L * hw, kl);
+    return fv_check_launch("reparam_kl_final");
+  }
   FV_REQUIRE(n * (L / 8) <= 65535, "reparam: too many (image, channel-group) rows");
   const dim3 grid(fv_cdiv(hw, NTH), n * (L / 8));
-  hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
     hipLaunchKernelGGL(reparam_fwd_kernel<bf16>, grid, dim3(NTH), 0, s, (const bf16*)h, eps, L, hw, L / 8,
                        (bf16*)mu, (bf16*)logstd, (bf16*)z);
   else
     hipLaunchKernelGGL(reparam_fwd_kernel<float>, grid, dim3(NTH), 0, s, (const float*)h, eps, L, hw, L / 8,
                        (float*)mu, (float*)logstd, (float*)z);
-  return fv_check_launch("reparam_fwd");
+  int st = fv_check_launch("reparam_fwd");
+  if (st || !kl) return st;
+  FV_REQUIRE(ws, "reparam: KL output needs the workspace");
+  return fv_kl_fwd(dtype, mu, logstd, (long)n * L * hw, kl, ws, stream);
+}
+
+int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu, void* logstd,
+                   void* z, void* stream) {
+  return fv_reparam_kl_fwd(dtype, h, eps, n, L, hw, mu, logstd, z, nullptr, nullptr, stream);
 }
 
 int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw, const void* dz,
                    const void* dmu, const void* dlogstd, void* dh, void* stream) {
   FV_REQUIRE(h && eps && dh && L % 8 == 0, "reparam bwd: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  if (hw % RP_PX == 0 && reparam_lds(L) <= 64 * 1024) {
+    const int nb = n * (hw / RP_PX);
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(reparam_bwd_tiled<bf16>, dim3(nb), dim3(NTH), reparam_lds(L), s, (const bf16*)h, eps, L, hw,
+                         (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, (bf16*)dh);
+    else
+      hipLaunchKernelGGL(reparam_bwd_tiled<float>, dim3(nb), dim3(NTH), reparam_lds(L), s, (const float*)h, eps, L,
+                         hw, (const float*)dz, (const float*)dmu, (const float*)dlogstd, (float*)dh);
+    return fv_check_launch("reparam_bwd_tiled");
+  }
   FV_REQUIRE(n * (L / 8) <= 65535, "reparam: too many (image, channel-group) rows");
   const dim3 grid(fv_cdiv(hw, NTH), n * (L / 8));
-  hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
     hipLaunchKernelGGL(reparam_bwd_kernel<bf16>, grid, dim3(NTH), 0, s, (const bf16*)h, eps, L, hw, L / 8,
                        (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, (bf16*)dh);
@@ -600,6 +756,15 @@ int fv_kl_bwd(int dtype, const void* mu, const void* logstd, long count, const f
               void* dlogstd, void* stream) {
   FV_REQUIRE(mu && logstd && gout, "kl bwd: bad args");
   hipStream_t s = (hipStream_t)stream;
+  if (count % 8 == 0) {
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(kl_bwd_vec_kernel<bf16>, dim3(grid_for(count / 8)), dim3(NTH), 0, s, (const bf16*)mu,
+                         (const bf16*)logstd, count, gout, (bf16*)dmu, (bf16*)dlogstd);
+    else
+      hipLaunchKernelGGL(kl_bwd_vec_kernel<float>, dim3(grid_for(count / 8)), dim3(NTH), 0, s, (const float*)mu,
+                         (const float*)logstd, count, gout, (float*)dmu, (float*)dlogstd);
+    return fv_check_launch("kl_bwd");
+  }
   if (dtype == FV_BF16)
     hipLaunchKernelGGL(kl_bwd_kernel<bf16>, dim3(grid_for(count)), dim3(NTH), 0, s, (const bf16*)mu, (const bf16*)logstd,
                        count, gout, (bf16*)dmu, (bf16*)dlogstd);

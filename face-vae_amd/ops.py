@@ -510,10 +510,13 @@ class ConvFn(torch.autograd.Function):
 
 
 class ReparamFn(torch.autograd.Function):
-    """mu = h[:, :L], logstd = h[:, L:], z = mu + exp(logstd) * eps (models.py:559-561)."""
+    """mu = h[:, :L], logstd = h[:, L:], z = mu + exp(logstd) * eps (models.py:559-561).
+    The same pass also reduces the KL of (mu, logstd) (losses.py:392); `reparameterise`
+    tags mu with it so that KLDivergenceLoss on exactly this (mu, logstd) pair reuses the
+    value instead of re-reading both tensors."""
 
     @staticmethod
-    def forward(ctx, h, eps, dtype):
+    def forward(ctx, h, eps, dtype, holder):
         hb, C2 = to_nhwc(h, dtype)
         N, _, H, W = h.shape
         Lc = C2 // 2
@@ -523,8 +526,11 @@ class ReparamFn(torch.autograd.Function):
         mu = torch.empty((N, Lc, H, W), dtype=dtype, device=h.device, memory_format=CL)
         ls = torch.empty_like(mu)
         z = torch.empty_like(mu)
-        call("fv_reparam_fwd", L.dtype_code(dtype), ptr(hb), ptr(e32), N, Lc, H * W, ptr(mu), ptr(ls), ptr(z),
-             stream())
+        kl = torch.empty((), dtype=F32, device=h.device)
+        ws = _empty(query("fv_reparam_ws_bytes", N, Lc, H * W) // 8 + 1, F64, h.device)
+        call("fv_reparam_kl_fwd", L.dtype_code(dtype), ptr(hb), ptr(e32), N, Lc, H * W, ptr(mu), ptr(ls), ptr(z),
+             ptr(kl), ptr(ws), stream())
+        holder["kl"] = kl
         ctx.save_for_backward(h, hb, e32)
         ctx.dtype = dtype
         return mu, ls, z
@@ -539,7 +545,7 @@ class ReparamFn(torch.autograd.Function):
              ptr(grad_in(dz, dt) if dz is not None else None),
              ptr(grad_in(dmu, dt) if dmu is not None else None),
              ptr(grad_in(dls, dt) if dls is not None else None), ptr(dh), stream())
-        return from_nhwc(dh, h), None, None
+        return from_nhwc(dh, h), None, None, None
 
 
 def _same_layout(a, b):
@@ -554,6 +560,10 @@ class KLFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mu, logstd):
+        pre = getattr(mu, "_fv_kl", None)
+        if pre is not None and pre[0] is logstd and mu._version == pre[2] and logstd._version == pre[3]:
+            ctx.save_for_backward(mu, logstd)      # value reduced by the reparameterisation pass
+            return pre[1].clone()
         if mu.dtype not in (F32, torch.bfloat16):
             mu, logstd = mu.float(), logstd.float()
         mu, logstd = _same_layout(mu, logstd)
@@ -612,4 +622,7 @@ def kl_loss(mu, logstd):
 
 
 def reparameterise(h, eps, dtype):
-    return ReparamFn.apply(h, eps, dtype)
+    holder = {}
+    mu, ls, z = ReparamFn.apply(h, eps, dtype, holder)
+    mu._fv_kl = (ls, holder["kl"], mu._version, ls._version)
+    return mu, ls, z

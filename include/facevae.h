@@ -191,6 +191,11 @@ size_t fv_loss_ws_bytes(void);
  * mu/logstd/z [P][L] NHWC */
 int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu,
                    void* logstd, void* z, void* stream);
+/* the same, also writing the KL mean of (mu, logstd) to kl[0] (KLDivergenceLoss forward,
+ * losses.py:392) from the values it already holds; ws of fv_reparam_ws_bytes bytes */
+size_t fv_reparam_ws_bytes(int n, int L, int hw);
+int fv_reparam_kl_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu,
+                      void* logstd, void* z, float* kl, void* ws, void* stream);
 /* dh = [dz + dmu | dz*exp(logstd)*eps + dlogstd]; dmu/dlogstd may be NULL */
 int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw,
                    const void* dz, const void* dmu, const void* dlogstd, void* dh, void* stream);

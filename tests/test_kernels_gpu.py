@@ -184,10 +184,11 @@ def test_spectral_norm():
     assert rel(gc, wr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("H", [8, 6])          # 8: tiled reparam + fused KL; 6: hw % 32 != 0 fallback
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_losses_and_reparam(dtype):
+def test_losses_and_reparam(dtype, H):
     g = gen(11)
-    N, Lc, H = 2, 16, 8
+    N, Lc = 2, 16
     h = torch.randn(N, 2 * Lc, H, H, generator=g) * 0.5
     eps = torch.randn(N, Lc, H, H, generator=g)
     hr = h.to(dtype).float().clone().requires_grad_(True)
@@ -204,6 +205,9 @@ def test_losses_and_reparam(dtype):
     tol = TOL[dtype]
     assert rel(z.float(), z_r) < tol
     assert abs(K.item() - K_r.item()) < tol * abs(K_r.item())
+    # the KL reduced inside the reparameterisation pass == the standalone KL kernel
+    K2 = fv.KLDivergenceLoss()((mu.detach().clone(), ls.detach().clone()))
+    assert abs(K.item() - K2.item()) < 1e-5 * abs(K2.item())
     assert rel(hc.grad.float(), hr.grad) < tol * 2
     # MSE / L1 on fp32 NCHW images
     a = torch.rand(2, 3, 16, 16, generator=g)
