@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libfacevae.so")
 
 FV_F32, FV_BF16, FV_F64 = 0, 1, 2
 ADAM_CHUNK = 4096
+ABI_VERSION = 2
 
 
 class ConvDesc(ctypes.Structure):
@@ -65,7 +66,13 @@ _SIGS = {
     "fv_bn_ws_bytes": (c_size_t, [c_int]),
     "fv_bn_stats_from_partials": (c_int, [P, c_int, c_int, c_long, c_int, P, P, P]),
     "fv_bn_stats_tensor": (c_int, [c_int, P, c_long, c_int, c_int, P, P, P]),
-    "fv_bn_finalize": (c_int, [P, c_int, P, P, c_float, c_float, c_int, P, P, P, P, P, P, P]),
+    "fv_bn_finalize": (c_int, [P, c_int, P, P, c_float, c_float, c_int, P, P, P, P, P, P, P, P]),
+    "fv_bn_stats_finalize_partials": (c_int, [P, c_int, c_int, c_long, c_int, P, P, c_float, c_float, P, P, P, P, P,
+                                              P, P, P, P]),
+    "fv_bn_stats_finalize_tensor": (c_int, [c_int, P, c_long, c_int, c_int, P, P, c_float, c_float, P, P, P, P, P, P,
+                                            P, P, P]),
+    "fv_bn_act_bwd_reduce_finalize": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_float,
+                                              c_int, c_long, P, P, P, P, P]),
     "fv_bn_act_fwd": (c_int, [c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, c_float, c_int, P, P]),
     "fv_bn_act_bwd_reduce": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_float,
                                      c_int, P, P, P]),
@@ -122,7 +129,7 @@ def load():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.fv_abi_version() != 1:
+    if lib.fv_abi_version() != ABI_VERSION:
         raise ImportError("libfacevae ABI mismatch")
     _lib = lib
     return lib

@@ -132,14 +132,13 @@ __global__ void sum_splits_kernel(const double* ws, int nsplit, int rec, int C, 
   if (lane == 0) out[i] = t;
 }
 
-__global__ void finalize_kernel(const double* stats, int C, const float* gamma, const float* beta,
-                                float eps, float mom, int training, float* rm, float* rv,
-                                float* save_mean, float* save_invstd, float* scale, float* shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// mean / invstd / fused affine / running statistics of one channel from (n, S, Q)
+__device__ __forceinline__ void bn_finalize_one(int c, int C, double n, double S, double Q, const float* gamma,
+                                                const float* beta, float eps, float mom, int training, float* rm,
+                                                float* rv, float* save_mean, float* save_invstd, float* scale,
+                                                float* shift) {
   double mean, var;
   if (training) {
-    const double n = stats[c], S = stats[C + c], Q = stats[2 * C + c];
     mean = S / n;
     var = Q / n - mean * mean;
     if (var < 0) var = 0;
@@ -156,6 +155,39 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
   const float sc = g * inv;
   if (scale) scale[c] = sc;
   if (shift) shift[c] = b - (float)mean * sc;
+}
+
+__global__ void finalize_kernel(const double* stats, int C, const float* gamma, const float* beta,
+                                float eps, float mom, int training, float* rm, float* rv, long long* nbt,
+                                float* save_mean, float* save_invstd, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nbt && training && c == 0) nbt[0] += 1;
+  if (c >= C) return;
+  const double n = training ? stats[c] : 0, S = training ? stats[C + c] : 0, Q = training ? stats[2 * C + c] : 0;
+  bn_finalize_one(c, C, n, S, Q, gamma, beta, eps, mom, training, rm, rv, save_mean, save_invstd, scale, shift);
+}
+
+// single-process form: sum the level-1 records [split][3][C] over the splits and finalize, one
+// wave per channel (replaces sum_splits + finalize + the num_batches_tracked increment)
+__global__ void sum_finalize_kernel(const double* ws, int nsplit, int C, const float* gamma, const float* beta,
+                                    float eps, float mom, float* rm, float* rv, long long* nbt, float* save_mean,
+                                    float* save_invstd, float* scale, float* shift) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  if (c >= C) return;
+  double n = 0, S = 0, Q = 0;
+  for (int sp = lane; sp < nsplit; sp += 64) {
+    const double* r = ws + (long)sp * 3 * C + c;
+    n += r[0];
+    S += r[C];
+    Q += r[2 * C];
+  }
+  n = wave_sum_d(n);
+  S = wave_sum_d(S);
+  Q = wave_sum_d(Q);
+  if (lane == 0)
+    bn_finalize_one(c, C, n, S, Q, gamma, beta, eps, mom, 1, rm, rv, save_mean, save_invstd, scale, shift);
 }
 
 // out = [pool](act(y*scale+shift)).  grid.y = output row (n*Ho + i), grid.x covers the row's
@@ -285,6 +317,27 @@ __global__ void bwd_finalize_kernel(const double* red, int C, double count, floa
   k[C + c] = (float)(sgy / count);
 }
 
+// single-process form: sum the level-1 records [split][2][C] and finalize, one wave per channel
+__global__ void bwd_sum_finalize_kernel(const double* ws, int nsplit, int C, double count, float* dgamma,
+                                        float* dbeta, float* k) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double sg = 0, sgy = 0;
+  for (int sp = lane; sp < nsplit; sp += 64) {
+    sg += ws[(long)sp * 2 * C + c];
+    sgy += ws[(long)sp * 2 * C + C + c];
+  }
+  sg = wave_sum_d(sg);
+  sgy = wave_sum_d(sgy);
+  if (lane == 0) {
+    if (dbeta) dbeta[c] = (float)sg;
+    if (dgamma) dgamma[c] = (float)sgy;
+    k[c] = (float)(sg / count);
+    k[C + c] = (float)(sgy / count);
+  }
+}
+
 // dx = gamma*invstd*(g - k0 - yhat*k1) [+ addend]; thread = (pixel, 8-channel chunk), the
 // grid stride is a multiple of C/8 so each thread keeps one chunk's parameters in registers
 template <typename T>
@@ -373,15 +426,56 @@ int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, do
 }
 
 int fv_bn_finalize(const double* stats, int c, const float* gamma, const float* beta, float eps,
-                   float momentum, int training, float* running_mean, float* running_var, float* save_mean,
-                   float* save_invstd, float* scale, float* shift, void* stream) {
+                   float momentum, int training, float* running_mean, float* running_var,
+                   long long* num_batches_tracked, float* save_mean, float* save_invstd, float* scale,
+                   float* shift, void* stream) {
   FV_REQUIRE(c > 0, "bad channels");
   FV_REQUIRE(!training || stats, "training finalize needs stats");
   FV_REQUIRE(training || (running_mean && running_var), "eval finalize needs running stats");
   hipLaunchKernelGGL(finalize_kernel, dim3(fv_cdiv(c, NTH)), dim3(NTH), 0, (hipStream_t)stream, stats, c, gamma,
-                     beta, eps, momentum, training, running_mean, running_var, save_mean, save_invstd, scale,
-                     shift);
+                     beta, eps, momentum, training, running_mean, running_var, num_batches_tracked, save_mean,
+                     save_invstd, scale, shift);
   return fv_check_launch("bn_finalize");
+}
+
+int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_pixels, long total_pixels, int c,
+                                  const float* gamma, const float* beta, float eps, float momentum,
+                                  float* running_mean, float* running_var, long long* num_batches_tracked,
+                                  float* save_mean, float* save_invstd, float* scale, float* shift, void* ws,
+                                  void* stream) {
+  FV_REQUIRE(partials && ws, "null pointer");
+  FV_REQUIRE(nblocks > 0 && c > 0, "bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), NSPLIT), dim3(NTH), 0, s, partials, nblocks,
+                     block_pixels, total_pixels, c, (double*)ws);
+  int st = fv_check_launch("bn_partials");
+  if (st) return st;
+  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, 4)), dim3(NTH), 0, s, (const double*)ws, NSPLIT, c, gamma,
+                     beta, eps, momentum, running_mean, running_var, num_batches_tracked, save_mean, save_invstd,
+                     scale, shift);
+  return fv_check_launch("bn_sum_finalize");
+}
+
+int fv_bn_stats_finalize_tensor(int dtype, const void* x, long pixels, int c, int ldc, const float* gamma,
+                                const float* beta, float eps, float momentum, float* running_mean,
+                                float* running_var, long long* num_batches_tracked, float* save_mean,
+                                float* save_invstd, float* scale, float* shift, void* ws, void* stream) {
+  int st = check_c(c, ldc);
+  if (st) return st;
+  FV_REQUIRE(x && ws, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = stream_blocks(pixels, c);
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(tensor_stats_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)x, pixels, c, ldc,
+                       (double*)ws);
+  else
+    hipLaunchKernelGGL(tensor_stats_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)x, pixels, c, ldc,
+                       (double*)ws);
+  if ((st = fv_check_launch("bn_tensor_stats"))) return st;
+  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, c, gamma,
+                     beta, eps, momentum, running_mean, running_var, num_batches_tracked, save_mean, save_invstd,
+                     scale, shift);
+  return fv_check_launch("bn_sum_finalize");
 }
 
 int fv_bn_act_fwd(int dtype, const void* y, int n, int h, int w, int c, int ldc, const float* scale,
@@ -425,6 +519,31 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
   hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, 2, c,
                      red);
   return fv_check_launch("bn_sum_splits");
+}
+
+int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
+                                  int ldc, const float* mean, const float* invstd, const float* gamma,
+                                  const float* beta, float slope, int pool, long count, float* dgamma,
+                                  float* dbeta, float* k, void* ws, void* stream) {
+  int st = check_c(c, ldc);
+  if (st) return st;
+  FV_REQUIRE(!pool || ldc == c, "pooled bwd needs dense channels");
+  FV_REQUIRE(k && ws && count > 0, "bad args");
+  hipStream_t s = (hipStream_t)stream;
+  FV_REQUIRE((long)n * h * w * ldc < (1L << 31), "bn: tensor too large for 32-bit indexing");
+  const int nb = stream_blocks((long)n * h * w, c);
+  const int P = n * h * w;
+  const FastDiv fw = make_fastdiv((uint32_t)w);
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
+                       (const bf16*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+  else
+    hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
+                       (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+  if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
+  hipLaunchKernelGGL(bwd_sum_finalize_kernel, dim3(fv_cdiv(c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, c,
+                     (double)count, dgamma, dbeta, k);
+  return fv_check_launch("bn_bwd_sum_finalize");
 }
 
 int fv_bn_bwd_finalize(const double* red, int c, long count, float* dgamma, float* dbeta, float* k,

@@ -252,23 +252,32 @@ class BNResult:
     __slots__ = ("mean", "invstd", "scale", "shift", "count")
 
 
-def bn_finalize(bn, stats, count, training):
-    """stats [3][C] fp64 (already all-reduced for SyncBN) -> BNResult; updates running stats."""
-    C = bn.num_features
-    dev = bn.weight.device
+def _bn_result(C, dev, count):
     r = BNResult()
     r.mean = torch.empty(C, dtype=F32, device=dev)
     r.invstd = torch.empty(C, dtype=F32, device=dev)
     r.scale = torch.empty(C, dtype=F32, device=dev)
     r.shift = torch.empty(C, dtype=F32, device=dev)
     r.count = count
+    return r
+
+
+def _running(bn, training):
+    """(running_mean, running_var, num_batches_tracked) pointers the finalize updates/reads."""
     upd = training and bn.track_running_stats
+    use = upd or not training
+    nbt = bn.num_batches_tracked if (upd and bn.num_batches_tracked is not None) else None
+    return (ptr(bn.running_mean if use else None), ptr(bn.running_var if use else None), ptr(nbt))
+
+
+def bn_finalize(bn, stats, count, training):
+    """stats [3][C] fp64 (already all-reduced for SyncBN) -> BNResult; updates running stats
+    and num_batches_tracked (torch/nn/modules/batchnorm.py:744-840)."""
+    C = bn.num_features
+    r = _bn_result(C, bn.weight.device, count)
+    rm, rv, nbt = _running(bn, training)
     call("fv_bn_finalize", ptr(stats), C, ptr(bn.weight), ptr(bn.bias), float(bn.eps), float(bn.momentum),
-         int(training), ptr(bn.running_mean if (upd or not training) else None),
-         ptr(bn.running_var if (upd or not training) else None), ptr(r.mean), ptr(r.invstd), ptr(r.scale),
-         ptr(r.shift), stream())
-    if upd:
-        bn.num_batches_tracked.add_(1)
+         int(training), rm, rv, nbt, ptr(r.mean), ptr(r.invstd), ptr(r.scale), ptr(r.shift), stream())
     return r
 
 
@@ -283,24 +292,37 @@ def bn_from_partials(bn, part, d, training, comm):
     P = d.n * d.h * d.w
     nb = query("fv_conv2d_stats_blocks", ctypes.byref(d))
     bp = query("fv_conv2d_stats_block_pixels", ctypes.byref(d))
-    stats = torch.empty(3 * C, dtype=F64, device=dev)
     ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, dev)
+    if comm is None:
+        # single process: statistics + finalize in two launches
+        r = _bn_result(C, dev, P)
+        rm, rv, nbt = _running(bn, True)
+        call("fv_bn_stats_finalize_partials", ptr(part), nb, bp, P, C, ptr(bn.weight), ptr(bn.bias), float(bn.eps),
+             float(bn.momentum), rm, rv, nbt, ptr(r.mean), ptr(r.invstd), ptr(r.scale), ptr(r.shift), ptr(ws),
+             stream())
+        return r
+    stats = torch.empty(3 * C, dtype=F64, device=dev)
     call("fv_bn_stats_from_partials", ptr(part), nb, bp, P, C, ptr(stats), ptr(ws), stream())
     _sync(stats, comm)
-    world = comm.world_size if comm is not None else 1
-    return bn_finalize(bn, stats, P * world, training)
+    return bn_finalize(bn, stats, P * comm.world_size, training)
 
 
 def bn_from_tensor(bn, x, training, comm):
     N, C, H, W = x.shape
     if not training:
         return bn_finalize(bn, None, 0, False)
-    stats = torch.empty(3 * C, dtype=F64, device=x.device)
     ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, x.device)
+    if comm is None:
+        r = _bn_result(C, x.device, N * H * W)
+        rm, rv, nbt = _running(bn, True)
+        call("fv_bn_stats_finalize_tensor", L.dtype_code(x.dtype), ptr(x), N * H * W, C, C, ptr(bn.weight),
+             ptr(bn.bias), float(bn.eps), float(bn.momentum), rm, rv, nbt, ptr(r.mean), ptr(r.invstd), ptr(r.scale),
+             ptr(r.shift), ptr(ws), stream())
+        return r
+    stats = torch.empty(3 * C, dtype=F64, device=x.device)
     call("fv_bn_stats_tensor", L.dtype_code(x.dtype), ptr(x), N * H * W, C, C, ptr(stats), ptr(ws), stream())
     _sync(stats, comm)
-    world = comm.world_size if comm is not None else 1
-    return bn_finalize(bn, stats, N * H * W * world, True)
+    return bn_finalize(bn, stats, N * H * W * comm.world_size, True)
 
 
 def bn_act_forward(y, r: BNResult, slope, pool):
@@ -317,15 +339,20 @@ def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, ne
     N, C, H, W = y.shape
     dev = y.device
     dc = L.dtype_code(y.dtype)
-    red = torch.empty(2 * C, dtype=F64, device=dev)
     ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, dev)
-    call("fv_bn_act_bwd_reduce", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd), ptr(bn.weight),
-         ptr(bn.bias), float(slope), int(pool), ptr(red), ptr(ws), stream())
-    _sync(red, comm)
     dg = torch.empty(C, dtype=F32, device=dev)
     dbt = torch.empty(C, dtype=F32, device=dev)
     k = torch.empty(2 * C, dtype=F32, device=dev)
-    call("fv_bn_bwd_finalize", ptr(red), C, int(r.count), ptr(dg), ptr(dbt), ptr(k), stream())
+    if comm is None:
+        call("fv_bn_act_bwd_reduce_finalize", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
+             ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), int(r.count), ptr(dg), ptr(dbt), ptr(k), ptr(ws),
+             stream())
+    else:
+        red = torch.empty(2 * C, dtype=F64, device=dev)
+        call("fv_bn_act_bwd_reduce", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
+             ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), ptr(red), ptr(ws), stream())
+        _sync(red, comm)
+        call("fv_bn_bwd_finalize", ptr(red), C, int(r.count), ptr(dg), ptr(dbt), ptr(k), stream())
     dx = None
     if need_dx:
         dx = torch.empty((N, C, H, W), dtype=y.dtype, device=dev, memory_format=CL)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define FV_ABI_VERSION 1
+#define FV_ABI_VERSION 2
 
 enum fv_status {
   FV_OK = 0,
@@ -152,8 +152,19 @@ int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, do
  * statistics are used and stats may be NULL. */
 int fv_bn_finalize(const double* stats, int c, const float* gamma, const float* beta, float eps,
                    float momentum, int training, float* running_mean, float* running_var,
-                   float* save_mean, float* save_invstd, float* scale, float* shift,
-                   void* stream);
+                   long long* num_batches_tracked, float* save_mean, float* save_invstd, float* scale,
+                   float* shift, void* stream);
+/* single-process training forms (no SyncBN exchange between the statistics and finalize):
+ * statistics + finalize (+ num_batches_tracked += 1) in two launches */
+int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_pixels, long total_pixels,
+                                  int c, const float* gamma, const float* beta, float eps, float momentum,
+                                  float* running_mean, float* running_var, long long* num_batches_tracked,
+                                  float* save_mean, float* save_invstd, float* scale, float* shift,
+                                  void* ws, void* stream);
+int fv_bn_stats_finalize_tensor(int dtype, const void* x, long pixels, int c, int ldc, const float* gamma,
+                                const float* beta, float eps, float momentum, float* running_mean,
+                                float* running_var, long long* num_batches_tracked, float* save_mean,
+                                float* save_invstd, float* scale, float* shift, void* ws, void* stream);
 /* out = [avgpool2](act(y*scale + shift)); y [n][h][w][ldc], out [n][h/p][w/p][c] */
 int fv_bn_act_fwd(int dtype, const void* y, int n, int h, int w, int c, int ldc,
                   const float* scale, const float* shift, float slope, int pool, void* out,
@@ -166,6 +177,11 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
 /* dgamma/dbeta (accumulated) and the two BN-backward coefficients k [2][c] */
 int fv_bn_bwd_finalize(const double* red, int c, long count, float* dgamma, float* dbeta,
                        float* k, void* stream);
+/* single-process form of fv_bn_act_bwd_reduce + fv_bn_bwd_finalize (two launches) */
+int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
+                                  int ldc, const float* mean, const float* invstd, const float* gamma,
+                                  const float* beta, float slope, int pool, long count, float* dgamma,
+                                  float* dbeta, float* k, void* ws, void* stream);
 /* dx = gamma*invstd*(g - k0 - yhat*k1) [+ addend]; dx/addend [n][h][w][ldc] */
 int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
                         int ldc, const float* mean, const float* invstd, const float* gamma,

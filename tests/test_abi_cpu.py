@@ -34,7 +34,7 @@ def test_library_exports_header(lib_built):
     from facevae_amd import _lib
     assert set(header_symbols()) == set(_lib.exported_symbols())
     lib = _lib.load()
-    assert lib.fv_abi_version() == 1
+    assert lib.fv_abi_version() == _lib.ABI_VERSION
     assert lib.fv_last_error() is not None
 
 
