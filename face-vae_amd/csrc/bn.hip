@@ -38,7 +38,7 @@ __device__ __forceinline__ void st8(T* p, const float* f) {
   c.store(p);
 }
 
-// conv per-block (sum, centred M2) partials -> ws [split][3][C] (n, S, Q) in fp64
+// conv per-record (sum, sum of squares) partials -> ws [split][3][C] (n, S, Q) in fp64
 __global__ void partials_kernel(const float* __restrict__ part, int nb, int bpix, long P, int C,
                                 double* ws) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -50,10 +50,9 @@ __global__ void partials_kernel(const float* __restrict__ part, int nb, int bpix
   if (c < C) {
     for (int b = b0 + r; b < b1; b += 4) {
       const double nb_ = (double)min((long)bpix, P - (long)b * bpix);
-      const double s = part[(long)(2 * b) * C + c], m2 = part[(long)(2 * b + 1) * C + c];
       n += nb_;
-      S += s;
-      Q += m2 + s * s / nb_;
+      S += part[(long)(2 * b) * C + c];
+      Q += part[(long)(2 * b + 1) * C + c];
     }
   }
   __shared__ double red[3][4][64];

@@ -157,69 +157,39 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
   }
 
   if (a.stats) {
-    // per-block (sum, centred M2) per output channel; rows of this block = valid pixels
-    float* red = reinterpret_cast<float*>(smem);        // [WM][BN]
-    float* meanv = red + WM * BN;                         // [BN]
-    const int cnt = a.lgtw ? BM : min(BM, a.P - p0);
-    float s[RN][4];
+    // BN statistics partials, one record per wave row (RM*16 pixels, record index
+    // tm*WM + wm): per output channel (sum, sum of squares) over the record's valid pixels,
+    // reduced over the 16 pixel lanes of each m-tile by shuffles -- no LDS, no barrier.
+    const int rec = tm * WM + wm;
 #pragma unroll
-    for (int n = 0; n < RN; ++n)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float t = 0.f;
-#pragma unroll
-        for (int m = 0; m < RM; ++m) t += pv[m] ? acc[n][m][i] : 0.f;
-        t += __shfl_xor(t, 1, 64);
-        t += __shfl_xor(t, 2, 64);
-        t += __shfl_xor(t, 4, 64);
-        t += __shfl_xor(t, 8, 64);
-        s[n][i] = t;
-      }
-    if (lr == 0) {
-#pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float S = 0.f;
-#pragma unroll
-      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
-      meanv[c] = S / (float)cnt;
-      if (co0 + c < a.Cout) a.stats[(long)(tm * 2) * a.Cout + co0 + c] = S;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int n = 0; n < RN; ++n)
+    for (int n = 0; n < RN; ++n) {
+      float sv[4], qv[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float mu = meanv[wn * RN * 16 + n * 16 + lh * 4 + i];
-        float t = 0.f;
+        float t = 0.f, q = 0.f;
 #pragma unroll
         for (int m = 0; m < RM; ++m) {
-          const float d = acc[n][m][i] - mu;
-          t += pv[m] ? d * d : 0.f;
+          const float v = pv[m] ? acc[n][m][i] : 0.f;
+          t += v;
+          q += v * v;
         }
-        t += __shfl_xor(t, 1, 64);
-        t += __shfl_xor(t, 2, 64);
-        t += __shfl_xor(t, 4, 64);
-        t += __shfl_xor(t, 8, 64);
-        s[n][i] = t;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          t += __shfl_xor(t, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        sv[i] = t;
+        qv[i] = q;
       }
-    __syncthreads();
-    if (lr == 0) {
+      const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
+      if (lr == 0) {
 #pragma unroll
-      for (int n = 0; n < RN; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) red[wm * BN + wn * RN * 16 + n * 16 + lh * 4 + i] = s[n][i];
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float S = 0.f;
-#pragma unroll
-      for (int j = 0; j < WM; ++j) S += red[j * BN + c];
-      if (co0 + c < a.Cout) a.stats[(long)(tm * 2 + 1) * a.Cout + co0 + c] = S;
+        for (int i = 0; i < 4; ++i)
+          if (cb + i < a.Cout) {
+            a.stats[(long)(rec * 2) * a.Cout + cb + i] = sv[i];
+            a.stats[(long)(rec * 2 + 1) * a.Cout + cb + i] = qv[i];
+          }
+      }
     }
   }
 
@@ -489,19 +459,29 @@ __device__ __forceinline__ void with_const(int s, F&& f) {
   }
 }
 
-template <int KS, int WN, int WM, int RN, int RM, bool UPS>
-__global__ void __launch_bounds__(64 * WN * WM, 2)
+// BKS = k per stage: 64 (128-B rows, 8 chunks) or 32 (64-B rows, 4 chunks; half the LDS, so
+// the 4-wave tiles run 4 blocks per CU and hide each other's DMA latency and epilogue).
+template <int BKS>
+__device__ __forceinline__ int swzk(int row) {
+  if constexpr (BKS == 64) return swz8(row);
+  else return rswz<bf16>(row);
+}
+
+template <int KS, int WN, int WM, int RN, int RM, bool UPS, int BKS>
+__global__ void __launch_bounds__(64 * WN * WM, (BKS == 32 && WN * WM == 4) ? 4 : 2)
 conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
   constexpr int BN = WN * RN * 16, BM = WM * RM * 16;
   constexpr int PAD = KS / 2;
-  constexpr int ROWB = BK2 * 2;
-  constexpr int QA = BM / 8, QB = BN / 8;            // 1-KB DMA pieces per stage
+  constexpr int ROWB = BKS * 2;
+  constexpr int CH = BKS / 8, RPP = 64 / CH;         // 16-B chunks per row, rows per 1-KB piece
+  constexpr int QA = BM / RPP, QB = BN / RPP;        // 1-KB DMA pieces per stage
   constexpr int JA = (QA + NW - 1) / NW, JB = (QB + NW - 1) / NW;
   constexpr int STAGE = (BM + BN) * ROWB;
   __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
+  const int nks = a.nks * (64 / BKS);   // a.nks counts 64-deep steps
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % WN, wm = wave / WN;
   // XCD-aware tile order: blocks b, b+8, ... share an XCD (observed round-robin dispatch);
@@ -517,9 +497,9 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
   const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
-  const int lrow = lane >> 3, lchk = lane & 7;
-  // per-piece constants.  A piece is 8 consecutive pixels of ONE image row (W % 8 == 0, so
-  // p0 + 8q never straddles a row) x 8 16-B chunks: its image row (n, h) is wave-uniform and
+  const int lrow = lane / CH, lchk = lane % CH;
+  // per-piece constants.  A piece is RPP consecutive pixels of ONE image row (W % RPP == 0,
+  // so p0 + RPP*q never straddles a row) x CH 16-B chunks: its image row (n, h) is wave-uniform and
   // the row part of the source address goes to soffset (SALU only); the lane's column part
   // for each tap column s is precomputed once, 0x80000000 marking a column outside the
   // image (the buffer range check then returns 0).  A k-step costs no address VALU beyond
@@ -530,13 +510,13 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
 #pragma unroll
   for (int j = 0; j < JA; ++j) {
     const int q = wave + j * NW;
-    const int pp = __builtin_amdgcn_readfirstlane(p0 + q * 8);
+    const int pp = __builtin_amdgcn_readfirstlane(p0 + q * RPP);
     pok[j] = (QA % NW == 0 || q < QA) && pp < a.P;
     const int n = pp / HW, rem = pp - n * HW;
     const int h = rem / a.W, w0 = rem - h * a.W;
     prn[j] = n * a.Hin;
     prh[j] = h;
-    const unsigned chunk = (unsigned)((lchk ^ swz8(q * 8 + lrow)) << 3);
+    const unsigned chunk = (unsigned)((lchk ^ swzk<BKS>(q * RPP + lrow)) << 3);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int ww = w0 + lrow + s - PAD;
@@ -547,13 +527,13 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   unsigned wbase[JB];
 #pragma unroll
   for (int j = 0; j < JB; ++j) {
-    const int row = (wave + j * NW) * 8 + lrow;
-    wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ swz8(row)) << 3)) * 2);
+    const int row = (wave + j * NW) * RPP + lrow;
+    wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ swzk<BKS>(row)) << 3)) * 2);
   }
 
   constexpr int PW = JA + JB;      // DMA pieces this wave issues per stage (upper bound)
   auto issue = [&](int ks, int buf) {
-    const int k0 = ks * BK2;
+    const int k0 = ks * BKS;
     const unsigned As = sbase + buf * STAGE;
     const unsigned Bs = As + BM * ROWB;
     const int tap = k0 >> a.lgCin, ci0 = k0 & (a.Cin - 1);
@@ -594,12 +574,12 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
 #pragma unroll
     for (int n = 0; n < RN; ++n) {
       const int row = wn * RN * 16 + n * 16 + lr;
-      fa[n].lds(Bs + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
+      fa[n].lds(Bs + row * ROWB + (((kk * 4 + lh) ^ swzk<BKS>(row)) << 4));
     }
 #pragma unroll
     for (int m = 0; m < RM; ++m) {
       const int row = wm * RM * 16 + m * 16 + lr;
-      fb[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swz8(row)) << 4));
+      fb[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swzk<BKS>(row)) << 4));
     }
   };
   auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
@@ -609,7 +589,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
       for (int m = 0; m < RM; ++m) acc[n][m] = mma(fa[n], fb[m], acc[n][m]);
   };
 
-  if (!(a.dbg & 8)) {
+  if (BKS == 64 && !(a.dbg & 8)) {
     // Software-pipelined k loop: the fragments of the next half-step are read while the
     // MFMAs of the current one run, and the per-step barrier sits between the two MFMA
     // groups of a step, so after it the matrix pipe has the second group (already in
@@ -622,32 +602,33 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (a.nks > 1) issue(1, 1);
+    if (nks > 1) issue(1, 1);
     load_frags(fa0, fb0, 0, 0);
-    for (int ks = 0; ks < a.nks; ++ks) {
+    for (int ks = 0; ks < nks; ++ks) {
       const int buf = ks & 1;
       load_frags(fa1, fb1, buf, 1);
       mfma_all(fa0, fb0);
-      if (ks + 1 < a.nks) {
+      if (ks + 1 < nks) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (ks + 2 < a.nks && !(a.dbg & 2)) issue(ks + 2, buf);
+        if (ks + 2 < nks && !(a.dbg & 2)) issue(ks + 2, buf);
         load_frags(fa0, fb0, buf ^ 1, 0);
       }
       mfma_all(fa1, fb1);
     }
   } else {
-    // reference loop (FV_CONV_DBG bit 3): one barrier per step, fragments read per half-step
+    // one barrier per step, fragments read per 32-deep half-step (the BKS = 32 loop, and the
+    // reference loop of FV_CONV_DBG bit 3)
     issue(0, 0);
-    for (int ks = 0; ks < a.nks; ++ks) {
+    for (int ks = 0; ks < nks; ++ks) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      const int nxt = (ks + 1 < a.nks && !(a.dbg & 2)) ? ks + 1 : -1;
+      const int nxt = (ks + 1 < nks && !(a.dbg & 2)) ? ks + 1 : -1;
       if (nxt >= 0) issue(nxt, nxt & 1);
       if (!(a.dbg & 1)) {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+        for (int kk = 0; kk < BKS / 32; ++kk) {
           Frag<bf16> af[RN], bfm[RM];
           load_frags(af, bfm, ks & 1, kk);
           mfma_all(af, bfm);
@@ -1659,16 +1640,28 @@ FwdTile fwd_tile_v2(int rows_needed) {
   return {c.bn, c.bm};
 }
 
-template <int KS, int WN, int WM, int RN, int RM>
-int launch_v2_t(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s) {
+template <int KS, int WN, int WM, int RN, int RM, int BKS>
+int launch_v2_b(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s) {
   dim3 g(nblk), b(64 * WN * WM);
   if (ups) {
-    if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, true>), g, b, 0, s, a, xb);
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, true, BKS>), g, b, 0, s, a, xb);
     else return FV_E_UNSUPPORTED;
   } else {
-    hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, false>), g, b, 0, s, a, xb);
+    hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, false, BKS>), g, b, 0, s, a, xb);
   }
   return FV_OK;
+}
+
+// 4-wave tiles stage 32-deep k slices when K is short (<= 640) or the input is upsampled:
+// there the 4-blocks-per-CU occupancy beats the deeper k step (A/B on the FaceVAE shapes;
+// FV_CONV_DBG bit 4 forces 64)
+template <int KS, int WN, int WM, int RN, int RM>
+int launch_v2_t(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s) {
+  if constexpr (WN * WM == 4) {
+    if (!(a.dbg & 16) && a.W % 16 == 0 && (a.Kpad <= 640 || ups))
+      return launch_v2_b<KS, WN, WM, RN, RM, 32>(a, ups, nblk, xb, s);
+  }
+  return launch_v2_b<KS, WN, WM, RN, RM, 64>(a, ups, nblk, xb, s);
 }
 
 template <int KS>
@@ -1917,11 +1910,25 @@ static FwdTile plan_tile(const fv_conv_desc* d) {
   return use_v2(d) ? fwd_tile_v2(d->cout) : fwd_tile(d->cout);
 }
 
-int fv_conv2d_stats_block_pixels(const fv_conv_desc* d) { return plan_tile(d).bm; }
+// pixels per BN-statistics record = the pixels of one wave row of the tile (BM / WM)
+static int stats_record_pixels(const fv_conv_desc* d) {
+  if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
+  const FwdTile t = plan_tile(d);
+  if (use_v2(d)) {
+    if (t.bn == 64 || t.bn == 16 || (t.bn == 128 && t.bm == 256)) return t.bm / 4;
+    return t.bm / 2;                                          // 128x128, 256x256, 256x128
+  }
+  return t.bn == 16 ? t.bm / 4 : t.bm / 2;                    // v1 layouts (launch_fwd_ks)
+}
+
+int fv_conv2d_stats_block_pixels(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  return stats_record_pixels(d);
+}
 
 int fv_conv2d_stats_blocks(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
-  return fv_cdiv((long)d->n * d->h * d->w, plan_tile(d).bm);
+  return fv_cdiv((long)d->n * d->h * d->w, stats_record_pixels(d));
 }
 
 int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma, void* wk,
@@ -1997,7 +2004,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");
     const FwdTile t2 = fwd_tile_v2(d->cout);
     a.ntn = fv_cdiv(d->cout, t2.bn);
-    a.nks = a.Kpad / BK2;
+    a.nks = a.Kpad / BK2;            // 64-deep steps; the 32-deep kernels double it themselves
     const int nblk2 = a.ntn * fv_cdiv(a.P, t2.bm);
     const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
     st = launch_v2(a, d->ksize, t2, d->upsample, nblk2, (unsigned)xb, s);

@@ -73,7 +73,8 @@ typedef struct fv_conv_desc {
 /* elements of the kernel-layout weight buffers (wk for fwd, wt for bwd-data) */
 size_t fv_conv_wk_elems(const fv_conv_desc* d);
 size_t fv_conv_wt_elems(const fv_conv_desc* d);
-/* number of per-block BN partial records written by fv_conv2d_fwd (stats: [blocks][2][cout]) */
+/* number of BN partial records written by fv_conv2d_fwd (stats: [records][2][cout], each
+ * (sum, sum of squares) over `block_pixels` consecutive output pixels, the last one short) */
 int fv_conv2d_stats_blocks(const fv_conv_desc* d);
 int fv_conv2d_stats_block_pixels(const fv_conv_desc* d);
 
@@ -82,8 +83,8 @@ int fv_conv2d_stats_block_pixels(const fv_conv_desc* d);
 int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma,
                         void* wk, void* wt, void* stream);
 
-/* y = epi(conv(pro(x), wk) + bias [+ res]); stats (optional) receives per-block
- * (sum, centred sum of squares) of the pre-sigmoid output per channel. */
+/* y = epi(conv(pro(x), wk) + bias [+ res]); stats (optional) receives per-record
+ * (sum, sum of squares) of the pre-sigmoid output per channel. */
 int fv_conv2d_fwd(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
                   const float* pro_scale, const float* pro_shift, const void* res, void* y,
                   float* stats, void* stream);
