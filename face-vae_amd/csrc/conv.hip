@@ -42,7 +42,22 @@ struct ConvArgs {
   int dbg;       // experiment knob (FV_CONV_DBG): bit0 skip MFMA (ref loop), bit1 skip DMA after
                  // the prologue, bit2 skip epilogue, bit3 v2 fwd: reference (unpipelined) k loop
   int lgtw;       // > 0: a block's pixels are a (BM >> lgtw) x (1 << lgtw) rectangle at p0
+  // sub-pixel phase of an upsample-conv (v2 MODE 2): the tile space is the LOW-res image
+  // (H x W = Hin x Win, powers of two: lgw, lghw) and tile pixel (n, h, w) of phase
+  // (pa, pb) stores to output pixel (n, 2h + pa, 2w + pb) of the Ho x Wo image
+  int sub;        // 0 = none, else 1 + 2 * pa + pb (set per block)
+  int lgw, lghw, Ho, Wo;
+  int wphase;     // elements per phase block of the weight buffer (MODE 2)
 };
+
+// output pixel of tile-space pixel p (identity unless a sub-pixel phase is set)
+__device__ __forceinline__ int out_pix(const ConvArgs& a, int p) {
+  if (!a.sub) return p;
+  const int ph = a.sub - 1, pa = ph >> 1, pb = ph & 1;
+  const int n = p >> a.lghw, rem = p & ((1 << a.lghw) - 1);
+  const int h = rem >> a.lgw, w = rem & ((1 << a.lgw) - 1);
+  return (n * a.Ho + 2 * h + pa) * a.Wo + 2 * w + pb;
+}
 
 // 16-B chunk swizzle of a 64-B bf16 LDS row (4 chunks): conflict-free ds_read_b128 for the
 // MFMA fragment read (16 consecutive rows, chunk = lane>>4).  f(row) = [0,2,3,1][(row>>2)&3].
@@ -130,8 +145,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
 #pragma unroll
   for (int m = 0; m < RM; ++m) {
     const int loc = wm * RM * 16 + m * 16 + lr;
-    pix_of[m] = a.lgtw ? p0 + (loc >> a.lgtw) * a.W + (loc & ((1 << a.lgtw) - 1)) : p0 + loc;
-    pv[m] = pix_of[m] < a.P;
+    const int tp = a.lgtw ? p0 + (loc >> a.lgtw) * a.W + (loc & ((1 << a.lgtw) - 1)) : p0 + loc;
+    pv[m] = tp < a.P;
+    pix_of[m] = out_pix(a, tp);
   }
 #pragma unroll
   for (int n = 0; n < RN; ++n) {
@@ -211,9 +227,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     __syncthreads();
     for (int idx = tid; idx < BM * CPR; idx += NT) {
       const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
-      const int pix = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
+      const int tp = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
       const int co = co0 + ch * 8;
-      if (pix >= a.P || co >= a.Cout) continue;
+      if (tp >= a.P || co >= a.Cout) continue;
+      const int pix = out_pix(a, tp);
       Chunk8<bf16> v;
       v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
       T* yp = reinterpret_cast<T*>(a.y) + (long)pix * a.ldy + co;
@@ -467,9 +484,14 @@ __device__ __forceinline__ int swzk(int row) {
   else return rswz<bf16>(row);
 }
 
-template <int KS, int WN, int WM, int RN, int RM, bool UPS, int BKS>
+// MODE 0: plain conv; 1: nearest-x2 upsample folded into the addressing (tile space =
+// output); 2: one sub-pixel phase of an upsample + 3x3 conv = a 2x2 conv over the low-res
+// input with phase-folded weights (tile space = low-res image, block phase = lid & 3,
+// KS == 2, taps at offsets {-1, 0} or {0, +1} per phase coordinate).
+template <int KS, int WN, int WM, int RN, int RM, int MODE, int BKS>
 __global__ void __launch_bounds__(64 * WN * WM, (BKS == 32 && WN * WM == 4) ? 4 : 2)
 conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
+  constexpr bool UPS = MODE == 1;
   constexpr int NW = WN * WM;
   constexpr int BN = WN * RN * 16, BM = WM * RM * 16;
   constexpr int PAD = KS / 2;
@@ -489,7 +511,14 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   // neighbours, which share halo rows).  Bijective for any grid size.  Speed only.
   const int nblk = gridDim.x, bid = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int lid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  // MODE 2: the 4 phases of one low-res tile are neighbours (same input rows)
+  const int phase = MODE == 2 ? (lid0 & 3) : 0;
+  const int lid = MODE == 2 ? (lid0 >> 2) : lid0;
+  if constexpr (MODE == 2) a.sub = 1 + phase;
+  const int pa = phase >> 1, pb = phase & 1;
+  // row / column tap offset: centred (MODE 0/1) or per phase (MODE 2)
+  const int roff = MODE == 2 ? pa - 1 : -PAD, coff = MODE == 2 ? pb - 1 : -PAD;
   const int tn = lid % a.ntn, tm = lid / a.ntn;
   const int co0 = tn * BN, p0 = tm * BM;
   const int HW = a.H * a.W;
@@ -519,9 +548,10 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     const unsigned chunk = (unsigned)((lchk ^ swzk<BKS>(q * RPP + lrow)) << 3);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int ww = w0 + lrow + s - PAD;
+      const int ww = w0 + lrow + s + coff;
       const int sc = UPS ? (ww >> 1) : ww;
-      vcol[j][s] = (ww >= 0 && ww < a.W) ? ((unsigned)(sc << a.lgCin) + chunk) * 2u : 0x80000000u;
+      const int wlim = UPS ? a.W : a.Win;
+      vcol[j][s] = (ww >= 0 && ww < wlim) ? ((unsigned)(sc << a.lgCin) + chunk) * 2u : 0x80000000u;
     }
   }
   unsigned wbase[JB];
@@ -544,9 +574,9 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
       for (int j = 0; j < JA; ++j) {
         const int q = wave + j * NW;
         if (QA % NW == 0 || q < QA) {
-          const int hh = prh[j] + r - PAD;
+          const int hh = prh[j] + r + roff;
           const int srow = UPS ? (hh >> 1) : hh;
-          if (pok[j] && hh >= 0 && hh < a.H)
+          if (pok[j] && hh >= 0 && hh < (UPS ? a.H : a.Hin))
             dma16s(xr, As + q * 1024, vcol[j][S], (unsigned)((((prn[j] + srow) * a.Win) << a.lgCin) + ci0) * 2u);
           else
             dma16s(xr, As + q * 1024, 0x80000000u, 0u);
@@ -556,7 +586,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
 #pragma unroll
     for (int j = 0; j < JB; ++j) {
       const int q = wave + j * NW;
-      if (QB % NW == 0 || q < QB) dma16s(wr, Bs + q * 1024, wbase[j], (unsigned)(k0 * 2));
+      if (QB % NW == 0 || q < QB) dma16s(wr, Bs + q * 1024, wbase[j], (unsigned)((k0 + phase * a.wphase) * 2));
     }
   };
 
@@ -641,7 +671,8 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.y)[tid] = acc[RN - 1][RM - 1][3];
     return;
   }
-  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, MODE == 2 ? tm * 4 + phase : tm, wn, wm, lane,
+                                             tid);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -1494,6 +1525,33 @@ __global__ void weight_prep_kernel(const float* __restrict__ wp, const float* si
   }
 }
 
+// sub-pixel phase weights of an upsample + 3x3 conv: for phase (pa, pb) the 2x2 tap (r', s')
+// sums the 3x3 taps that land on the same low-res input pixel (rows r in [lo, hi] with
+// lo = r' ? 1 + pa : 0, hi = r' ? 2 : pa; columns alike).  wk [4][rows][Kpad], k = (r'*2+s')*cin + ci.
+template <typename T>
+__global__ void weight_prep_subpix_kernel(const float* __restrict__ wp, const float* sigma, T* wk, int rows, int Kpad,
+                                          int cout, int cin_valid, int lgCin) {
+  const long per = (long)rows * Kpad, total = 4 * per;
+  const float inv = sigma ? 1.f / sigma[0] : 1.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int ph = (int)(e / per);
+    const long e2 = e - ph * per;
+    const int row = (int)(e2 / Kpad), k = (int)(e2 - (long)row * Kpad);
+    const int pa = ph >> 1, pb = ph & 1;
+    const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
+    float v = 0.f;
+    if (tap < 4 && row < cout && c < cin_valid) {
+      const int rr = tap >> 1, ss = tap & 1;
+      const int r0 = rr ? 1 + pa : 0, r1 = rr ? 2 : pa;
+      const int s0 = ss ? 1 + pb : 0, s1 = ss ? 2 : pb;
+      const float* w = wp + ((long)row * cin_valid + c) * 9;
+      for (int r = r0; r <= r1; ++r)
+        for (int q = s0; q <= s1; ++q) v += w[r * 3 + q];
+    }
+    wk[e] = Elt<T>::from_f(v * inv);
+  }
+}
+
 // sum of the per-split slabs -> dW in the reference layout [co][ci][r][s] (+ db).  Block =
 // 64 consecutive outputs x 4 split lanes (4 independent partial sums each), so that large
 // split counts do not serialise on load latency; blocks >= nb_main reduce the bias slab.
@@ -1640,14 +1698,19 @@ FwdTile fwd_tile_v2(int rows_needed) {
   return {c.bn, c.bm};
 }
 
+// mode: 0 plain, 1 upsample folded (KS 3), 2 sub-pixel phases (KS 2)
 template <int KS, int WN, int WM, int RN, int RM, int BKS>
-int launch_v2_b(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s) {
+int launch_v2_b(const ConvArgs& a, int mode, int nblk, unsigned xb, hipStream_t s) {
   dim3 g(nblk), b(64 * WN * WM);
-  if (ups) {
-    if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, true, BKS>), g, b, 0, s, a, xb);
+  if (mode == 2) {
+    if constexpr (KS == 2) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 2, BKS>), g, b, 0, s, a, xb);
+    else return FV_E_UNSUPPORTED;
+  } else if (mode == 1) {
+    if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 1, BKS>), g, b, 0, s, a, xb);
     else return FV_E_UNSUPPORTED;
   } else {
-    hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, false, BKS>), g, b, 0, s, a, xb);
+    if constexpr (KS != 2) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 0, BKS>), g, b, 0, s, a, xb);
+    else return FV_E_UNSUPPORTED;
   }
   return FV_OK;
 }
@@ -1656,16 +1719,17 @@ int launch_v2_b(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s
 // there the 4-blocks-per-CU occupancy beats the deeper k step (A/B on the FaceVAE shapes;
 // FV_CONV_DBG bit 4 forces 64)
 template <int KS, int WN, int WM, int RN, int RM>
-int launch_v2_t(const ConvArgs& a, int ups, int nblk, unsigned xb, hipStream_t s) {
+int launch_v2_t(const ConvArgs& a, int mode, int nblk, unsigned xb, hipStream_t s) {
   if constexpr (WN * WM == 4) {
-    if (!(a.dbg & 16) && a.W % 16 == 0 && (a.Kpad <= 640 || ups))
-      return launch_v2_b<KS, WN, WM, RN, RM, 32>(a, ups, nblk, xb, s);
+    if (!(a.dbg & 16) && a.W % 16 == 0 && (a.Kpad <= 640 || mode != 0))
+      return launch_v2_b<KS, WN, WM, RN, RM, 32>(a, mode, nblk, xb, s);
   }
-  return launch_v2_b<KS, WN, WM, RN, RM, 64>(a, ups, nblk, xb, s);
+  return launch_v2_b<KS, WN, WM, RN, RM, 64>(a, mode, nblk, xb, s);
 }
 
 template <int KS>
-int launch_v2_ks(const ConvArgs& a, FwdTile t, int ups, int nblk, unsigned xb, hipStream_t s) {
+int launch_v2_ks(const ConvArgs& a, FwdTile t, int mode, int nblk, unsigned xb, hipStream_t s) {
+  const int ups = mode;
   if (t.bn == 128 && t.bm == 128) return launch_v2_t<KS, 2, 2, 4, 4>(a, ups, nblk, xb, s);
   if (t.bn == 64) return launch_v2_t<KS, 1, 4, 4, 4>(a, ups, nblk, xb, s);
   if (t.bn == 16) return launch_v2_t<KS, 1, 4, 1, 4>(a, ups, nblk, xb, s);
@@ -1677,11 +1741,28 @@ int launch_v2_ks(const ConvArgs& a, FwdTile t, int ups, int nblk, unsigned xb, h
 
 int launch_v2(const ConvArgs& a, int ks, FwdTile t, int ups, int nblk, unsigned xb, hipStream_t s) {
   switch (ks) {
+    case 2: return launch_v2_ks<2>(a, t, 2, nblk, xb, s);       // sub-pixel phases only
     case 1: return launch_v2_ks<1>(a, t, ups, nblk, xb, s);
     case 3: return launch_v2_ks<3>(a, t, ups, nblk, xb, s);
     case 7: return launch_v2_ks<7>(a, t, ups, nblk, xb, s);
   }
   return FV_E_UNSUPPORTED;
+}
+
+// upsample + 3x3 conv as 4 sub-pixel phases of a 2x2 conv over the low-res input (bf16 v2
+// path; FV_DISABLE_SUBPIX=1 keeps the folded-upsample 3x3 kernel).  2.25x fewer MACs than the
+// reference formulation (reported utilisation still uses the reference FLOPs).
+static int g_disable_subpix = -1;
+bool use_subpix(const fv_conv_desc* d) {
+  if (g_disable_subpix < 0) {
+    const char* e = getenv("FV_DISABLE_SUBPIX");
+    g_disable_subpix = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_disable_subpix || !d->upsample || d->ksize != 3 || !use_v2(d)) return false;
+  const int hl = d->h / 2, wl = d->w / 2;
+  if (fv_ilog2(hl) < 0 || fv_ilog2(wl) < 0 || wl % 16) return false;
+  const long pl = (long)d->n * hl * wl;
+  return pl % fwd_tile_v2(d->cout).bm == 0;
 }
 
 int check_desc(const fv_conv_desc* d) {
@@ -1878,7 +1959,9 @@ extern "C" {
 size_t fv_conv_wk_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const FwdTile t = fwd_tile(d->cout);
-  return (size_t)fv_cdiv(d->cout, t.bn) * t.bn * kpad_of(d->ksize, d->cin);
+  const size_t rows = (size_t)fv_cdiv(d->cout, t.bn) * t.bn;
+  if (use_subpix(d)) return 4 * rows * kpad_of(2, d->cin);
+  return rows * kpad_of(d->ksize, d->cin);
 }
 
 size_t fv_conv_wt_elems(const fv_conv_desc* d) {
@@ -1937,7 +2020,15 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   if (st) return st;
   hipStream_t s = (hipStream_t)stream;
   const int ks = d->ksize;
-  if (wk) {
+  if (wk && use_subpix(d)) {
+    const FwdTile t = fwd_tile(d->cout);
+    const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_of(2, d->cin);
+    const long tot = 4L * rows * Kp;
+    const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
+    hipLaunchKernelGGL(weight_prep_subpix_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wk, rows, Kp,
+                       d->cout, d->cin_valid, fv_ilog2(d->cin));
+    if ((st = fv_check_launch("weight_prep_subpix"))) return st;
+  } else if (wk) {
     const FwdTile t = fwd_tile(d->cout);
     const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_of(ks, d->cin);
     const long tot = (long)rows * Kp;
@@ -1999,6 +2090,26 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     else
       hipLaunchKernelGGL((conv_halo_fwd<7, 64, 1, 2, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
     return fv_check_launch("conv2d_fwd_halo");
+  }
+  if (use_subpix(d)) {
+    FV_REQUIRE(!res, "sub-pixel conv: no residual");
+    const FwdTile t2 = fwd_tile_v2(d->cout);
+    a.H = a.Hin; a.W = a.Win;                       // tile space = the low-res input image
+    a.Ho = d->h; a.Wo = d->w;
+    a.P = d->n * a.H * a.W;
+    a.lgw = fv_ilog2(a.W); a.lghw = fv_ilog2(a.H * a.W);
+    a.Kpad = kpad_of(2, d->cin);
+    a.nks = a.Kpad / BK2;
+    a.ntn = fv_cdiv(d->cout, t2.bn);
+    a.wphase = fv_cdiv(d->cout, t.bn) * t.bn * a.Kpad;
+    const int nblk2 = 4 * a.ntn * (a.P / t2.bm);
+    const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
+    st = launch_v2(a, 2, t2, 2, nblk2, (unsigned)xb, s);
+    if (st) {
+      fv_set_error("sub-pixel conv variant unsupported (cout=%d)", d->cout);
+      return st;
+    }
+    return fv_check_launch("conv2d_fwd_subpix");
   }
   if (use_v2(d)) {
     FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");
