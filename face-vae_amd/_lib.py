@@ -51,6 +51,7 @@ _SIGS = {
     "fv_conv_weight_prep": (c_int, [D, P, P, P, P, P]),
     "fv_conv2d_fwd": (c_int, [D, P, P, P, P, P, P, P, P, P]),
     "fv_conv2d_bwd_data": (c_int, [D, P, c_int, P, P, P]),
+    "fv_conv2d_dgrad_lowres": (c_int, [D]),
     "fv_conv2d_wgrad_nsplit": (c_int, [D]),
     "fv_conv2d_wgrad_slab_elems": (c_size_t, [D]),
     "fv_conv2d_wgrad_bias_slab_elems": (c_size_t, [D]),

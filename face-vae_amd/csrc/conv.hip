@@ -487,7 +487,9 @@ __device__ __forceinline__ int swzk(int row) {
 // MODE 0: plain conv; 1: nearest-x2 upsample folded into the addressing (tile space =
 // output); 2: one sub-pixel phase of an upsample + 3x3 conv = a 2x2 conv over the low-res
 // input with phase-folded weights (tile space = low-res image, block phase = lid & 3,
-// KS == 2, taps at offsets {-1, 0} or {0, +1} per phase coordinate).
+// KS == 2, taps at offsets {-1, 0} or {0, +1} per phase coordinate); 3: stride-2 4x4 conv
+// (input coordinate 2 * out + tap - 1): the data gradient of an upsample + 3x3 conv
+// straight at the low resolution (tile space = low-res dx, input = high-res dy).
 template <int KS, int WN, int WM, int RN, int RM, int MODE, int BKS>
 __global__ void __launch_bounds__(64 * WN * WM, (BKS == 32 && WN * WM == 4) ? 4 : 2)
 conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
@@ -517,8 +519,10 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   const int lid = MODE == 2 ? (lid0 >> 2) : lid0;
   if constexpr (MODE == 2) a.sub = 1 + phase;
   const int pa = phase >> 1, pb = phase & 1;
-  // row / column tap offset: centred (MODE 0/1) or per phase (MODE 2)
-  const int roff = MODE == 2 ? pa - 1 : -PAD, coff = MODE == 2 ? pb - 1 : -PAD;
+  // row / column tap offset: centred (MODE 0/1), per phase (MODE 2), -1 after the stride (3)
+  const int roff = MODE == 2 ? pa - 1 : MODE == 3 ? -1 : -PAD;
+  const int coff = MODE == 2 ? pb - 1 : MODE == 3 ? -1 : -PAD;
+  constexpr int STR = MODE == 3 ? 2 : 1;
   const int tn = lid % a.ntn, tm = lid / a.ntn;
   const int co0 = tn * BN, p0 = tm * BM;
   const int HW = a.H * a.W;
@@ -548,7 +552,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     const unsigned chunk = (unsigned)((lchk ^ swzk<BKS>(q * RPP + lrow)) << 3);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int ww = w0 + lrow + s + coff;
+      const int ww = STR * (w0 + lrow) + s + coff;
       const int sc = UPS ? (ww >> 1) : ww;
       const int wlim = UPS ? a.W : a.Win;
       vcol[j][s] = (ww >= 0 && ww < wlim) ? ((unsigned)(sc << a.lgCin) + chunk) * 2u : 0x80000000u;
@@ -574,7 +578,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
       for (int j = 0; j < JA; ++j) {
         const int q = wave + j * NW;
         if (QA % NW == 0 || q < QA) {
-          const int hh = prh[j] + r + roff;
+          const int hh = STR * prh[j] + r + roff;
           const int srow = UPS ? (hh >> 1) : hh;
           if (pok[j] && hh >= 0 && hh < (UPS ? a.H : a.Hin))
             dma16s(xr, As + q * 1024, vcol[j][S], (unsigned)((((prn[j] + srow) * a.Win) << a.lgCin) + ci0) * 2u);
@@ -1552,6 +1556,29 @@ __global__ void weight_prep_subpix_kernel(const float* __restrict__ wp, const fl
   }
 }
 
+// stride-2 4x4 weights of the low-res data gradient of an upsample + 3x3 conv:
+// wt[ci][(tr*4 + tc)*cin_t + co] = sum of W[co][ci][r][s] over r in [max(0, 2-tr), min(2, 3-tr)]
+// and s alike (dy row 2u + tr - 1 reaches low-res row u through those taps).
+template <typename T>
+__global__ void weight_prep_s2_kernel(const float* __restrict__ wp, const float* sigma, T* wt, int rows, int Kpad,
+                                      int cout, int cin_valid, int lgCt) {
+  const long total = (long)rows * Kpad;
+  const float inv = sigma ? 1.f / sigma[0] : 1.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(e / Kpad), k = (int)(e - (long)row * Kpad);
+    const int tap = k >> lgCt, co = k & ((1 << lgCt) - 1);
+    float v = 0.f;
+    if (tap < 16 && row < cin_valid && co < cout) {
+      const int tr = tap >> 2, tc = tap & 3;
+      const int r0 = max(0, 2 - tr), r1 = min(2, 3 - tr), s0 = max(0, 2 - tc), s1 = min(2, 3 - tc);
+      const float* w = wp + ((long)co * cin_valid + row) * 9;
+      for (int r = r0; r <= r1; ++r)
+        for (int q = s0; q <= s1; ++q) v += w[r * 3 + q];
+    }
+    wt[e] = Elt<T>::from_f(v * inv);
+  }
+}
+
 // sum of the per-split slabs -> dW in the reference layout [co][ci][r][s] (+ db).  Block =
 // 64 consecutive outputs x 4 split lanes (4 independent partial sums each), so that large
 // split counts do not serialise on load latency; blocks >= nb_main reduce the bias slab.
@@ -1702,14 +1729,17 @@ FwdTile fwd_tile_v2(int rows_needed) {
 template <int KS, int WN, int WM, int RN, int RM, int BKS>
 int launch_v2_b(const ConvArgs& a, int mode, int nblk, unsigned xb, hipStream_t s) {
   dim3 g(nblk), b(64 * WN * WM);
-  if (mode == 2) {
+  if (mode == 3) {
+    if constexpr (KS == 4) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 3, BKS>), g, b, 0, s, a, xb);
+    else return FV_E_UNSUPPORTED;
+  } else if (mode == 2) {
     if constexpr (KS == 2) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 2, BKS>), g, b, 0, s, a, xb);
     else return FV_E_UNSUPPORTED;
   } else if (mode == 1) {
     if constexpr (KS == 3) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 1, BKS>), g, b, 0, s, a, xb);
     else return FV_E_UNSUPPORTED;
   } else {
-    if constexpr (KS != 2) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 0, BKS>), g, b, 0, s, a, xb);
+    if constexpr (KS != 2 && KS != 4) hipLaunchKernelGGL((conv_fwd_v2<KS, WN, WM, RN, RM, 0, BKS>), g, b, 0, s, a, xb);
     else return FV_E_UNSUPPORTED;
   }
   return FV_OK;
@@ -1742,6 +1772,7 @@ int launch_v2_ks(const ConvArgs& a, FwdTile t, int mode, int nblk, unsigned xb, 
 int launch_v2(const ConvArgs& a, int ks, FwdTile t, int ups, int nblk, unsigned xb, hipStream_t s) {
   switch (ks) {
     case 2: return launch_v2_ks<2>(a, t, 2, nblk, xb, s);       // sub-pixel phases only
+    case 4: return launch_v2_ks<4>(a, t, 3, nblk, xb, s);       // stride-2 low-res dgrad only
     case 1: return launch_v2_ks<1>(a, t, ups, nblk, xb, s);
     case 3: return launch_v2_ks<3>(a, t, ups, nblk, xb, s);
     case 7: return launch_v2_ks<7>(a, t, ups, nblk, xb, s);
@@ -1763,6 +1794,17 @@ bool use_subpix(const fv_conv_desc* d) {
   if (fv_ilog2(hl) < 0 || fv_ilog2(wl) < 0 || wl % 16) return false;
   const long pl = (long)d->n * hl * wl;
   return pl % fwd_tile_v2(d->cout).bm == 0;
+}
+
+// data gradient of an upsample + 3x3 conv computed directly at the low resolution as a
+// stride-2 4x4 conv over dy (bf16 v2 path; replaces dgrad at the high resolution followed by
+// the 2x2 sum of fv_upsample2x_bwd: 0.44x the MACs, one pass fewer)
+bool use_dgrad_lowres(const fv_conv_desc* d) {
+  if (g_disable_subpix < 0) use_subpix(d);     // reads FV_DISABLE_SUBPIX
+  if (g_disable_subpix || !d->upsample || d->ksize != 3 || d->dtype != FV_BF16) return false;
+  const int ct = pad_pow2_8(d->cout);
+  if (ct % 64 || d->cin % 8 || (d->w / 2) % 16) return false;
+  return (long)d->n * d->h * d->w * ct * 2 < (1L << 31);
 }
 
 int check_desc(const fv_conv_desc* d) {
@@ -1968,7 +2010,14 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const int cin_t = pad_pow2_8(d->cout);
   const FwdTile t = fwd_tile(d->cin);
-  return (size_t)fv_cdiv(d->cin, t.bn) * t.bn * kpad_of(d->ksize, cin_t);
+  const size_t rows = (size_t)fv_cdiv(d->cin, t.bn) * t.bn;
+  if (use_dgrad_lowres(d)) return rows * 16 * cin_t;
+  return rows * kpad_of(d->ksize, cin_t);
+}
+
+int fv_conv2d_dgrad_lowres(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  return use_dgrad_lowres(d) ? 1 : 0;
 }
 
 // 7x7 halo path: (cin 8 -> cout 64, TR 8, weights in LDS) or (cin 64 -> cout <= 16, TR 2)
@@ -2041,7 +2090,16 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
                          rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0);
     if ((st = fv_check_launch("weight_prep"))) return st;
   }
-  if (wt) {
+  if (wt && use_dgrad_lowres(d)) {
+    const int cin_t = pad_pow2_8(d->cout);
+    const FwdTile t = fwd_tile(d->cin);
+    const int rows = fv_cdiv(d->cin, t.bn) * t.bn, Kp = 16 * cin_t;
+    const long tot = (long)rows * Kp;
+    const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
+    hipLaunchKernelGGL(weight_prep_s2_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wt, rows, Kp,
+                       d->cout, d->cin_valid, fv_ilog2(cin_t));
+    if ((st = fv_check_launch("weight_prep_s2"))) return st;
+  } else if (wt) {
     const int cin_t = pad_pow2_8(d->cout);
     const FwdTile t = fwd_tile(d->cin);
     const int rows = fv_cdiv(d->cin, t.bn) * t.bn, Kp = kpad_of(ks, cin_t);
@@ -2161,6 +2219,32 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
   t.cout = d->cin;   // every (padded) input channel; padded ones come out 0
   t.ldy = d->cin;
   t.ksize = d->ksize;
+  if (use_dgrad_lowres(d)) {
+    FV_REQUIRE(dy && wt && dx, "null pointer");
+    ConvArgs a{};
+    const FwdTile t2 = fwd_tile_v2(d->cin);
+    a.x = dy; a.w = wt; a.y = dx;
+    a.N = d->n; a.H = d->h / 2; a.W = d->w / 2; a.Hin = d->h; a.Win = d->w;
+    a.Ho = a.H; a.Wo = a.W;
+    a.P = d->n * a.H * a.W;
+    a.Cin = t.cin; a.lgCin = fv_ilog2(t.cin);
+    a.Cout = d->cin; a.ldy = d->cin;
+    a.Kpad = 16 * t.cin; a.K = a.Kpad; a.nks = a.Kpad / BK2;
+    a.ntn = fv_cdiv(d->cin, t2.bn);
+    if (g_conv_dbg < 0) {
+      const char* e = getenv("FV_CONV_DBG");
+      g_conv_dbg = e ? atoi(e) : 0;
+    }
+    a.dbg = g_conv_dbg;
+    const int nblk = a.ntn * fv_cdiv(a.P, t2.bm);
+    const long xb = (long)d->n * d->h * d->w * t.cin * 2;
+    const int st = launch_v2(a, 4, t2, 3, nblk, (unsigned)xb, (hipStream_t)stream);
+    if (st) {
+      fv_set_error("low-res dgrad variant unsupported (cin=%d)", d->cin);
+      return st;
+    }
+    return fv_check_launch("conv2d_bwd_data_lowres");
+  }
   return conv_run(&t, dy, wt, nullptr, nullptr, nullptr, nullptr, dx, nullptr, (hipStream_t)stream);
 }
 

@@ -232,7 +232,12 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
     if cs.conv.sn:
         spectral_norm_bwd(cs.w, dw, cs.u, cs.v, cs.sigma)
     dx = None
-    if need_dx:
+    if need_dx and d.upsample and query("fv_conv2d_dgrad_lowres", ctypes.byref(d)):
+        # gradient of the upsample's (low-res) input in one stride-2 pass
+        dx = torch.empty((d.n, d.cin, d.h // 2, d.w // 2), dtype=dy.dtype, device=dev, memory_format=CL)
+        _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data", ctypes.byref(d), ptr(dy), ldd, ptr(cs.wt), ptr(dx),
+                                        stream()))
+    elif need_dx:
         dx = torch.empty((d.n, d.cin, d.h, d.w), dtype=dy.dtype, device=dev, memory_format=CL)
         _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data", ctypes.byref(d), ptr(dy), ldd, ptr(cs.wt), ptr(dx),
                                         stream()))

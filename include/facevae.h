@@ -94,6 +94,11 @@ int fv_conv2d_fwd(const fv_conv_desc* d, const void* x, const void* wk, const fl
  * fv_upsample2x_bwd).  dy has channel stride ldy_dy (>= cout, multiple of 8). */
 int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt,
                        void* dx, void* stream);
+/* 1 when, for this upsample descriptor, fv_conv2d_bwd_data writes dx directly at the LOW
+ * (conv input, h/2 x w/2) resolution -- the gradient of the upsample's input, computed as a
+ * stride-2 4x4 conv over dy -- and wt (fv_conv_wt_elems / fv_conv_weight_prep) holds those
+ * 4x4 weights; then no fv_upsample2x_bwd follows.  0 otherwise. */
+int fv_conv2d_dgrad_lowres(const fv_conv_desc* d);
 
 /* weight gradient w.r.t. the effective (post-SN) weight, split over pixels:
  * slab [nsplit][rows][Kpad] fp32 and bias slab [nsplit][rows] fp32 (sizes from the queries). */

@@ -151,7 +151,12 @@ def test_conv_bwd(case, dtype):
     assert rel(dw, wr.grad) < tol
     assert rel(db, br.grad) < tol
     # data gradient (w.r.t. the conv input, before the prologue)
-    if not pro:
+    if not pro and ups and L.query("fv_conv2d_dgrad_lowres", ctypes.byref(d)):
+        dx = torch.empty((2, xb.shape[1], H, W), dtype=dtype, device="cuda", memory_format=CL)
+        L.call("fv_conv2d_bwd_data", ctypes.byref(d), gyb.data_ptr(), ldd, wt.data_ptr(), dx.data_ptr(), L.stream())
+        torch.cuda.synchronize()
+        assert rel(dx[:, :cin].float(), xr.grad) < tol
+    elif not pro:
         dx = torch.empty((2, xb.shape[1], shp[2], shp[3]), dtype=dtype, device="cuda", memory_format=CL)
         L.call("fv_conv2d_bwd_data", ctypes.byref(d), gyb.data_ptr(), ldd, wt.data_ptr(), dx.data_ptr(), L.stream())
         if ups:
