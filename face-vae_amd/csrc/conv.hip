@@ -1088,6 +1088,10 @@ struct Wg2Args {
   FastDiv fhw, fw, fh;
   unsigned xbytes, dybytes;
   int rowal;   // W % PX == 0: each stage lies in one image row
+  // sub-pixel phases of an upsample + 3x3 conv (SUB): pixels are the LOW-res image (H x W),
+  // the block's phase (pa, pb) pairs low-res pixel (n, i, j) with dy pixel (n, 2i+pa, 2j+pb)
+  // of the Ho x Wo image; phase slabs follow each other ([4][nsplit][CW][KW])
+  int Ho, Wo, nsplit;
 };
 
 // 32-B-block XOR of a [row][NCOL] bf16 image: the 8 rows {0-3, 8-11} (and {4-7, 12-15}) one
@@ -1120,9 +1124,21 @@ __device__ __forceinline__ bf16x8 tfrag(const char* base, int r0, int cbase, int
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-template <int KS, int BKT, int BC, int WK, int WC, int PX, int NS, bool UPS>
+// ring wait: retire the oldest stage while `ahead` (0 .. NS-2, run-time) younger ones stay in flight
+template <int NS, int PW, int A = NS - 2>  // vmcnt immediate <= 63: (NS - 2) * PW must fit
+__device__ __forceinline__ void wait_ahead(int ahead) {
+  if constexpr (A <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (ahead >= A) wait_vmcnt<A * PW>();
+    else wait_ahead<NS, PW, A - 1>(ahead);
+  }
+}
+
+template <int KS, int BKT, int BC, int WK, int WC, int PX, int NS, bool UPS, bool SUB = false>
 __global__ void __launch_bounds__(512, 2)
 conv_wgrad_v2(Wg2Args a) {
+  static_assert(!SUB || (KS == 2 && !UPS), "sub-pixel wgrad: 2x2 taps, no upsample");
   static_assert(WK * WC == 8, "8 waves");
   constexpr int RK = BKT / (16 * WK), RC = BC / (16 * WC);
   static_assert(RK * 16 * WK == BKT && RC * 16 * WC == BC, "wave tiling");
@@ -1142,7 +1158,10 @@ conv_wgrad_v2(Wg2Args a) {
   // x rows) share an XCD's L2.  Bijective remap; speed only.
   const int nblk = gridDim.x, bid = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int lid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int phase = SUB ? (lid0 & 3) : 0;      // the 4 phases of a split are neighbours
+  const int lid = SUB ? (lid0 >> 2) : lid0;
+  const int pa = phase >> 1, pb = phase & 1;
   const int ntile = a.ntk * a.ntc;
   const int split = lid / ntile, tile = lid - split * ntile;
   const int tc = tile % a.ntc, tk = tile / a.ntc;
@@ -1166,8 +1185,8 @@ conv_wgrad_v2(Wg2Args a) {
     const int tap = k >> a.lgCin;
     const int r = tap / KS, s = tap - (tap / KS) * KS;
     arow[j] = row;
-    adh[j] = r - PAD;
-    adw[j] = s - PAD;
+    adh[j] = SUB ? r + pa - 1 : r - PAD;
+    adw[j] = SUB ? s + pb - 1 : s - PAD;
     aci[j] = k & ((1 << a.lgCin) - 1);
     akin[j] = (QA % 8 == 0 || q < QA) && k < a.K;
   }
@@ -1202,7 +1221,7 @@ conv_wgrad_v2(Wg2Args a) {
   }
   unsigned cB[JB];
 #pragma unroll
-  for (int j = 0; j < JB; ++j) cB[j] = bok[j] ? (unsigned)(brow[j] * a.ldd + bco[j]) * 2u : 0x80000000u;
+  for (int j = 0; j < JB; ++j) cB[j] = bok[j] ? (unsigned)(brow[j] * (SUB ? 2 : 1) * a.ldd + bco[j]) * 2u : 0x80000000u;
   const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
 
   auto issue_rowal = [&](int st, int buf) {
@@ -1230,14 +1249,16 @@ conv_wgrad_v2(Wg2Args a) {
     for (int j = 0; j < JB; ++j) {
       const int q = wave + j * 8;
       if (QB % 8 == 0 || q < QB) {
-        if (sok) dma16s(dr, Bs + q * 1024, cB[j], (unsigned)pbase * (unsigned)a.ldd * 2u);
+        // dy pixel of the stage's first pixel: itself, or (n, 2h+pa, 2*w0+pb) for a phase
+        const unsigned dp = SUB ? (unsigned)((n * a.Ho + 2 * h + pa) * a.Wo + 2 * w0 + pb) : (unsigned)pbase;
+        if (sok) dma16s(dr, Bs + q * 1024, cB[j], dp * (unsigned)a.ldd * 2u);
         else dma16s(dr, Bs + q * 1024, 0x80000000u, 0u);
       }
     }
   };
 
   auto issue = [&](int st, int buf) {
-    if (a.rowal) {
+    if (SUB || a.rowal) {        // SUB: the host only launches row-aligned stages
       issue_rowal(st, buf);
       return;
     }
@@ -1316,16 +1337,7 @@ conv_wgrad_v2(Wg2Args a) {
     if (i < nst) issue(i, i);
   for (int it = 0; it < nst; ++it) {
     const int ahead = min(NS - 2, nst - 1 - it);   // younger stages allowed in flight
-    if constexpr (NS >= 4) {
-      if (ahead >= 2) wait_vmcnt<2 * PW>();
-      else if (ahead == 1) wait_vmcnt<PW>();
-      else wait_vmcnt<0>();
-    } else if constexpr (NS == 3) {
-      if (ahead >= 1) wait_vmcnt<PW>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
+    wait_ahead<NS, PW>(ahead);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (it + NS - 1 < nst) issue(it + NS - 1, (it + NS - 1) % NS);
@@ -1334,7 +1346,7 @@ conv_wgrad_v2(Wg2Args a) {
 
   // D[k][co]: lane holds k = kb + 4*(lane>>4) + i for co = cb + (lane & 15)
   const int lr = lane & 15, lh = lane >> 4;
-  float* slab = a.slab + (long)split * a.CW * a.KW;
+  float* slab = a.slab + (long)(SUB ? phase * a.nsplit + split : split) * a.CW * a.KW;
 #pragma unroll
   for (int i = 0; i < RK; ++i) {
     const int kb = k0 + wk * RK * 16 + i * 16 + lh * 4;
@@ -1347,7 +1359,8 @@ conv_wgrad_v2(Wg2Args a) {
   }
   if (do_bias && lh == 0) {
 #pragma unroll
-    for (int j = 0; j < RC; ++j) a.bslab[(long)split * a.CW + c0 + wc * RC * 16 + j * 16 + lr] = accb[j][0];
+    for (int j = 0; j < RC; ++j)
+      a.bslab[(long)(SUB ? phase * a.nsplit + split : split) * a.CW + c0 + wc * RC * 16 + j * 16 + lr] = accb[j][0];
   }
 }
 
@@ -1576,6 +1589,48 @@ __global__ void weight_prep_s2_kernel(const float* __restrict__ wp, const float*
         for (int q = s0; q <= s1; ++q) v += w[r * 3 + q];
     }
     wt[e] = Elt<T>::from_f(v * inv);
+  }
+}
+
+// sub-pixel phase slabs [4][nsplit][CW][KW] (k = (r'*2+s')*cin + ci) -> dW [co][ci][3][3]:
+// each 3x3 tap r takes, per phase row pa, the 2x2 tap r' whose folded range holds it
+// (pa = 0: r' = r > 0; pa = 1: r' = r == 2), columns alike; + db from the bias slabs.
+// One wave per 64 outputs, 4 lanes per output summing interleaved splits.
+__global__ void wgrad_reduce_subpix_kernel(const float* __restrict__ slab, const float* __restrict__ bslab, float* dw,
+                                           float* db, int nsplit, int CW, int KW, int cout, int cin_valid,
+                                           int lgCin, int nb_main) {
+  const int sg = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __shared__ float red[4][64];
+  float g = 0.f;
+  long dst = -1;
+  const int nterm = 4 * nsplit;
+  if ((int)blockIdx.x < nb_main) {
+    const long e = (long)blockIdx.x * 64 + l;
+    const long tot = (long)cout * cin_valid * 9;
+    if (e < tot) {
+      dst = e;
+      const int rs = (int)(e % 9), ci = (int)((e / 9) % cin_valid), co = (int)(e / (9L * cin_valid));
+      const int r = rs / 3, sc = rs % 3;
+      for (int t = sg; t < nterm; t += 4) {
+        const int ph = t / nsplit, sp = t - ph * nsplit;
+        const int pa = ph >> 1, pb = ph & 1;
+        const int rr = pa ? (r == 2) : (r > 0), ss = pb ? (sc == 2) : (sc > 0);
+        g += slab[((long)(ph * nsplit + sp) * CW + co) * KW + (((rr * 2 + ss) << lgCin) + ci)];
+      }
+    }
+  } else {
+    const int co = ((int)blockIdx.x - nb_main) * 64 + l;
+    if (co < cout) {
+      dst = co;
+      for (int t = sg; t < nterm; t += 4) g += bslab[(long)t * CW + co];
+    }
+  }
+  red[sg][l] = g;
+  __syncthreads();
+  if (sg == 0 && dst >= 0) {
+    const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    if ((int)blockIdx.x < nb_main) dw[dst] = v;
+    else db[dst] = v;
   }
 }
 
@@ -1834,7 +1889,7 @@ static int halo_wg_tr(const fv_conv_desc* d) {
 
 // wgrad plan: v2 (bf16 DMA-fed, 8 waves), halo (7x7), or the register-staged v1 (fp32 / BN prologue)
 struct WgPlan {
-  int v2, bkt, bc, px, ntk, ntc, nsplit, nsteps, sps, KW, CW, cfg;
+  int v2, bkt, bc, px, ntk, ntc, nsplit, nsteps, sps, KW, CW, cfg, sub;
 };
 
 // wgrad v2 tile configs: k rows x co cols per block, 8 waves as wk x wc, pixels per stage,
@@ -1852,6 +1907,8 @@ constexpr Wg2Cfg kWg2Cfg[] = {
     {384, 64, 4, 2, 64, 2},    // 8
     {128, 128, 2, 4, 32, 4},   // 9
     {256, 128, 4, 2, 32, 4},   // 10
+    {256, 64, 8, 1, 64, 3},    // 11 (sub-pixel phases of the 64-channel up conv, K = 512)
+    {512, 64, 8, 1, 64, 2},    // 12
 };
 constexpr int kNumWg2Cfg = sizeof(kWg2Cfg) / sizeof(kWg2Cfg[0]);
 static int g_wg2_force = -2;
@@ -1902,6 +1959,30 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
     p.CW = p.bc;
     return p;
   }
+  if (p.v2 && use_subpix(d) && (d->w / 2) % 64 == 0) {
+    // weight gradient of the 4 sub-pixel phases (2x2 taps over the low-res input, 0.44x the
+    // MACs of the upsampled 3x3 formulation); wgrad_reduce folds the phases back into 3x3
+    p.sub = 1;
+    p.cfg = d->cout > 64 ? (d->cout > 128 ? 0 : 2) : 11;
+    const Wg2Cfg& c = kWg2Cfg[p.cfg];
+    p.bkt = c.bkt;
+    p.bc = c.bc;
+    p.px = c.px;
+    const int K2 = 4 * d->cin;
+    const long P2 = (long)d->n * (d->h / 2) * (d->w / 2);
+    p.ntk = fv_cdiv(K2, p.bkt);
+    p.ntc = fv_cdiv(d->cout, p.bc);
+    p.nsteps = (int)(P2 / p.px);
+    const int ntile = p.ntk * p.ntc;
+    int ns = (64 + ntile / 2) / ntile;         // x4 phases ~ one block per CU
+    if (ns < 1) ns = 1;
+    if (ns > p.nsteps) ns = p.nsteps;
+    p.sps = fv_cdiv(p.nsteps, ns);
+    p.nsplit = fv_cdiv(p.nsteps, p.sps);
+    p.KW = p.ntk * p.bkt;
+    p.CW = p.ntc * p.bc;
+    return p;
+  }
   if (p.v2) {
     p.cfg = wg2_cfg(d, K);
     const Wg2Cfg& c = kWg2Cfg[p.cfg];
@@ -1930,6 +2011,15 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
 template <int KS, int CFG>
 int launch_wg2_t(const Wg2Args& a, int ups, int nblk, hipStream_t s) {
   constexpr Wg2Cfg c = kWg2Cfg[CFG];
+  if constexpr (KS == 2) {     // sub-pixel phases only
+    if constexpr (CFG == 0 || CFG == 2 || CFG == 11 || CFG == 12) {
+      hipLaunchKernelGGL((conv_wgrad_v2<2, c.bkt, c.bc, c.wk, c.wc, c.px, c.ns, false, true>), dim3(nblk), dim3(512), 0,
+                         s, a);
+      return FV_OK;
+    } else {
+      return FV_E_UNSUPPORTED;
+    }
+  } else {
   if (ups) {
     if constexpr (KS == 3)
       hipLaunchKernelGGL((conv_wgrad_v2<KS, c.bkt, c.bc, c.wk, c.wc, c.px, c.ns, true>), dim3(nblk), dim3(512), 0, s, a);
@@ -1938,12 +2028,13 @@ int launch_wg2_t(const Wg2Args& a, int ups, int nblk, hipStream_t s) {
     hipLaunchKernelGGL((conv_wgrad_v2<KS, c.bkt, c.bc, c.wk, c.wc, c.px, c.ns, false>), dim3(nblk), dim3(512), 0, s, a);
   }
   return FV_OK;
+  }
 }
 
 template <int KS, int CFG = 0>
 int launch_wg2_ks(const Wg2Args& a, const WgPlan& p, int ups, int nblk, hipStream_t s) {
   if constexpr (CFG < kNumWg2Cfg) {
-    if constexpr (KS != 3 && CFG > 5) return FV_E_UNSUPPORTED;   // experiment configs: 3x3 only
+    if constexpr (KS != 3 && KS != 2 && CFG > 5) return FV_E_UNSUPPORTED;   // experiment configs: 3x3 only
     if (p.cfg == CFG) return launch_wg2_t<KS, CFG>(a, ups, nblk, s);
     return launch_wg2_ks<KS, CFG + 1>(a, p, ups, nblk, s);
   }
@@ -1951,6 +2042,7 @@ int launch_wg2_ks(const Wg2Args& a, const WgPlan& p, int ups, int nblk, hipStrea
 }
 
 int launch_wg2(const Wg2Args& a, int ks, const WgPlan& p, int ups, int nblk, hipStream_t s) {
+  if (p.sub) return launch_wg2_ks<2>(a, p, 0, nblk, s);
   switch (ks) {
     case 1: return launch_wg2_ks<1>(a, p, ups, nblk, s);
     case 3: return launch_wg2_ks<3>(a, p, ups, nblk, s);
@@ -2256,13 +2348,13 @@ int fv_conv2d_wgrad_nsplit(const fv_conv_desc* d) {
 size_t fv_conv2d_wgrad_slab_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const WgPlan p = plan_wgrad(d);
-  return (size_t)p.nsplit * p.CW * p.KW;
+  return (size_t)(p.sub ? 4 : 1) * p.nsplit * p.CW * p.KW;
 }
 
 size_t fv_conv2d_wgrad_bias_slab_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const WgPlan p = plan_wgrad(d);
-  return (size_t)p.nsplit * p.CW;
+  return (size_t)(p.sub ? 4 : 1) * p.nsplit * p.CW;
 }
 
 int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_scale,
@@ -2290,6 +2382,30 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     else
       hipLaunchKernelGGL((conv_halo_wgrad<7, 64, 1, 2>), dim3(t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
     return fv_check_launch("conv2d_bwd_weight_halo");
+  }
+  if (t.sub) {
+    FV_REQUIRE(P * ldy_dy * 2 < (1L << 31), "wgrad: dy larger than 2 GB");
+    Wg2Args a{};
+    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+    a.H = Hin; a.W = Win; a.Hin = Hin; a.Win = Win; a.P = d->n * Hin * Win;
+    a.Ho = d->h; a.Wo = d->w; a.nsplit = t.nsplit;
+    a.lgCin = fv_ilog2(d->cin);
+    a.K = 4 * d->cin;
+    a.KW = t.KW; a.ldd = ldy_dy; a.CW = t.CW;
+    a.ntk = t.ntk; a.ntc = t.ntc; a.nsteps = t.nsteps; a.sps = t.sps;
+    a.fhw = make_fastdiv((uint32_t)(Hin * Win));
+    a.fw = make_fastdiv((uint32_t)Win);
+    a.fh = make_fastdiv((uint32_t)Hin);
+    a.rowal = 1;
+    a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
+    a.dybytes = (unsigned)(P * ldy_dy * 2);
+    const int nblk = 4 * t.ntk * t.ntc * t.nsplit;
+    st = launch_wg2(a, 2, t, 0, nblk, (hipStream_t)stream);
+    if (st) {
+      fv_set_error("sub-pixel wgrad variant unsupported (cfg %d)", t.cfg);
+      return st;
+    }
+    return fv_check_launch("conv2d_bwd_weight_subpix");
   }
   if (t.v2) {
     FV_REQUIRE(P * ldy_dy * 2 < (1L << 31), "wgrad: dy larger than 2 GB");
@@ -2345,6 +2461,13 @@ int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float
   FV_REQUIRE(slab && dw_param, "null pointer");
   FV_REQUIRE(!db || bias_slab, "db needs the bias slab");
   const WgPlan t = plan_wgrad(d);
+  if (t.sub) {
+    const int nb_main = fv_cdiv((long)d->cout * d->cin_valid * 9, 64);
+    const int nb_bias = db ? fv_cdiv(d->cout, 64) : 0;
+    hipLaunchKernelGGL(wgrad_reduce_subpix_kernel, dim3(nb_main + nb_bias), dim3(256), 0, (hipStream_t)stream, slab,
+                       bias_slab, dw_param, db, t.nsplit, t.CW, t.KW, d->cout, d->cin_valid, fv_ilog2(d->cin), nb_main);
+    return fv_check_launch("wgrad_reduce_subpix");
+  }
   const int K = d->ksize * d->ksize * d->cin;
   const long tot = (long)d->cout * K;
   const int nb_main = fv_cdiv(tot, 64);

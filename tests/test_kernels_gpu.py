@@ -62,6 +62,9 @@ CONV_CASES = [
     # sub-pixel phases of upsample + 3x3 (bf16, power-of-two low-res side >= 16): UpBlock2D shapes
     (3, 128, 64, 16, 16, True, False),
     (3, 256, 128, 16, 32, True, False),
+    # ... with low-res width 64: the sub-pixel weight gradient too
+    (3, 128, 64, 8, 64, True, False),
+    (3, 256, 128, 4, 64, True, False),
 ]
 
 
