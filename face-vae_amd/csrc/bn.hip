@@ -48,6 +48,7 @@ __global__ void partials_kernel(const float* __restrict__ part, int nb, int bpix
   const int b0 = split * per, b1 = min(nb, b0 + per);
   double n = 0, S = 0, Q = 0;
   if (c < C) {
+#pragma unroll 8
     for (int b = b0 + r; b < b1; b += 4) {
       const double nb_ = (double)min((long)bpix, P - (long)b * bpix);
       n += nb_;
@@ -176,6 +177,7 @@ __global__ void sum_finalize_kernel(const double* ws, int nsplit, int C, const f
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
   if (c >= C) return;
   double n = 0, S = 0, Q = 0;
+#pragma unroll 4
   for (int sp = lane; sp < nsplit; sp += 64) {
     const double* r = ws + (long)sp * 3 * C + c;
     n += r[0];
@@ -323,6 +325,7 @@ __global__ void bwd_sum_finalize_kernel(const double* ws, int nsplit, int C, dou
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
   double sg = 0, sgy = 0;
+#pragma unroll 8
   for (int sp = lane; sp < nsplit; sp += 64) {
     sg += ws[(long)sp * 2 * C + c];
     sgy += ws[(long)sp * 2 * C + C + c];

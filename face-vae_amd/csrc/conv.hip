@@ -616,11 +616,16 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
       fb[m].lds(As + row * ROWB + (((kk * 4 + lh) ^ swzk<BKS>(row)) << 4));
     }
   };
+  // s_setprio(1) around each MFMA cluster keeps hipcc from moving MFMAs across the raw
+  // barriers into the DMA / fragment-read sections (guide T5); FV_CONV_DBG bit 5 disables it
+  const bool prio = !(a.dbg & 32);
   auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
+    if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int n = 0; n < RN; ++n)
 #pragma unroll
       for (int m = 0; m < RM; ++m) acc[n][m] = mma(fa[n], fb[m], acc[n][m]);
+    if (prio) __builtin_amdgcn_s_setprio(0);
   };
 
   if (BKS == 64 && !(a.dbg & 8)) {
@@ -640,14 +645,14 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     load_frags(fa0, fb0, 0, 0);
     for (int ks = 0; ks < nks; ++ks) {
       const int buf = ks & 1;
-      load_frags(fa1, fb1, buf, 1);
+      if (!(a.dbg & 64)) load_frags(fa1, fb1, buf, 1);    // bit 6: MFMA on stale fragments (experiment)
       mfma_all(fa0, fb0);
       if (ks + 1 < nks) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (ks + 2 < nks && !(a.dbg & 2)) issue(ks + 2, buf);
-        load_frags(fa0, fb0, buf ^ 1, 0);
+        if (!(a.dbg & 64)) load_frags(fa0, fb0, buf ^ 1, 0);
       }
       mfma_all(fa1, fb1);
     }

@@ -428,11 +428,19 @@ __global__ void dot_partial_kernel(const float* __restrict__ a, const float* __r
 __global__ void sn_bwd_apply_kernel(const float* __restrict__ g, int rows, int cols, const float* u,
                                     const float* v, const float* sigma, const float* part, int nparts,
                                     float* out) {
+  // <g, w> from the dot partials: every thread takes some, then a block reduction (a serial
+  // loop in one thread was a chain of nparts dependent L2 round trips per block)
+  __shared__ float red[NTH / 64];
   __shared__ float dot_s;
+  float d = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += NTH) d += part[i];
+  d = wave_sum(d);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    float d = 0.f;
-    for (int i = 0; i < nparts; ++i) d += part[i];
-    dot_s = d;
+    float t = 0.f;
+    for (int i = 0; i < NTH / 64; ++i) t += red[i];
+    dot_s = t;
   }
   __syncthreads();
   const float sg = sigma[0];
