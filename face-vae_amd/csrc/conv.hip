@@ -441,27 +441,23 @@ __device__ __forceinline__ int swz8(int row) { return (row >> 1) & 7; }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-// 16 B per lane, buffer -> LDS (wave-uniform LDS base in M0, lane-linear destination).
+// 16 B per lane, buffer -> LDS (wave-uniform LDS byte address in M0, lane-linear
+// destination), byte offset voffset + soffset (an out-of-range voffset of 0x80000000 stays
+// out of range for any soffset < 2^31, so the hardware returns zeros).
 // Issued as inline asm on purpose: hipcc cannot tell that the ds_reads of the buffer being
 // computed do not alias the stage in flight and would put an s_waitcnt vmcnt(0) in front
 // of them, serialising the ring.  Ordering is therefore explicit: counted vmcnt + barrier.
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, unsigned voff) {
-  unsigned keep;
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)lds);
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(r), "s"(la)
-               : "memory");
-}
-// the same with an LDS byte address and a wave-uniform byte offset in soffset (offset = voffset + soffset; an
-// out-of-range voffset of 0x80000000 stays out of range for any soffset < 2^31)
+// The asm has NO outputs (M0 is declared clobbered): hipcc models an inline asm containing a
+// VMEM op as writing its outputs asynchronously and waits vmcnt(0) before such a register is
+// reused -- with an output, every DMA of a loop waited for the previous one.
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff, unsigned soff) {
-  // no asm outputs: hipcc models an inline asm that contains a VMEM op as writing its outputs
-  // asynchronously and then waits vmcnt before those registers are reused (M0 is clobbered)
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
                :
                : "v"(voff), "s"(r), "s"(lds), "s"(soff)
                : "memory", "m0");
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, const void* lds, unsigned voff) {
+  dma16s(r, __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)lds), voff, 0u);
 }
 
 // f(integral_constant<S>) for the run-time, wave-uniform s in [0, N): a scalar branch to
@@ -833,6 +829,139 @@ conv_halo_fwd(ConvArgs a, unsigned x_bytes) {
     conv_epilogue<bf16, 1, 8, 1, 1>(a, t, smem + HB + WB, 0, p0, tile, 0, wave, lane, tid);
   } else {
     conv_epilogue<bf16, 1, 8, RN, RM>(a, acc, smem + HB + WB, 0, p0, tile, 0, wave, lane, tid);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// 7x7 conv with a 64-channel input and <= 4 output channels (Generator.out_conv 64 -> 3,
+// models.py:1099 + sigmoid 1110), "column taps in N": for every input pixel w' of a row the
+// block computes D[h][w'][(co, s)] = sum_{r, ci} x[h + r - 3][w'][ci] * W[co][ci][r][s]
+// (M = pixels incl. the 3-pixel column halo, N = co x 7 taps = 21 of 32, K = 7 rows x 64 ci
+// = 448), then out[h][w][co] = bias + sum_s D[h][w + s - 3][(co, s)].  3.5x fewer MFMAs than
+// padding N = 3 to 16 with K = 3136, and each A fragment feeds two n-tiles.
+// Block: TR = 4 output rows x 64 columns, 8 waves; halo [10 rows][70 cols][64 ci] in LDS.
+// Wave w: row w >> 1 and five (m-tile, n-tile) pairs of that row's 5 m-tiles x 2 n-tiles.
+// Weights wn [32][448] (n = co * 7 + s, k = r * 64 + ci, 28 KB) are staged in LDS with the halo.
+// ----------------------------------------------------------------------------------------
+constexpr int C7_TR = 4;
+__global__ void __launch_bounds__(512, 1)
+conv7_n3_fwd(ConvArgs a, unsigned x_bytes) {
+  constexpr int TW = 64, HWD = 70, HR = C7_TR + 6, CPP = 8;
+  constexpr int HCH = HR * HWD * CPP, HQ = (HCH + 63) / 64;
+  constexpr int HB = HQ * 1024;
+  constexpr int DL = C7_TR * 80 * 33 * 4;                // D tile in LDS (fp32, rows of 32 + 1 pad)
+  constexpr int WB = 32 * 448 * 2, WQ = WB / 1024;       // weights [32][448] bf16 after the halo
+  __shared__ __attribute__((aligned(1024))) char smem[(HB > DL ? HB : DL) + WB];
+  char* wl = smem + (HB > DL ? HB : DL);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_w = a.W / TW, tiles_h = a.H / C7_TR;
+  const int tile = blockIdx.x;
+  const int n = tile / (tiles_h * tiles_w);
+  const int rem = tile - n * tiles_h * tiles_w;
+  const int h0 = (rem / tiles_w) * C7_TR, w0 = (rem % tiles_w) * TW;
+  const int li = lane & 15, g = lane >> 4;
+
+  // halo: pixel (hr, hc) <- x[h0 + hr - 3][w0 + hc - 3], 16-B chunks XOR-swizzled by pixel
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  for (int q = wave; q < HQ; q += 8) {
+    const int L = q * 64 + lane;
+    const int hp = L >> 3, ch = L & 7;
+    const int hr = hp / HWD, hc = hp - hr * HWD;
+    const int hh = h0 + hr - 3, ww = w0 + hc - 3;
+    const int sc = ch ^ (hp & 7);
+    const bool ok = L < HCH && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+    const unsigned off = ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * 64 + sc * 8) * 2) : 0x80000000u;
+    dma16(xr, smem + q * 1024, off);
+  }
+  // weights: row n (896 B = 56 chunks) with its 16-B chunks XOR-swizzled by (n & 7)
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, WB, 0x00020000);
+  for (int q = wave; q < WQ; q += 8) {
+    const int L = q * 64 + lane;
+    const int wrow = L / 56, slot = L - wrow * 56;
+    dma16(wr, wl + q * 1024, (unsigned)(wrow * 896 + ((slot ^ (wrow & 7)) << 4)));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int row = wave >> 1, half = wave & 1;
+  // this wave's pairs: half 0 -> (m0,n0)(m0,n1)(m1,n0)(m1,n1)(m2,n0); half 1 -> (m2,n1)(m3,n0)(m3,n1)(m4,n0)(m4,n1)
+  const int mb = half ? 2 : 0;                             // first of the wave's 3 m-tiles
+  f32x4 acc[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int apix[3];                                             // halo pixel of this lane, tap row 0
+#pragma unroll
+  for (int t = 0; t < 3; ++t) apix[t] = row * HWD + min((mb + t) * 16 + li, HWD - 1);
+#pragma unroll 2
+  for (int ks = 0; ks < 14; ++ks) {
+    const int r = ks >> 1, c = (ks & 1) * 4 + g;            // tap row, this lane's 16-B chunk
+    bf16x8 bfr[2], afr[3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int nr = t * 16 + li;
+      bfr[t] = *reinterpret_cast<const bf16x8*>(wl + nr * 896 + (((ks * 4 + g) ^ (nr & 7)) << 4));
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int hp = apix[t] + r * HWD;
+      afr[t] = *reinterpret_cast<const bf16x8*>(smem + (hp * CPP + (c ^ (hp & 7))) * 16);
+    }
+    if (half == 0) {
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bfr[0], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bfr[1], acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[0], acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[1], acc[3], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bfr[0], acc[4], 0, 0, 0);
+    } else {
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bfr[1], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[0], acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[1], acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bfr[0], acc[3], 0, 0, 0);
+      acc[4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bfr[1], acc[4], 0, 0, 0);
+    }
+  }
+  __syncthreads();                                         // halo reads done: reuse LDS for D
+  // D[row][col][n] fp32, col = m*16 + 4*(lane>>4) + i (the MFMA row), n = nt*16 + (lane & 15)
+  float* Dl = reinterpret_cast<float*>(smem);
+  const int pm[5] = {half ? 2 : 0, half ? 3 : 0, half ? 3 : 1, half ? 4 : 1, half ? 4 : 2};
+  const int pn[5] = {half ? 1 : 0, half ? 0 : 1, half ? 1 : 0, half ? 0 : 1, half ? 1 : 0};
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Dl[(row * 80 + pm[i] * 16 + g * 4 + j) * 33 + pn[i] * 16 + li] = acc[i][j];
+  __syncthreads();
+  // out[h0+row][w0+w][co] = bias + sum_s D[row][w + s][co*7 + s]; NCHW fp32 (+ sigmoid)
+  const int HWo = a.H * a.W;
+  // a wave covers one (co, row) segment of 64 pixels = one BN-statistics record
+  for (int o = tid; o < C7_TR * TW * a.Cout; o += 512) {
+    const int co = o / (C7_TR * TW), rr = (o / TW) % C7_TR, w = o % TW;
+    float v = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+    for (int s7 = 0; s7 < 7; ++s7) v += Dl[(rr * 80 + w + s7) * 33 + co * 7 + s7];
+    if (a.stats) {
+      const float sv = wave_sum(v), qv = wave_sum(v * v);
+      const int rec = ((n * a.H + h0 + rr) * a.W + w0) >> 6;
+      if (lane == 0) {
+        a.stats[(long)(rec * 2) * a.Cout + co] = sv;
+        a.stats[(long)(rec * 2 + 1) * a.Cout + co] = qv;
+      }
+    }
+    if (a.sigmoid) v = 1.f / (1.f + expf(-v));
+    const int pix = (h0 + rr) * a.W + w0 + w;
+    if (a.nchw) reinterpret_cast<float*>(a.y)[((long)(n * a.Cout + co)) * HWo + pix] = v;
+    else reinterpret_cast<bf16*>(a.y)[((long)n * HWo + pix) * a.ldy + co] = (bf16)v;
+  }
+}
+
+// wn [32][448]: n = co * 7 + s (co < cout, s < 7), k = r * 64 + ci
+__global__ void weight_prep_c7n_kernel(const float* __restrict__ wp, const float* sigma, bf16* wn, int cout) {
+  const float inv = sigma ? 1.f / sigma[0] : 1.f;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < 32 * 448; e += gridDim.x * blockDim.x) {
+    const int nn = e / 448, k = e - nn * 448;
+    const int co = nn / 7, s = nn - co * 7, r = k >> 6, ci = k & 63;
+    const float v = co < cout ? wp[((co * 64 + ci) * 7 + r) * 7 + s] * inv : 0.f;
+    wn[e] = (bf16)v;
   }
 }
 
@@ -1370,6 +1499,194 @@ conv_wgrad_v2(Wg2Args a) {
 }
 
 // ----------------------------------------------------------------------------------------
+// Weight gradient of the 7x7 64 -> <= 4 channel conv (Generator.out_conv), "row taps in N":
+//   D[(s, ci)][(r, co)] = sum_{x row h, column w} x[h][w + s - 3][ci] * dy[h - r + 3][w][co]
+//                      = dW[co][ci][r][s]
+// M = 7 column taps x 64 ci = 448 (28 m-tiles), N = 7 row taps x 4 co = 28 of 32 (2 n-tiles),
+// K = x pixels: 3.5x fewer MFMAs than M = 3136, N = 3 -> 16.  A block walks the x rows of a
+// 64-column strip segment: per row the x row (70 columns incl. the column halo) lands in LDS
+// by DMA (double buffered) and the dy row 3 below it is transposed into a ring of 8
+// channel-major dy rows, from which a B fragment (8 consecutive columns of one (r, co)) is a
+// single ds_read_b128; A fragments are transposed reads (pixels are the MFMA K) of the x row.
+// Output: per-block fp32 slabs [block][32][448] (n = r*4 + co, m = s*64 + ci) + bias sums.
+// ----------------------------------------------------------------------------------------
+struct W7Args {
+  const void* x;
+  const void* dy;
+  float* slab;
+  float* bslab;
+  int H, W, ldd, cout, seg_rows, nseg;
+  unsigned xbytes, dybytes;
+};
+
+__global__ void __launch_bounds__(512, 2)
+conv7_n3_wgrad(W7Args a) {
+  constexpr int XROW = 9 * 1024;                            // 70 px x 128 B, padded to whole pieces
+  constexpr int XQ = 70 * 128 / 1024 + 1;                    // 9 pieces (the last one partly past 70 px)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * XROW + 2 * 1024 + 8 * 512];
+  char* xb = smem;                                           // [2][70 px][64 ci] (timg_off<64> layout)
+  char* dys = smem + 2 * XROW;                               // [2][64 px][8 ch] as stored in dy
+  bf16* dyT = reinterpret_cast<bf16*>(smem + 2 * XROW + 2 * 1024);   // [8 rows][4 co][64 w]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int strips = a.W / 64;
+  const int blk = blockIdx.x;
+  const int seg = blk % a.nseg, strip = (blk / a.nseg) % strips, n = blk / (a.nseg * strips);
+  const int w0 = strip * 64;
+  const int hb = seg * a.seg_rows, he = min(a.H, hb + a.seg_rows);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), 0, (int)a.dybytes, 0x00020000);
+
+  // x row h -> xb[buf] (pixel p = column w0 - 3 + p; 32-B blocks XOR-swizzled, timg_off<64>)
+  auto issue_x = [&](int h, int buf) {
+    for (int q = wave; q < XQ; q += 8) {
+      const int o = q * 1024 + lane * 16;
+      const int p = o >> 7, b = o & 127;
+      const int ci = ((((b >> 5) ^ tswz<64>(p)) << 4) | (((b >> 4) & 1) << 3));
+      const int ww = w0 - 3 + p;
+      const bool ok = p < 70 && h >= 0 && h < a.H && ww >= 0 && ww < a.W;
+      dma16(xr, xb + buf * XROW + q * 1024,
+            ok ? (unsigned)((((n * a.H + h) * a.W + ww) * 64 + ci) * 2) : 0x80000000u);
+    }
+  };
+  // dy row y (64 px x ldd = 8 channels = 1 KB) -> dys[buf], one piece by wave 0
+  auto issue_dy = [&](int y, int buf) {
+    if (wave == 0) {
+      const bool ok = y >= 0 && y < a.H;
+      dma16(dr, dys + buf * 1024, ok ? (unsigned)((((n * a.H + y) * a.W + w0) * 8) * 2 + lane * 16) : 0x80000000u);
+    }
+  };
+  // dys[buf] -> dyT[y & 7] (channel-major; zero rows outside the image / channels >= cout)
+  auto transpose_dy = [&](int y, int buf) {
+    if (tid < 256) {
+      const int w = tid & 63, co = tid >> 6;
+      const bf16 v = (y >= 0 && y < a.H && co < a.cout) ? reinterpret_cast<const bf16*>(dys + buf * 1024)[w * 8 + co]
+                                                          : (bf16)0.f;
+      dyT[((y & 7) * 4 + co) * 64 + w] = v;
+    }
+  };
+
+  // prologue: dy rows hb-3 .. hb+2 straight into the ring (plain loads), first x / dy DMAs
+  for (int e = tid; e < 6 * 256; e += 512) {
+    const int y = hb - 3 + e / 256, w = e & 63, co = (e >> 6) & 3;
+    bf16 v = (bf16)0.f;
+    if (y >= 0 && y < a.H && co < a.cout)
+      v = reinterpret_cast<const bf16*>(a.dy)[((long)(n * a.H + y) * a.W + w0 + w) * 8 + co];
+    dyT[((y & 7) * 4 + co) * 64 + w] = v;
+  }
+  issue_x(hb, 0);
+  issue_dy(hb + 3, 0);
+
+  // this wave's m-tiles: w, w + 8, w + 16, w + 24 (< 28), each with both n-tiles
+  const int nmt = wave < 4 ? 4 : 3;
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;                                          // bias gradient: this thread's (w, co)
+
+  for (int h = hb; h < he; ++h) {
+    const int buf = (h - hb) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                                         // x row h, dy row h+3 landed; step h-1 done
+    transpose_dy(h + 3, buf);
+    if (h + 1 < he) {
+      issue_x(h + 1, buf ^ 1);
+      issue_dy(h + 4, buf ^ 1);
+    }
+    __syncthreads();                                         // dy row h+3 visible in the ring
+    if (tid < 256) {
+      const int w = tid & 63, co = tid >> 6;
+      bsum += (float)dyT[((h & 7) * 4 + co) * 64 + w];
+    }
+    const char* xbuf = xb + buf * XROW;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bfr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int nn = t * 16 + li, r = nn >> 2, co = nn & 3;
+        const int y = h - r + 3;
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(dyT + ((y & 7) * 4 + co) * 64 + kk * 32 + g * 8);
+        if (r > 6) v = bf16x8{};
+        bfr[t] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < nmt) {
+          const int mt = wave + 8 * i, s7 = mt >> 2, cb = (mt & 3) * 16;
+          const bf16x8 afr = tfrag<64>(xbuf, kk * 32 + s7, cb, lane);
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[0], acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr[1], acc[i][1], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // slab[blk][n][m]: lane holds D[m = mt*16 + 4g + j][n = t*16 + li]
+  float* sl = a.slab + (long)blk * 32 * 448;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i < nmt) {
+      const int mt = wave + 8 * i;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sl[(t * 16 + li) * 448 + mt * 16 + 4 * g + j] = acc[i][t][j];
+    }
+  }
+  // bias: sum over the 64 columns of each co (waves 0..3 hold co = wave)
+  if (a.bslab && tid < 256) {
+    const float t = wave_sum(bsum);
+    if (lane == 0) a.bslab[blk * 4 + wave] = t;
+  }
+}
+
+// slabs [nblk][32][448] + [nblk][4] -> dW[co][64][7][7], db[co] in two deterministic passes.
+// Pass 1: block (column chunk, group g) sums the slab rows [g*rpg, (g+1)*rpg) of 64 columns
+// (4 waves x rows strided by 4, 4 loads in flight per lane) and stores the partial in place
+// over row g*rpg.  Pass 2 sums the G partials in order.  Column e < 12544 is slab element
+// (n = e / 448, m = e % 448); e in [12544, 12548) is bias co = e - 12544.
+constexpr int W7_COLS = 28 * 448;
+__device__ __forceinline__ float* w7_elem(float* slab, float* bslab, int b, int e) {
+  return e < W7_COLS ? slab + (long)b * 32 * 448 + e : bslab + b * 4 + (e - W7_COLS);
+}
+
+__global__ void __launch_bounds__(256)
+w7_reduce1_kernel(float* slab, float* bslab, int nblk, int rpg, int ncol) {
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), sg = threadIdx.x >> 6;
+  const int b0 = blockIdx.y * rpg, b1 = min(nblk, b0 + rpg);
+  __shared__ float red[4][64];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (e < ncol) {
+    int b = b0 + sg;
+    for (; b + 12 < b1; b += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += *w7_elem(slab, bslab, b + 4 * u, e);
+    }
+    for (; b < b1; b += 4) acc[0] += *w7_elem(slab, bslab, b, e);
+  }
+  red[sg][threadIdx.x & 63] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (sg == 0 && e < ncol && b0 < b1)
+    *w7_elem(slab, bslab, b0, e) = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+__global__ void w7_reduce2_kernel(float* slab, float* bslab, int nblk, int rpg, int cout, float* dw, float* db) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= W7_COLS + (db ? cout : 0)) return;
+  const int nn = e / 448, co = nn & 3;
+  if (e < W7_COLS && co >= cout) return;
+  float v = 0.f;
+  for (int b = 0; b < nblk; b += rpg) v += *w7_elem(slab, bslab, b, e);
+  if (e < W7_COLS) {
+    const int r = nn >> 2, m = e - nn * 448, s7 = m >> 6, ci = m & 63;
+    dw[((co * 64 + ci) * 7 + r) * 7 + s7] = v;
+  } else {
+    db[e - W7_COLS] = v;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // Halo-tiled 7x7 weight gradient (bf16): Generator.out_conv 64->3 and AFE.in_conv 3->64.
 //   dW[co][k = (tap, ci)] = sum_p dy[p][co] * x[p + off(tap)][ci]      (M = k, N = co, K = p)
 // Persistent blocks (one per CU) walk TR x 64 pixel tiles; per tile the input halo and the
@@ -1867,6 +2184,30 @@ bool use_dgrad_lowres(const fv_conv_desc* d) {
   return (long)d->n * d->h * d->w * ct * 2 < (1L << 31);
 }
 
+// Generator.out_conv shape: 7x7, 64 -> <= 4 channels, NCHW fp32 output (bf16 operands)
+static int g_disable_c7n = -1;
+bool use_c7n(const fv_conv_desc* d) {
+  if (g_disable_c7n < 0) {
+    const char* e = getenv("FV_DISABLE_C7N");
+    g_disable_c7n = (e && e[0] == '1') ? 1 : 0;
+  }
+  return !g_disable_c7n && d->dtype == FV_BF16 && d->ksize == 7 && d->cin == 64 && d->cin_valid == 64 &&
+         d->cout <= 4 && !d->pro_act && !d->upsample && d->w % 64 == 0 && d->h % C7_TR == 0 &&
+         (long)d->n * d->h * d->w * 64 * 2 < (1L << 31);
+}
+
+// out_conv weight gradient as "row taps in N" (conv7_n3_wgrad)
+int g_disable_c7w = -1;
+bool use_c7w(const fv_conv_desc* d) {
+  if (g_disable_c7w < 0) {
+    const char* e = getenv("FV_DISABLE_C7W");
+    g_disable_c7w = (e && e[0] == '1') ? 1 : 0;
+  }
+  return !g_disable_c7w && d->dtype == FV_BF16 && d->ksize == 7 && d->cin == 64 && d->cin_valid == 64 &&
+         d->cout <= 4 && !d->pro_act && !d->upsample && d->w % 64 == 0 &&
+         (long)d->n * d->h * d->w * 64 * 2 < (1L << 31);
+}
+
 int check_desc(const fv_conv_desc* d) {
   FV_REQUIRE(d, "null conv descriptor");
   FV_REQUIRE(d->dtype == FV_F32 || d->dtype == FV_BF16, "conv dtype must be f32 or bf16");
@@ -1947,6 +2288,22 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
   p.v2 = !g_disable_wg2 && d->dtype == FV_BF16 && !d->pro_act && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
          P * 256 * 2 < (1L << 31);
+  // out_conv 7x7 64 -> <= 4 (v2 == 3): blocks = (image, 64-column strip, row segment), about
+  // 4 per CU; slab [block][32 (r, co)][448 (s, ci)]
+  if (p.v2 && use_c7w(d)) {
+    const int strips = d->w / 64;
+    int nseg = fv_cdiv(1024, d->n * strips);
+    if (nseg > fv_cdiv(d->h, 8)) nseg = fv_cdiv(d->h, 8);
+    if (nseg < 1) nseg = 1;
+    p.v2 = 3;
+    p.sps = fv_cdiv(d->h, nseg);                 // rows per segment
+    p.nsteps = fv_cdiv(d->h, p.sps);             // segments
+    p.nsplit = d->n * strips * p.nsteps;
+    p.CW = 32;
+    p.KW = 448;
+    p.ntk = p.ntc = 1;
+    return p;
+  }
   // 7x7 halo path (v2 == 2): one persistent block per CU, ntk = 1 (all k in one tile)
   const int htr = halo_wg_tr(d);
   if (p.v2 && htr) {
@@ -2099,6 +2456,7 @@ size_t fv_conv_wk_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const FwdTile t = fwd_tile(d->cout);
   const size_t rows = (size_t)fv_cdiv(d->cout, t.bn) * t.bn;
+  if (use_c7n(d)) return 32 * 448;
   if (use_subpix(d)) return 4 * rows * kpad_of(2, d->cin);
   return rows * kpad_of(d->ksize, d->cin);
 }
@@ -2141,6 +2499,7 @@ static FwdTile plan_tile(const fv_conv_desc* d) {
 
 // pixels per BN-statistics record = the pixels of one wave row of the tile (BM / WM)
 static int stats_record_pixels(const fv_conv_desc* d) {
+  if (use_c7n(d)) return 64;                                  // one 64-pixel row segment
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
   const FwdTile t = plan_tile(d);
   if (use_v2(d)) {
@@ -2166,7 +2525,10 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   if (st) return st;
   hipStream_t s = (hipStream_t)stream;
   const int ks = d->ksize;
-  if (wk && use_subpix(d)) {
+  if (wk && use_c7n(d)) {
+    hipLaunchKernelGGL(weight_prep_c7n_kernel, dim3(56), dim3(256), 0, s, w_param, sigma, (bf16*)wk, d->cout);
+    if ((st = fv_check_launch("weight_prep_c7n"))) return st;
+  } else if (wk && use_subpix(d)) {
     const FwdTile t = fwd_tile(d->cout);
     const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_of(2, d->cin);
     const long tot = 4L * rows * Kp;
@@ -2236,6 +2598,13 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   }
   a.dbg = g_conv_dbg;
   int st;
+  if (use_c7n(d)) {
+    FV_REQUIRE(!res, "out_conv kernel: no residual");
+    const int nblk = d->n * (d->h / C7_TR) * (d->w / 64);
+    const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
+    hipLaunchKernelGGL(conv7_n3_fwd, dim3(nblk), dim3(512), 0, s, a, xb);
+    return fv_check_launch("conv2d_fwd_c7n");
+  }
   if (const int tr = halo_tr(d)) {
     a.lgtw = 6;
     const int nblk = d->n * (d->h / tr) * (d->w / 64);
@@ -2373,6 +2742,17 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
   const WgPlan t = plan_wgrad(d);
   const int Hin = d->upsample ? d->h / 2 : d->h, Win = d->upsample ? d->w / 2 : d->w;
   const long P = (long)d->n * d->h * d->w;
+  if (t.v2 == 3) {
+    FV_REQUIRE(ldy_dy == 8, "wgrad (out_conv 7x7): dy channel stride must be 8 (got %d)", ldy_dy);
+    W7Args a{};
+    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+    a.H = d->h; a.W = d->w; a.ldd = ldy_dy; a.cout = d->cout;
+    a.seg_rows = t.sps; a.nseg = t.nsteps;
+    a.xbytes = (unsigned)(P * 64 * 2);
+    a.dybytes = (unsigned)(P * 8 * 2);
+    hipLaunchKernelGGL(conv7_n3_wgrad, dim3(t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    return fv_check_launch("conv2d_bwd_weight_c7");
+  }
   if (t.v2 == 2) {
     const int ldd_need = d->cin == 8 ? 64 : 8;
     FV_REQUIRE(ldy_dy == ldd_need, "wgrad (7x7 halo): dy channel stride must be %d (got %d)", ldd_need, ldy_dy);
@@ -2466,6 +2846,17 @@ int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float
   FV_REQUIRE(slab && dw_param, "null pointer");
   FV_REQUIRE(!db || bias_slab, "db needs the bias slab");
   const WgPlan t = plan_wgrad(d);
+  if (t.v2 == 3) {
+    // the two passes reuse the slab rows in place (the slabs are dead after the reduce)
+    const int ncol = W7_COLS + (db ? 4 : 0);
+    const int G = t.nsplit >= 256 ? 16 : (t.nsplit >= 16 ? 4 : 1);
+    const int rpg = fv_cdiv(t.nsplit, G);
+    hipLaunchKernelGGL(w7_reduce1_kernel, dim3(fv_cdiv(ncol, 64), G), dim3(256), 0, (hipStream_t)stream,
+                       const_cast<float*>(slab), const_cast<float*>(bias_slab), t.nsplit, rpg, ncol);
+    hipLaunchKernelGGL(w7_reduce2_kernel, dim3(fv_cdiv(ncol, 256)), dim3(256), 0, (hipStream_t)stream,
+                       const_cast<float*>(slab), const_cast<float*>(bias_slab), t.nsplit, rpg, d->cout, dw_param, db);
+    return fv_check_launch("wgrad_reduce_c7");
+  }
   if (t.sub) {
     const int nb_main = fv_cdiv((long)d->cout * d->cin_valid * 9, 64);
     const int nb_bias = db ? fv_cdiv(d->cout, 64) : 0;

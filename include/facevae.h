@@ -109,7 +109,8 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
                          const float* pro_shift, const void* dy, int ldy_dy, float* slab,
                          float* bias_slab, void* stream);
 /* reduce the slabs into dw_param [cout][cin_valid][k][k] (fp32, reference layout) and
- * db [cout] (db may be NULL). */
+ * db [cout] (db may be NULL).  The slab contents are scratch afterwards: the reduce may use
+ * them for its partial sums. */
 int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab,
                            float* dw_param, float* db, void* stream);
 

@@ -59,6 +59,7 @@ CONV_CASES = [
     # 7x7 halo path (bf16, W % 64 == 0): in_conv shape, out_conv shape (+ its dgrad)
     (7, 3, 64, 16, 64, False, False),
     (7, 64, 3, 8, 128, False, False),
+    (7, 64, 3, 20, 64, False, False),   # out_conv wgrad: 3 ragged row segments
     # sub-pixel phases of upsample + 3x3 (bf16, power-of-two low-res side >= 16): UpBlock2D shapes
     (3, 128, 64, 16, 16, True, False),
     (3, 256, 128, 16, 32, True, False),
