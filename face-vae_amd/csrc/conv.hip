@@ -172,7 +172,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     }
   }
 
-  if (a.stats) {
+  if (a.stats && !(a.dbg & 128)) {   // (bit 7: experiment, no statistics)
     // BN statistics partials, one record per wave row (RM*16 pixels, record index
     // tm*WM + wm): per output channel (sum, sum of squares) over the record's valid pixels,
     // reduced over the 16 pixel lanes of each m-tile by shuffles -- no LDS, no barrier.
@@ -189,28 +189,23 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
           t += v;
           q += v * v;
         }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          t += __shfl_xor(t, o, 64);
-          q += __shfl_xor(q, o, 64);
-        }
-        sv[i] = t;
-        qv[i] = q;
+        sv[i] = row16_sum(t);
+        qv[i] = row16_sum(q);
       }
+      // every lane of a 16-lane row holds the row's 4 channel sums: lanes 0-3 store the sums,
+      // lanes 4-7 the squares (one store instruction per n, 4 x 2 x 16 B)
       const int cb = co0 + wn * RN * 16 + n * 16 + lh * 4;
-      if (lr == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (cb + i < a.Cout) {
-            a.stats[(long)(rec * 2) * a.Cout + cb + i] = sv[i];
-            a.stats[(long)(rec * 2 + 1) * a.Cout + cb + i] = qv[i];
-          }
-      }
+      const int ii = lr & 3;
+      const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
+      const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
+      const float val = lr < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
+      if (lr < 8 && cb + ii < a.Cout) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
     }
   }
 
   if constexpr (STAGED) {
     static_assert(sizeof(T) == 2, "staged epilogue is bf16 NHWC");
+    if (a.dbg & 512) return;                            // (bit 9: experiment, stop after the stats)
     constexpr int CPR = BN / 8;                         // 16-B chunks per pixel row
     __syncthreads();                                    // stats scratch / last k-step reads done
 #pragma unroll
@@ -229,7 +224,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
       const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
       const int tp = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
       const int co = co0 + ch * 8;
-      if (tp >= a.P || co >= a.Cout) continue;
+      if (tp >= a.P || co >= a.Cout || (a.dbg & 256)) continue;   // (bit 8: experiment, no stores)
       const int pix = out_pix(a, tp);
       Chunk8<bf16> v;
       v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
@@ -678,6 +673,145 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
   }
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, MODE == 2 ? tm * 4 + phase : tm, wn, wm, lane,
                                              tid);
+}
+
+// ----------------------------------------------------------------------------------------
+// 3x3 stride-1 conv with a halo-staged input (bf16 NHWC, cin % 64 == 0, W % 64 == 0):
+// the res / down convs and their data gradients.  The per-tap DMA of conv_fwd_v2 moves 9
+// copies of every input pixel into LDS; at 1 KB per ~30 CU-cycles that fill, not the MFMA,
+// bounds the short-K layers (AFE.down1 forward: DMA alone 300 us of 530).  Here a block owns
+// TR = 4 image rows x 64 columns; per 32-channel chunk the (TR+2) x 66 halo lands in LDS once
+// and the 9 taps read their shifted windows from it, so a 32-deep k step moves the weight
+// slice (BN x 64 B) plus 1/9 of a halo: 1.7x (BN 256) to 2.6x (BN 64) fewer bytes per MAC.
+//   k step ks = (chunk c = ks / 9, tap t = ks % 9); weights [co][tap][ci] as in v2.
+//   halo pixel hp = hr * 66 + hc at hp * 64 B, 16-B chunk XOR ((hp >> 2) & 1) * 2: a fragment
+//   read (16 consecutive halo pixels from ANY start) is bank-conflict free (ds_read_b128
+//   lane groups of the guide's table).
+// ----------------------------------------------------------------------------------------
+__device__ __forceinline__ int h3swz(int hp) { return ((hp >> 2) & 1) << 1; }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <int WN, int WM, int RN, int RM>
+__global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
+conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
+  constexpr int NW = WN * WM;
+  constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
+  constexpr int HP = (TR + 2) * 66, HQ = (HP + 15) / 16, JH = (HQ + NW - 1) / NW;
+  constexpr int HALO = HQ * 1024;
+  constexpr int QB = BN / 16, JB = QB / NW;
+  static_assert(QB % NW == 0, "weight pieces per wave");
+  constexpr int BST = BN * 64;
+  constexpr int MAIN = 2 * HALO + 2 * BST, EPI = BM * BN * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tn = lid % a.ntn, tm = lid / a.ntn;
+  const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
+  const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
+  const int co0 = tn * BN;
+  const int p0 = (n * a.H + th * TR) * a.W + tw * 64;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+  const int lrow = lane >> 2, lchk = lane & 3;
+
+  // halo pieces of this wave: source offsets (0x80000000: outside the image -> zero fill)
+  unsigned hoff[JH];
+#pragma unroll
+  for (int j = 0; j < JH; ++j) {
+    const int hp = (wave + j * NW) * 16 + lrow;
+    const int hr = hp / 66, hc = hp - (hp / 66) * 66;
+    const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
+    const bool ok = hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+    hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + ((lchk ^ h3swz(hp)) << 3)) * 2) : 0x80000000u;
+  }
+  const int nh = (HQ - wave + NW - 1) / NW;        // halo pieces this wave issues (JH or JH - 1)
+  unsigned wbase[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    const int row = (wave + j * NW) * 16 + lrow;
+    wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ rswz<bf16>(row)) << 3)) * 2);
+  }
+  auto issue_b = [&](int ks) {
+    const int c = ks / 9, t = ks - c * 9;
+    const unsigned Bs = sbase + 2 * HALO + (ks & 1) * BST;
+    const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
+#pragma unroll
+    for (int j = 0; j < JB; ++j) dma16s(wr, Bs + (wave + j * NW) * 1024, wbase[j], k0 * 2);
+  };
+  auto issue_halo = [&](int c) {
+    const unsigned Hs = sbase + (c & 1) * HALO;
+#pragma unroll
+    for (int j = 0; j < JH; ++j)
+      if (j < JH - 1 || wave + j * NW < HQ) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], (unsigned)(c * 64));
+  };
+
+  const int lr = lane & 15, lh = lane >> 4;
+  int hpb[RM];
+#pragma unroll
+  for (int m = 0; m < RM; ++m) {
+    const int loc = wm * RM * 16 + m * 16 + lr;
+    hpb[m] = (loc >> 6) * 66 + (loc & 63);
+  }
+  f32x4 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.Cin >> 5, nks = 9 * nch;
+  const bool prio = !(a.dbg & 32);
+  issue_b(0);
+  issue_halo(0);
+  for (int ks = 0; ks < nks; ++ks) {
+    const int c = ks / 9, t = ks - c * 9;
+    // step 9c+1 may leave the halo of chunk c+1 (issued last, at step 9c) in flight
+    if (t == 1 && c + 1 < nch) {
+      if (nh == JH) wait_vm<JH>();
+      else wait_vm<(JH > 0 ? JH - 1 : 0)>();
+    } else {
+      wait_vm<0>();
+    }
+    __syncthreads();
+    if (!(a.dbg & 2)) {                               // bit 1: DMA only the first stage (experiment)
+      if (ks + 1 < nks) issue_b(ks + 1);
+      if (t == 0 && c + 1 < nch) issue_halo(c + 1);
+    }
+    if (a.dbg & 1) continue;                          // bit 0: no fragment reads / MFMA (experiment)
+    const int r = t / 3, s3 = t - (t / 3) * 3;
+    const char* Hs = smem + (c & 1) * HALO;
+    const char* Bs = smem + 2 * HALO + (ks & 1) * BST;
+    Frag<bf16> fa[RN], fb[RM];
+#pragma unroll
+    for (int i = 0; i < RN; ++i) {
+      const int row = wn * RN * 16 + i * 16 + lr;
+      fa[i].lds(Bs + row * 64 + ((lh ^ rswz<bf16>(row)) << 4));
+    }
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int hp = hpb[m] + r * 66 + s3;
+      fb[m].lds(Hs + hp * 64 + ((lh ^ h3swz(hp)) << 4));
+    }
+    if (prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
+    if (prio) __builtin_amdgcn_s_setprio(0);
+  }
+  if (a.dbg & 4) {   // experiment: skip the epilogue (keep one store so the MFMAs stay live)
+    if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.y)[tid] = acc[RN - 1][RM - 1][3];
+    return;
+  }
+  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -2075,6 +2209,22 @@ bool use_v2(const fv_conv_desc* d) {
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
 
+// 3x3 halo path (conv3_halo_fwd): co per block (256 / 128 / 64), 0 when not eligible
+static int g_disable_h3 = -1;
+int halo3_bn(const fv_conv_desc* d) {
+  if (g_disable_h3 < 0) {
+    const char* e = getenv("FV_DISABLE_H3");
+    g_disable_h3 = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_disable_h3 || !use_v2(d) || d->ksize != 3 || d->upsample || d->w % 64 || d->h % 4) return 0;
+  if ((long)d->n * d->h * d->w * d->ldy * 2 >= (1L << 31)) return 0;
+  // co % 256 layers keep conv_fwd_v2's 256 x 256 pipelined tile (faster there; FV_H3_256=1
+  // routes them here for A/B)
+  static const bool h3_256 = getenv("FV_H3_256") != nullptr;
+  if (d->cout % 256 == 0) return h3_256 ? 256 : 0;
+  return d->cout % 128 == 0 ? 128 : d->cout % 64 == 0 ? 64 : 0;
+}
+
 // v2 tile configs: id -> (co per block, pixels per block); waves/layout in launch_v2_ks
 struct V2Cfg { int bn, bm; };
 constexpr V2Cfg kV2Cfg[] = {
@@ -2502,6 +2652,7 @@ static int stats_record_pixels(const fv_conv_desc* d) {
   if (use_c7n(d)) return 64;                                  // one 64-pixel row segment
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
   const FwdTile t = plan_tile(d);
+  if (const int bn = halo3_bn(d)) return bn == 256 ? 128 : 64;   // RM * 16 pixels per wave row
   if (use_v2(d)) {
     if (t.bn == 64 || t.bn == 16 || (t.bn == 128 && t.bm == 256)) return t.bm / 4;
     return t.bm / 2;                                          // 128x128, 256x256, 256x128
@@ -2634,6 +2785,20 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
       return st;
     }
     return fv_check_launch("conv2d_fwd_subpix");
+  }
+  if (const int bn = halo3_bn(d)) {
+    FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");
+    a.lgtw = 6;
+    a.ntn = d->cout / bn;
+    const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
+    const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
+    if (bn == 256)
+      hipLaunchKernelGGL((conv3_halo_fwd<4, 2, 4, 8>), dim3(nblk), dim3(512), 0, s, a, xb);
+    else if (bn == 128)
+      hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+    else
+      hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
+    return fv_check_launch("conv2d_fwd_halo3");
   }
   if (use_v2(d)) {
     FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");

@@ -60,6 +60,10 @@ CONV_CASES = [
     (7, 3, 64, 16, 64, False, False),
     (7, 64, 3, 8, 128, False, False),
     (7, 64, 3, 20, 64, False, False),   # out_conv wgrad: 3 ragged row segments
+    # halo-staged 3x3 (bf16, W % 64 == 0, H % 4 == 0): co tiles of 128 / 256 / 64, 2 column tiles
+    (3, 64, 128, 8, 64, False, False),
+    (3, 256, 256, 4, 64, False, False),
+    (3, 128, 64, 12, 128, False, False),
     # sub-pixel phases of upsample + 3x3 (bf16, power-of-two low-res side >= 16): UpBlock2D shapes
     (3, 128, 64, 16, 16, True, False),
     (3, 256, 128, 16, 32, True, False),
