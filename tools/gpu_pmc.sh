@@ -1,14 +1,13 @@
 #!/bin/bash
-# PMC counter passes (separate rocprofv3 runs, kernel-trace only) over a convbench slice.
+# HBM traffic of the bench's kernels: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; they
+# do not fit one pass), each its own short bench run; then tools/pmc_traffic.py.
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 export TMPDIR=/tmp
-ARGS=${PMC_ARGS:---layers res --only fwd,dgrad,wgrad --iters 3}
-rocprofv3 -L > gpurun_out/counters_list.txt 2>&1 || true
+R=$GRAFT_REPO_ROOT
 cd /tmp
-i=0
-for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE"; do
-  i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc$i -o run -- python3 $GRAFT_REPO_ROOT/tools/convbench.py $ARGS > $GRAFT_REPO_ROOT/gpurun_out/pmc$i.log 2>&1 || exit 1
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/pmc_$c -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --cpu-seconds 0 > $R/gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 $R/gpurun_out/pmc_$c.log; exit 1; }
 done
+cd $R && python tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE > gpurun_out/pmc_traffic.json && cat gpurun_out/pmc_traffic.json
