@@ -814,6 +814,145 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
 }
 
+// Software-pipelined variant: a step is a PAIR of taps (64 k), the weight stage holds both
+// taps' 32-channel slices, and the loop is conv_fwd_v2's: the fragments of the step's second
+// tap are read while the first tap's MFMAs run and the barrier sits between the two MFMA
+// groups.  Chunk c's halo goes into buffer c & 1 right after the barrier that retires the
+// last read of chunk c - 2 (5 steps before its first use).
+template <int WN, int WM, int RN, int RM>
+__global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
+conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
+  constexpr int NW = WN * WM;
+  constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
+  constexpr int HP = (TR + 2) * 66, HQ = (HP + 15) / 16, JH = (HQ + NW - 1) / NW;
+  constexpr int HALO = HQ * 1024;
+  constexpr int QB = BN / 16, JB = QB / NW;
+  static_assert(QB % NW == 0, "weight pieces per wave");
+  constexpr int BST = BN * 64, STG = 2 * BST;
+  constexpr int MAIN = 2 * HALO + 2 * STG, EPI = BM * BN * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tn = lid % a.ntn, tm = lid / a.ntn;
+  const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
+  const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
+  const int co0 = tn * BN;
+  const int p0 = (n * a.H + th * TR) * a.W + tw * 64;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+  const int lrow = lane >> 2, lchk = lane & 3;
+
+  unsigned hoff[JH];
+#pragma unroll
+  for (int j = 0; j < JH; ++j) {
+    const int hp = (wave + j * NW) * 16 + lrow;
+    const int hr = hp / 66, hc = hp - (hp / 66) * 66;
+    const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
+    const bool ok = hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+    hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + ((lchk ^ h3swz(hp)) << 3)) * 2) : 0x80000000u;
+  }
+  unsigned wbase[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    const int row = (wave + j * NW) * 16 + lrow;
+    wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ rswz<bf16>(row)) << 3)) * 2);
+  }
+  const int nch = a.Cin >> 5, ntap = 9 * nch, nsteps = (ntap + 1) >> 1;
+  auto issue_b = [&](int j) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = 2 * j + h;
+      if (u < ntap) {
+        const int c = u / 9, t = u - c * 9;
+        const unsigned Bs = sbase + 2 * HALO + (j & 1) * STG + h * BST;
+        const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
+#pragma unroll
+        for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase[jb], k0 * 2);
+      }
+    }
+  };
+  auto issue_halo = [&](int c) {
+    const unsigned Hs = sbase + (c & 1) * HALO;
+#pragma unroll
+    for (int j = 0; j < JH; ++j)
+      if (j < JH - 1 || wave + j * NW < HQ) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], (unsigned)(c * 64));
+  };
+
+  const int lr = lane & 15, lh = lane >> 4;
+  int hpb[RM];
+#pragma unroll
+  for (int m = 0; m < RM; ++m) {
+    const int loc = wm * RM * 16 + m * 16 + lr;
+    hpb[m] = (loc >> 6) * 66 + (loc & 63);
+  }
+  auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], int u) {
+    const int c = u / 9, t = u - c * 9, r = t / 3, s3 = t - (t / 3) * 3;
+    const char* Bs = smem + 2 * HALO + ((u >> 1) & 1) * STG + (u & 1) * BST;
+    const char* Hs = smem + (c & 1) * HALO;
+#pragma unroll
+    for (int i = 0; i < RN; ++i) {
+      const int row = wn * RN * 16 + i * 16 + lr;
+      fa[i].lds(Bs + row * 64 + ((lh ^ rswz<bf16>(row)) << 4));
+    }
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int hp = hpb[m] + r * 66 + s3;
+      fb[m].lds(Hs + hp * 64 + ((lh ^ h3swz(hp)) << 4));
+    }
+  };
+  f32x4 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool prio = !(a.dbg & 32);
+  auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
+    if (prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
+    if (prio) __builtin_amdgcn_s_setprio(0);
+  };
+
+  Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
+  issue_b(0);
+  issue_halo(0);
+  if (nch > 1) issue_halo(1);
+  wait_vm<0>();
+  __syncthreads();
+  if (nsteps > 1) issue_b(1);
+  load_frags(fa0, fb0, 0);
+  int hn = 2, hstep = (9 * 2 - 10) / 2;       // next halo chunk and the step that issues it
+  for (int j = 0; j < nsteps; ++j) {
+    const bool two = 2 * j + 1 < ntap;
+    if (two) load_frags(fa1, fb1, 2 * j + 1);
+    mfma_all(fa0, fb0);
+    if (j + 1 < nsteps) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (j + 2 < nsteps) issue_b(j + 2);
+      if (hn < nch && j == hstep) {
+        issue_halo(hn);
+        ++hn;
+        hstep = (9 * hn - 10) / 2;
+      }
+      load_frags(fa0, fb0, 2 * j + 2);
+    }
+    if (two) mfma_all(fa1, fb1);
+  }
+  __syncthreads();
+  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+}
+
 // ----------------------------------------------------------------------------------------
 // Halo-tiled 7x7 forward for a small channel side (bf16): AFE.in_conv 3->64 forward,
 // Generator.out_conv 64->3 forward and its 3->64 backward-data.  The block's TR x 64 output
@@ -2218,9 +2357,9 @@ int halo3_bn(const fv_conv_desc* d) {
   }
   if (g_disable_h3 || !use_v2(d) || d->ksize != 3 || d->upsample || d->w % 64 || d->h % 4) return 0;
   if ((long)d->n * d->h * d->w * d->ldy * 2 >= (1L << 31)) return 0;
-  // co % 256 layers keep conv_fwd_v2's 256 x 256 pipelined tile (faster there; FV_H3_256=1
-  // routes them here for A/B)
-  static const bool h3_256 = getenv("FV_H3_256") != nullptr;
+  // co % 256: the pipelined pair-of-taps kernel (3 % over conv_fwd_v2's 256 x 256 tile on
+  // the res convs; FV_H3_256=0 keeps conv_fwd_v2 for A/B)
+  static const bool h3_256 = !getenv("FV_H3_256") || atoi(getenv("FV_H3_256")) != 0;
   if (d->cout % 256 == 0) return h3_256 ? 256 : 0;
   return d->cout % 128 == 0 ? 128 : d->cout % 64 == 0 ? 64 : 0;
 }
@@ -2792,12 +2931,20 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.ntn = d->cout / bn;
     const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
-    if (bn == 256)
-      hipLaunchKernelGGL((conv3_halo_fwd<4, 2, 4, 8>), dim3(nblk), dim3(512), 0, s, a, xb);
-    else if (bn == 128)
-      hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
-    else
-      hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
+    // 256: pipelined (1 block/CU either way); 128 / 64: the 2-blocks-per-CU single-tap loop
+    // wins (FV_H3_PIPE=0/1 forces one for A/B)
+    static const int pipe_env = getenv("FV_H3_PIPE") ? atoi(getenv("FV_H3_PIPE")) : -1;
+    const int pipe = pipe_env >= 0 ? pipe_env : bn == 256;
+    if (bn == 256) {
+      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8>), dim3(nblk), dim3(512), 0, s, a, xb);
+      else hipLaunchKernelGGL((conv3_halo_fwd<4, 2, 4, 8>), dim3(nblk), dim3(512), 0, s, a, xb);
+    } else if (bn == 128) {
+      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+      else hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+    } else {
+      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
+      else hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
+    }
     return fv_check_launch("conv2d_fwd_halo3");
   }
   if (use_v2(d)) {
