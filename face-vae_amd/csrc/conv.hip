@@ -1507,6 +1507,7 @@ template <int NCOL>
 __device__ __forceinline__ int tswz(int row) {
   if constexpr (NCOL >= 128) return (row & 3) | (((row >> 3) & 1) << 2);
   else if constexpr (NCOL == 64) return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  else if constexpr (NCOL == 32) return (row >> 3) & 1;   // rows r and r + 8 in different halves
   else return 0;
 }
 template <int NCOL>
@@ -1768,6 +1769,170 @@ conv_wgrad_v2(Wg2Args a) {
 #pragma unroll
     for (int j = 0; j < RC; ++j)
       a.bslab[(long)(SUB ? phase * a.nsplit + split : split) * a.CW + c0 + wc * RC * 16 + j * 16 + lr] = accb[j][0];
+  }
+}
+
+// ----------------------------------------------------------------------------------------
+// Weight gradient of a 3x3 stride-1 conv with a halo-staged input (bf16, cin % 32 == 0,
+// cout % 128 == 0, W % 64 == 0): dW[co][tap][ci] = sum_p dy[p][co] * x[p + off(tap)][ci].
+// A block owns 128 co x (9 taps x 32 ci) = 128 x 288 and walks 64-pixel row segments of its
+// pixel split.  Per segment the dy row (64 px x 128 co, 16 KB) and the x halo (3 rows x 66 px
+// x 32 ci, 13 KB) land in LDS by DMA through a 3-stage ring (counted vmcnt); the 9 taps read
+// shifted windows of the halo as transposed B fragments: 29 KB per 2.4 M MACs, against
+// conv_wgrad_v2's im2col tiles (64 KB per 4.2 M at 256 x 256, 32 KB per 1 M at 128 x 128).
+//   8 waves = 2 (64 co) x 4 (k-tiles of 16: 5, 5, 4, 4 of the 18), <= 20 accumulators.
+// Output: slab [split][cout][9 cin] (k = tap * cin + ci, wgrad_reduce_kernel's layout) and
+// bias slab [split][cout] (blocks of ci chunk 0).
+// ----------------------------------------------------------------------------------------
+struct H3WgArgs {
+  const void* x;
+  const void* dy;
+  float* slab;
+  float* bslab;
+  int H, W, Cin, Cout, ldd, nsegs, spb, ntile, nct;
+  unsigned xbytes, dybytes;
+};
+
+__global__ void __launch_bounds__(512, 1)
+conv3_halo_wgrad(H3WgArgs a) {
+  constexpr int BC = 128, NS = 3;
+  constexpr int DYB = 64 * BC * 2;                  // 16 pieces
+  constexpr int HPX = 3 * 66, HQ = (HPX * 64 + 1023) / 1024, HALO = HQ * 1024;   // 13 pieces
+  constexpr int BUF = DYB + HALO;
+  constexpr int JD = DYB / 1024 / 8, JH = (HQ + 7) / 8;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * BUF];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave & 1, wk = wave >> 1;
+  const int kt0 = wk < 2 ? 5 * wk : 10 + 4 * (wk - 2), nkt = wk < 2 ? 5 : 4;
+  const int li = lane & 15, g = lane >> 4;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tile = lid % a.ntile, sp = lid / a.ntile;   // blocks of one split share an XCD
+  const int tc = tile % a.nct, cc = tile / a.nct;
+  const int co0 = tc * BC, ci0 = cc * 32;
+  const int sw = a.W >> 6;
+  const int g0 = sp * a.spb, g1 = min(a.nsegs, g0 + a.spb);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), 0, (int)a.dybytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+
+  // per-lane piece constants: dy (pixel, channel) and halo (row, column, channel)
+  int dpx[JD], dco[JD];
+#pragma unroll
+  for (int j = 0; j < JD; ++j) {
+    const int o = (wave + 8 * j) * 1024 + lane * 16;
+    dpx[j] = o / (BC * 2);
+    const int b = o - dpx[j] * (BC * 2);
+    dco[j] = ((((b >> 5) ^ tswz<BC>(dpx[j])) << 4) | (((b >> 4) & 1) << 3));
+  }
+  int hhr[JH], hhc[JH], hci[JH];
+#pragma unroll
+  for (int j = 0; j < JH; ++j) {
+    const int o = (wave + 8 * j) * 1024 + lane * 16;
+    const int hp = o >> 6, b = o & 63;
+    hci[j] = ((((b >> 5) ^ tswz<32>(hp)) << 4) | (((b >> 4) & 1) << 3));
+    hhr[j] = hp < HPX ? hp / 66 : 99;
+    hhc[j] = hp - (hp / 66) * 66;
+  }
+  const int nh = (HQ - wave + 7) / 8;               // halo pieces of this wave (JH or JH - 1)
+
+  auto issue = [&](int gs, int buf) {
+    const int n = gs / (a.H * sw), rem = gs - n * a.H * sw;
+    const int h = rem / sw, w0 = (rem - h * sw) * 64;
+    const unsigned ds = sbase + buf * BUF, hs = ds + DYB;
+    const int pbase = (n * a.H + h) * a.W + w0;
+#pragma unroll
+    for (int j = 0; j < JD; ++j)
+      dma16s(dr, ds + (wave + 8 * j) * 1024, (unsigned)(((pbase + dpx[j]) * a.ldd + co0 + dco[j]) * 2), 0u);
+#pragma unroll
+    for (int j = 0; j < JH; ++j) {
+      if (j < JH - 1 || wave + 8 * j < HQ) {
+        const int ih = h + hhr[j] - 1, iw = w0 + hhc[j] - 1;
+        const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+        dma16s(xr, hs + (wave + 8 * j) * 1024,
+               ok ? (unsigned)((((n * a.H + ih) * a.W + iw) * a.Cin + ci0 + hci[j]) * 2) : 0x80000000u, 0u);
+      }
+    }
+  };
+  // wait until the stage issued `ahead` issues ago has landed (the later ones may stay in flight)
+  auto wait_stage = [&](int ahead) {
+    if (ahead >= 2) {
+      if (nh == JH) wait_vm<2 * (JD + JH)>();
+      else wait_vm<2 * (JD + JH - 1)>();
+    } else if (ahead == 1) {
+      if (nh == JH) wait_vm<JD + JH>();
+      else wait_vm<JD + JH - 1>();
+    } else {
+      wait_vm<0>();
+    }
+  };
+
+  f32x4 acc[4][5];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  const bool do_bias = a.bslab && cc == 0;
+  const int bco = tid & (BC - 1), bpg = tid >> 7;      // bias: channel, 16-pixel group
+
+  const int nseg = g1 - g0;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nseg) issue(g0 + i, i);
+  for (int i = 0; i < nseg; ++i) {
+    // stages issued after stage i: min(NS - 2, nseg - 1 - i)
+    wait_stage(min(NS - 2, nseg - 1 - i));
+    __syncthreads();                                  // stage i landed everywhere; stage i-1 retired
+    if (i + NS - 1 < nseg) issue(g0 + i + NS - 1, (i + NS - 1) % NS);
+    const char* dys = smem + (i % NS) * BUF;
+    const char* hal = dys + DYB;
+    if (do_bias) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        bsum += (float)*reinterpret_cast<const bf16*>(dys + timg_off<BC>(bpg * 16 + k, bco));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) af[q] = tfrag<BC>(dys, kk * 32, wc * 64 + q * 16, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        if (j < nkt) {
+          const int kt = kt0 + j, tap = kt >> 1, cb = (kt & 1) * 16;
+          const int r = tap / 3, s3 = tap - (tap / 3) * 3;
+          const bf16x8 bfr = tfrag<32>(hal, r * 66 + kk * 32 + s3, cb, lane);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bfr, acc[q][j], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  // slab[sp][co][tap * Cin + ci0 + ci]: lane holds D[co = 4g + jj][k-col = li]
+  const long K = 9L * a.Cin;
+  float* sl = a.slab + (long)sp * a.Cout * K;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    if (j < nkt) {
+      const int kt = kt0 + j, tap = kt >> 1, cb = (kt & 1) * 16;
+      const long kcol = (long)tap * a.Cin + ci0 + cb + li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) sl[(long)(co0 + wc * 64 + q * 16 + 4 * g + jj) * K + kcol] = acc[q][j][jj];
+    }
+  }
+  if (do_bias) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    red[tid] = bsum;
+    __syncthreads();
+    if (tid < BC) a.bslab[(long)sp * a.Cout + co0 + tid] = (red[tid] + red[tid + 128]) + (red[tid + 256] + red[tid + 384]);
   }
 }
 
@@ -2485,6 +2650,20 @@ bool use_c7n(const fv_conv_desc* d) {
          (long)d->n * d->h * d->w * 64 * 2 < (1L << 31);
 }
 
+// 3x3 weight gradient with the halo-staged input (conv3_halo_wgrad)
+static int g_disable_h3w = -1;
+bool use_h3w(const fv_conv_desc* d) {
+  if (g_disable_h3w < 0) {
+    const char* e = getenv("FV_DISABLE_H3W");
+    g_disable_h3w = (e && e[0] == '1') ? 1 : 0;
+  }
+  // measured against conv_wgrad_v2 (tools/convbench.py): 12 % faster on AFE.down1 (64 -> 128,
+  // whose v2 tile is 128 x 128), slower where v2 runs 256 x 256 tiles (LDS fill per MAC of
+  // the two is then within 20 %), so only cin == 64 takes it
+  return !g_disable_h3w && d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && !d->pro_act &&
+         d->cin == 64 && d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
+}
+
 // out_conv weight gradient as "row taps in N" (conv7_n3_wgrad)
 int g_disable_c7w = -1;
 bool use_c7w(const fv_conv_desc* d) {
@@ -2591,6 +2770,21 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
     p.CW = 32;
     p.KW = 448;
     p.ntk = p.ntc = 1;
+    return p;
+  }
+  // 3x3 halo wgrad (v2 == 4): tiles of 128 co x (9 taps x 64 ci), ~1 block per CU
+  if (p.v2 && use_h3w(d)) {
+    p.v2 = 4;
+    p.ntc = d->cout / 128;
+    p.ntk = d->cin / 32;
+    const int ntile = p.ntc * p.ntk;
+    p.nsteps = d->n * d->h * (d->w / 64);        // 64-pixel row segments
+    int ns = 256 / ntile;
+    if (ns < 1) ns = 1;
+    p.sps = fv_cdiv(p.nsteps, ns);               // segments per split
+    p.nsplit = fv_cdiv(p.nsteps, p.sps);
+    p.CW = d->cout;
+    p.KW = K;
     return p;
   }
   // 7x7 halo path (v2 == 2): one persistent block per CU, ntk = 1 (all k in one tile)
@@ -3054,6 +3248,17 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
   const WgPlan t = plan_wgrad(d);
   const int Hin = d->upsample ? d->h / 2 : d->h, Win = d->upsample ? d->w / 2 : d->w;
   const long P = (long)d->n * d->h * d->w;
+  if (t.v2 == 4) {
+    FV_REQUIRE(P * ldy_dy * 2 < (1L << 31) && P * d->cin * 2 < (1L << 31), "wgrad: operand larger than 2 GB");
+    H3WgArgs a{};
+    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+    a.H = d->h; a.W = d->w; a.Cin = d->cin; a.Cout = d->cout; a.ldd = ldy_dy;
+    a.nsegs = t.nsteps; a.spb = t.sps; a.ntile = t.ntc * t.ntk; a.nct = t.ntc;
+    a.xbytes = (unsigned)(P * d->cin * 2);
+    a.dybytes = (unsigned)(P * ldy_dy * 2);
+    hipLaunchKernelGGL(conv3_halo_wgrad, dim3(a.ntile * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    return fv_check_launch("conv2d_bwd_weight_halo3");
+  }
   if (t.v2 == 3) {
     FV_REQUIRE(ldy_dy == 8, "wgrad (out_conv 7x7): dy channel stride must be 8 (got %d)", ldy_dy);
     W7Args a{};
