@@ -15,6 +15,17 @@ constexpr int NSPLIT = 128;   // level-1 splits of the conv-partials reduction
 constexpr int MAXBLK = 1024;  // max blocks (= level-1 records) of the streaming reductions
 constexpr int NTH = 256;
 
+// level-1 splits of the conv-partials reduction: enough blocks to cover the chip (>= 1024 over
+// all channel groups) with >= 16 records per split; <= MAXBLK (the ws size)
+int partial_splits(int nb, int c) {
+  int ns = 1024 / ((c + 63) / 64);
+  if (ns < NSPLIT) ns = NSPLIT;
+  const int by_records = (nb + 15) / 16;
+  if (ns > by_records) ns = by_records;
+  if (ns < 1) ns = 1;
+  return ns > MAXBLK ? MAXBLK : ns;
+}
+
 // blocks of a streaming per-channel reduction over `pixels` x (C/8) chunks: >= 8 chunks per thread
 int stream_blocks(long pixels, int C) {
   const long work = pixels * (C / 8);
@@ -44,7 +55,7 @@ __global__ void partials_kernel(const float* __restrict__ part, int nb, int bpix
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r = threadIdx.x >> 6;
   const int split = blockIdx.y;
-  const int per = (nb + NSPLIT - 1) / NSPLIT;
+  const int per = (nb + gridDim.y - 1) / gridDim.y;
   const int b0 = split * per, b1 = min(nb, b0 + per);
   double n = 0, S = 0, Q = 0;
   if (c < C) {
@@ -169,26 +180,42 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
 
 // single-process form: sum the level-1 records [split][3][C] over the splits and finalize, one
 // wave per channel (replaces sum_splits + finalize + the num_batches_tracked increment)
-__global__ void sum_finalize_kernel(const double* ws, int nsplit, int C, const float* gamma, const float* beta,
-                                    float eps, float mom, float* rm, float* rv, long long* nbt, float* save_mean,
-                                    float* save_invstd, float* scale, float* shift) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+// sum the level-1 records [split][3][C] and finalize.  Block = 16 channels x 64 split phases
+// (1024 threads: lane = (channel, phase & 3), wave = phase >> 2), so one load instruction
+// reads 4 split rows x 128 contiguous bytes; fixed-order LDS combine of the 64 phases.
+constexpr int SUMT = 1024, SUMCH = 16, SUMPH = SUMT / SUMCH;
+__global__ void __launch_bounds__(SUMT)
+sum_finalize_kernel(const double* ws, int nsplit, int C, const float* gamma, const float* beta,
+                    float eps, float mom, float* rm, float* rv, long long* nbt, float* save_mean,
+                    float* save_invstd, float* scale, float* shift) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ch = lane & 15, ph = w * 4 + (lane >> 4);
+  const int c = blockIdx.x * SUMCH + ch;
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
-  if (c >= C) return;
   double n = 0, S = 0, Q = 0;
+  if (c < C) {
 #pragma unroll 4
-  for (int sp = lane; sp < nsplit; sp += 64) {
-    const double* r = ws + (long)sp * 3 * C + c;
-    n += r[0];
-    S += r[C];
-    Q += r[2 * C];
+    for (int sp = ph; sp < nsplit; sp += SUMPH) {
+      const double* r = ws + (long)sp * 3 * C + c;
+      n += r[0];
+      S += r[C];
+      Q += r[2 * C];
+    }
   }
-  n = wave_sum_d(n);
-  S = wave_sum_d(S);
-  Q = wave_sum_d(Q);
-  if (lane == 0)
+  __shared__ double red[3][SUMPH][SUMCH];
+  red[0][ph][ch] = n;
+  red[1][ph][ch] = S;
+  red[2][ph][ch] = Q;
+  __syncthreads();
+  if (threadIdx.x < SUMCH && c < C) {
+    n = S = Q = 0;
+    for (int k = 0; k < SUMPH; ++k) {
+      n += red[0][k][ch];
+      S += red[1][k][ch];
+      Q += red[2][k][ch];
+    }
     bn_finalize_one(c, C, n, S, Q, gamma, beta, eps, mom, 1, rm, rv, save_mean, save_invstd, scale, shift);
+  }
 }
 
 // out = [pool](act(y*scale+shift)).  grid.y = output row (n*Ho + i), grid.x covers the row's
@@ -318,21 +345,31 @@ __global__ void bwd_finalize_kernel(const double* red, int C, double count, floa
   k[C + c] = (float)(sgy / count);
 }
 
-// single-process form: sum the level-1 records [split][2][C] and finalize, one wave per channel
-__global__ void bwd_sum_finalize_kernel(const double* ws, int nsplit, int C, double count, float* dgamma,
-                                        float* dbeta, float* k) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
+// single-process form: sum the level-1 records [split][2][C] and finalize (mapping of
+// sum_finalize_kernel)
+__global__ void __launch_bounds__(SUMT)
+bwd_sum_finalize_kernel(const double* ws, int nsplit, int C, double count, float* dgamma, float* dbeta, float* k) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ch = lane & 15, ph = w * 4 + (lane >> 4);
+  const int c = blockIdx.x * SUMCH + ch;
   double sg = 0, sgy = 0;
-#pragma unroll 8
-  for (int sp = lane; sp < nsplit; sp += 64) {
-    sg += ws[(long)sp * 2 * C + c];
-    sgy += ws[(long)sp * 2 * C + C + c];
+  if (c < C) {
+#pragma unroll 4
+    for (int sp = ph; sp < nsplit; sp += SUMPH) {
+      sg += ws[(long)sp * 2 * C + c];
+      sgy += ws[(long)sp * 2 * C + C + c];
+    }
   }
-  sg = wave_sum_d(sg);
-  sgy = wave_sum_d(sgy);
-  if (lane == 0) {
+  __shared__ double red[2][SUMPH][SUMCH];
+  red[0][ph][ch] = sg;
+  red[1][ph][ch] = sgy;
+  __syncthreads();
+  if (threadIdx.x < SUMCH && c < C) {
+    sg = sgy = 0;
+    for (int j = 0; j < SUMPH; ++j) {
+      sg += red[0][j][ch];
+      sgy += red[1][j][ch];
+    }
     if (dbeta) dbeta[c] = (float)sg;
     if (dgamma) dgamma[c] = (float)sgy;
     k[c] = (float)(sg / count);
@@ -399,11 +436,12 @@ int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixe
   FV_REQUIRE(partials && stats && ws, "null pointer");
   FV_REQUIRE(nblocks > 0 && c > 0, "bad sizes");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), NSPLIT), dim3(NTH), 0, s, partials, nblocks,
+  const int ns = partial_splits(nblocks, c);
+  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), ns), dim3(NTH), 0, s, partials, nblocks,
                      block_pixels, total_pixels, c, (double*)ws);
   int st = fv_check_launch("bn_partials");
   if (st) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 4)), dim3(NTH), 0, s, (const double*)ws, NSPLIT,
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 4)), dim3(NTH), 0, s, (const double*)ws, ns,
                      3, c, stats);
   return fv_check_launch("bn_sum_splits");
 }
@@ -448,11 +486,12 @@ int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_
   FV_REQUIRE(partials && ws, "null pointer");
   FV_REQUIRE(nblocks > 0 && c > 0, "bad sizes");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), NSPLIT), dim3(NTH), 0, s, partials, nblocks,
+  const int ns = partial_splits(nblocks, c);
+  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), ns), dim3(NTH), 0, s, partials, nblocks,
                      block_pixels, total_pixels, c, (double*)ws);
   int st = fv_check_launch("bn_partials");
   if (st) return st;
-  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, 4)), dim3(NTH), 0, s, (const double*)ws, NSPLIT, c, gamma,
+  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, (const double*)ws, ns, c, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, save_mean, save_invstd,
                      scale, shift);
   return fv_check_launch("bn_sum_finalize");
@@ -474,7 +513,7 @@ int fv_bn_stats_finalize_tensor(int dtype, const void* x, long pixels, int c, in
     hipLaunchKernelGGL(tensor_stats_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)x, pixels, c, ldc,
                        (double*)ws);
   if ((st = fv_check_launch("bn_tensor_stats"))) return st;
-  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, c, gamma,
+  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, (const double*)ws, nb, c, gamma,
                      beta, eps, momentum, running_mean, running_var, num_batches_tracked, save_mean, save_invstd,
                      scale, shift);
   return fv_check_launch("bn_sum_finalize");
@@ -543,7 +582,7 @@ int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, in
     hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
                        (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
-  hipLaunchKernelGGL(bwd_sum_finalize_kernel, dim3(fv_cdiv(c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, c,
+  hipLaunchKernelGGL(bwd_sum_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, (const double*)ws, nb, c,
                      (double)count, dgamma, dbeta, k);
   return fv_check_launch("bn_bwd_sum_finalize");
 }

@@ -2280,12 +2280,12 @@ conv_halo_wgrad(HaloWgArgs a) {
 // weight re-layout (+ 1/sigma) and slab reduction
 // ----------------------------------------------------------------------------------------
 template <typename T>
-__global__ void weight_prep_kernel(const float* __restrict__ wp, const float* sigma, T* wk,
-                                   int rows, int Kpad, int cout, int cin_valid, int lgCin, int KS,
-                                   int K, int transposed) {
+__device__ __forceinline__ void weight_prep_body(const float* __restrict__ wp, const float* sigma, T* wk, int rows,
+                                                 int Kpad, int cout, int cin_valid, int lgCin, int KS, int K,
+                                                 int transposed, int bid, int nblk) {
   const long total = (long)rows * Kpad;
   const float inv = sigma ? 1.f / sigma[0] : 1.f;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+  for (long e = bid * (long)blockDim.x + threadIdx.x; e < total; e += (long)nblk * blockDim.x) {
     const int row = (int)(e / Kpad), k = (int)(e - (long)row * Kpad);
     float v = 0.f;
     if (k < K) {
@@ -2300,6 +2300,24 @@ __global__ void weight_prep_kernel(const float* __restrict__ wp, const float* si
     }
     wk[e] = Elt<T>::from_f(v * inv);
   }
+}
+
+template <typename T>
+__global__ void weight_prep_kernel(const float* __restrict__ wp, const float* sigma, T* wk,
+                                   int rows, int Kpad, int cout, int cin_valid, int lgCin, int KS,
+                                   int K, int transposed) {
+  weight_prep_body<T>(wp, sigma, wk, rows, Kpad, cout, cin_valid, lgCin, KS, K, transposed, blockIdx.x, gridDim.x);
+}
+
+// both layouts in one launch: blocks [0, nb1) write wk, the rest wt
+struct WPrepJob { void* out; int rows, Kpad, lgCin, K, transposed, nb; };
+template <typename T>
+__global__ void weight_prep2_kernel(const float* __restrict__ wp, const float* sigma, int cout, int cin_valid, int KS,
+                                    WPrepJob j0, WPrepJob j1) {
+  const bool second = (int)blockIdx.x >= j0.nb;
+  const WPrepJob& j = second ? j1 : j0;
+  weight_prep_body<T>(wp, sigma, (T*)j.out, j.rows, j.Kpad, cout, cin_valid, j.lgCin, KS, j.K, j.transposed,
+                      second ? blockIdx.x - j0.nb : blockIdx.x, j.nb);
 }
 
 // sub-pixel phase weights of an upsample + 3x3 conv: for phase (pa, pb) the 2x2 tap (r', s')
@@ -3009,6 +3027,24 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   if (st) return st;
   hipStream_t s = (hipStream_t)stream;
   const int ks = d->ksize;
+  const bool generic_wk = wk && !use_c7n(d) && !use_subpix(d);
+  const bool generic_wt = wt && !use_dgrad_lowres(d);
+  if (generic_wk && generic_wt) {
+    // the common case: forward and transposed layouts in one launch
+    const FwdTile tk = fwd_tile(d->cout), tt = fwd_tile(d->cin);
+    const int cin_t = pad_pow2_8(d->cout);
+    WPrepJob j0{wk, fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin), ks * ks * d->cin, 0, 0};
+    WPrepJob j1{wt, fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t), ks * ks * cin_t, 1, 0};
+    j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 4096);
+    j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 4096);
+    if (d->dtype == FV_BF16)
+      hipLaunchKernelGGL(weight_prep2_kernel<bf16>, dim3(j0.nb + j1.nb), dim3(256), 0, s, w_param, sigma, d->cout,
+                         d->cin_valid, ks, j0, j1);
+    else
+      hipLaunchKernelGGL(weight_prep2_kernel<float>, dim3(j0.nb + j1.nb), dim3(256), 0, s, w_param, sigma, d->cout,
+                         d->cin_valid, ks, j0, j1);
+    return fv_check_launch("weight_prep2");
+  }
   if (wk && use_c7n(d)) {
     hipLaunchKernelGGL(weight_prep_c7n_kernel, dim3(56), dim3(256), 0, s, w_param, sigma, (bf16*)wk, d->cout);
     if ((st = fv_check_launch("weight_prep_c7n"))) return st;
