@@ -692,6 +692,27 @@ __device__ __forceinline__ int h3swz(int hp) { return ((hp >> 2) & 1) << 1; }
 
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// wave-uniform count -> the matching immediate (counts above 15 wait for 15: stricter, safe)
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    case 8: wait_vm<8>(); break;
+    case 9: wait_vm<9>(); break;
+    case 10: wait_vm<10>(); break;
+    case 11: wait_vm<11>(); break;
+    case 12: wait_vm<12>(); break;
+    case 13: wait_vm<13>(); break;
+    case 14: wait_vm<14>(); break;
+    default: wait_vm<15>(); break;
+  }
+}
 
 template <int WN, int WM, int RN, int RM>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
@@ -818,8 +839,9 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
 // taps' 32-channel slices, and the loop is conv_fwd_v2's: the fragments of the step's second
 // tap are read while the first tap's MFMAs run and the barrier sits between the two MFMA
 // groups.  Chunk c's halo goes into buffer c & 1 right after the barrier that retires the
-// last read of chunk c - 2 (5 steps before its first use).
-template <int WN, int WM, int RN, int RM>
+// last read of chunk c - 2 (5 steps before its first use).  The weight stages form a ring of
+// NSB buffers issued NSB - 1 steps ahead, so a DMA has NSB - 2 full steps to land.
+template <int WN, int WM, int RN, int RM, int NSB>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
@@ -829,7 +851,7 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   constexpr int QB = BN / 16, JB = QB / NW;
   static_assert(QB % NW == 0, "weight pieces per wave");
   constexpr int BST = BN * 64, STG = 2 * BST;
-  constexpr int MAIN = 2 * HALO + 2 * STG, EPI = BM * BN * 2;
+  constexpr int MAIN = 2 * HALO + NSB * STG, EPI = BM * BN * 2;
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -865,13 +887,13 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
     wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ rswz<bf16>(row)) << 3)) * 2);
   }
   const int nch = a.Cin >> 5, ntap = 9 * nch, nsteps = (ntap + 1) >> 1;
-  auto issue_b = [&](int j) {
+  auto issue_b = [&](int j, int buf) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int u = 2 * j + h;
       if (u < ntap) {
         const int c = u / 9, t = u - c * 9;
-        const unsigned Bs = sbase + 2 * HALO + (j & 1) * STG + h * BST;
+        const unsigned Bs = sbase + 2 * HALO + buf * STG + h * BST;
         const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
 #pragma unroll
         for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase[jb], k0 * 2);
@@ -892,9 +914,9 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
     const int loc = wm * RM * 16 + m * 16 + lr;
     hpb[m] = (loc >> 6) * 66 + (loc & 63);
   }
-  auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], int u) {
+  auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], int u, int buf) {
     const int c = u / 9, t = u - c * 9, r = t / 3, s3 = t - (t / 3) * 3;
-    const char* Bs = smem + 2 * HALO + ((u >> 1) & 1) * STG + (u & 1) * BST;
+    const char* Bs = smem + 2 * HALO + buf * STG + (u & 1) * BST;
     const char* Hs = smem + (c & 1) * HALO;
 #pragma unroll
     for (int i = 0; i < RN; ++i) {
@@ -923,31 +945,54 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   };
 
   Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
-  issue_b(0);
+  const int nh = (HQ - wave + NW - 1) / NW;   // halo pieces this wave issues
+  auto bcnt = [&](int j) { return j < nsteps ? (2 * j + 1 < ntap ? 2 : 1) * JB : 0; };
+  // ring of NSB weight stages: stage j in buffer j % NSB, issued NSB - 1 steps ahead; the
+  // barrier of step j waits for stage j + 1 only (counted vmcnt: what this wave issued in
+  // step j - 1 may stay in flight)
+  issue_b(0, 0);
   issue_halo(0);
   if (nch > 1) issue_halo(1);
+  for (int i = 1; i < NSB - 1; ++i)
+    if (i < nsteps) issue_b(i, i);
   wait_vm<0>();
   __syncthreads();
-  if (nsteps > 1) issue_b(1);
-  load_frags(fa0, fb0, 0);
-  int hn = 2, hstep = (9 * 2 - 10) / 2;       // next halo chunk and the step that issues it
+  int pend = 0;                                 // DMAs this wave issued in the previous step
+  if (NSB - 1 < nsteps) {
+    issue_b(NSB - 1, NSB - 1);
+    pend = bcnt(NSB - 1);
+  }
+  load_frags(fa0, fb0, 0, 0);
+  int hn = 2, hstep = (9 * 2 - 10) / 2;         // next halo chunk and the step that issues it
+  int bj = 0;                                   // buffer of stage j
   for (int j = 0; j < nsteps; ++j) {
     const bool two = 2 * j + 1 < ntap;
-    if (two) load_frags(fa1, fb1, 2 * j + 1);
+    if (two) load_frags(fa1, fb1, 2 * j + 1, bj);
     mfma_all(fa0, fb0);
+    const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
     if (j + 1 < nsteps) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      // the weight stage is issued LAST in a step, so the count left in flight is that
+      // stage's alone (a halo issued before it is waited for one step later)
+      if constexpr (NSB == 2) wait_vm<0>();     // stage j + 1 was the one issued last
+      else if (pend == 2 * JB) wait_vm<2 * JB>();
+      else wait_vm_dyn(pend);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (j + 2 < nsteps) issue_b(j + 2);
       if (hn < nch && j == hstep) {
         issue_halo(hn);
         ++hn;
         hstep = (9 * hn - 10) / 2;
       }
-      load_frags(fa0, fb0, 2 * j + 2);
+      pend = 0;
+      if (j + NSB < nsteps) {
+        issue_b(j + NSB, bj);
+        pend = bcnt(j + NSB);
+      }
+      load_frags(fa0, fb0, 2 * j + 2, bn1);
     }
     if (two) mfma_all(fa1, fb1);
+    bj = bn1;
   }
   __syncthreads();
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
@@ -3166,13 +3211,15 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     static const int pipe_env = getenv("FV_H3_PIPE") ? atoi(getenv("FV_H3_PIPE")) : -1;
     const int pipe = pipe_env >= 0 ? pipe_env : bn == 256;
     if (bn == 256) {
-      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8>), dim3(nblk), dim3(512), 0, s, a, xb);
+      static const int nsb = getenv("FV_H3_NSB") ? atoi(getenv("FV_H3_NSB")) : 2;   // 3: deeper ring (A/B: 2.5 % slower)
+      if (pipe && nsb == 2) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+      else if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd<4, 2, 4, 8>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 128) {
-      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else {
-      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
+      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4, 3>), dim3(nblk), dim3(256), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
     }
     return fv_check_launch("conv2d_fwd_halo3");
