@@ -714,9 +714,14 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
   }
 }
 
-template <int WN, int WM, int RN, int RM>
+// SUBP: one sub-pixel phase of an upsample + 3x3 conv (conv_fwd_v2 MODE 2's algebra): tile
+// space = the low-res input, block phase = lid & 3 (the 4 phases of a tile are neighbours),
+// 4 taps (r', s') per chunk at input offsets (r' + pa - 1, s' + pb - 1), phase-folded weights
+// [4][rows][4 cin]; the halo is the same (TR + 2) x 66 window.
+template <int WN, int WM, int RN, int RM, bool SUBP = false>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
+  constexpr int NT = SUBP ? 4 : 9;                  // taps per 32-channel chunk
   constexpr int NW = WN * WM;
   constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
   constexpr int HP = (TR + 2) * 66, HQ = (HP + 15) / 16, JH = (HQ + NW - 1) / NW;
@@ -732,7 +737,11 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
   const int wn = wave % WN, wm = wave / WN;
   const int nblk = gridDim.x, bid = blockIdx.x;
   const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int lid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int phase = SUBP ? (lid0 & 3) : 0;
+  const int lid = SUBP ? (lid0 >> 2) : lid0;
+  if constexpr (SUBP) a.sub = 1 + phase;
+  const int pa = phase >> 1, pb = phase & 1;
   const int tn = lid % a.ntn, tm = lid / a.ntn;
   const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
   const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
@@ -743,6 +752,7 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
   const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
   const int lrow = lane >> 2, lchk = lane & 3;
+  const unsigned wph = SUBP ? (unsigned)(phase * a.wphase) : 0u;   // this phase's weight block
 
   // halo pieces of this wave: source offsets (0x80000000: outside the image -> zero fill)
   unsigned hoff[JH];
@@ -762,9 +772,9 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
     wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ rswz<bf16>(row)) << 3)) * 2);
   }
   auto issue_b = [&](int ks) {
-    const int c = ks / 9, t = ks - c * 9;
+    const int c = ks / NT, t = ks - c * NT;
     const unsigned Bs = sbase + 2 * HALO + (ks & 1) * BST;
-    const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
+    const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32) + wph;
 #pragma unroll
     for (int j = 0; j < JB; ++j) dma16s(wr, Bs + (wave + j * NW) * 1024, wbase[j], k0 * 2);
   };
@@ -788,12 +798,12 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
 #pragma unroll
     for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nch = a.Cin >> 5, nks = 9 * nch;
+  const int nch = a.Cin >> 5, nks = NT * nch;
   const bool prio = !(a.dbg & 32);
   issue_b(0);
   issue_halo(0);
   for (int ks = 0; ks < nks; ++ks) {
-    const int c = ks / 9, t = ks - c * 9;
+    const int c = ks / NT, t = ks - c * NT;
     // step 9c+1 may leave the halo of chunk c+1 (issued last, at step 9c) in flight
     if (t == 1 && c + 1 < nch) {
       if (nh == JH) wait_vm<JH>();
@@ -807,7 +817,8 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
       if (t == 0 && c + 1 < nch) issue_halo(c + 1);
     }
     if (a.dbg & 1) continue;                          // bit 0: no fragment reads / MFMA (experiment)
-    const int r = t / 3, s3 = t - (t / 3) * 3;
+    // halo row / column of the tap (the halo starts one pixel above / left of the tile)
+    const int r = SUBP ? (t >> 1) + pa : t / 3, s3 = SUBP ? (t & 1) + pb : t - (t / 3) * 3;
     const char* Hs = smem + (c & 1) * HALO;
     const char* Bs = smem + 2 * HALO + (ks & 1) * BST;
     Frag<bf16> fa[RN], fb[RM];
@@ -832,7 +843,7 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
     if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.y)[tid] = acc[RN - 1][RM - 1][3];
     return;
   }
-  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, SUBP ? tm * 4 + phase : tm, wn, wm, lane, tid);
 }
 
 // Software-pipelined variant: a step is a PAIR of taps (64 k), the weight stage holds both
@@ -2690,6 +2701,20 @@ bool use_subpix(const fv_conv_desc* d) {
   return pl % fwd_tile_v2(d->cout).bm == 0;
 }
 
+// sub-pixel phases through the halo-staged kernel: co tile (128 / 64), 0 when not eligible
+static int g_disable_h3sub = -1;
+int subpix_halo_bn(const fv_conv_desc* d) {
+  if (g_disable_h3sub < 0) {
+    const char* e = getenv("FV_DISABLE_H3SUB");
+    g_disable_h3sub = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_disable_h3sub || !use_subpix(d)) return 0;
+  const int hl = d->h / 2, wl = d->w / 2;
+  if (wl % 64 || hl % 4 || d->cin % 32) return 0;
+  // co tiles of 128 only: up1 -17 %; with 64 (up2) conv_fwd_v2 MODE 2 stays 5 % faster
+  return d->cout % 128 == 0 ? 128 : 0;
+}
+
 // data gradient of an upsample + 3x3 conv computed directly at the low resolution as a
 // stride-2 4x4 conv over dy (bf16 v2 path; replaces dgrad at the high resolution followed by
 // the 2x2 sum of fv_upsample2x_bwd: 0.44x the MACs, one pass fewer)
@@ -3049,6 +3074,7 @@ static int stats_record_pixels(const fv_conv_desc* d) {
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
   const FwdTile t = plan_tile(d);
   if (const int bn = halo3_bn(d)) return bn == 256 ? 128 : 64;   // RM * 16 pixels per wave row
+  if (subpix_halo_bn(d)) return 64;                            // RM * 16 (both co tiles)
   if (use_v2(d)) {
     if (t.bn == 64 || t.bn == 16 || (t.bn == 128 && t.bm == 256)) return t.bm / 4;
     return t.bm / 2;                                          // 128x128, 256x256, 256x128
@@ -3191,6 +3217,19 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.nks = a.Kpad / BK2;
     a.ntn = fv_cdiv(d->cout, t2.bn);
     a.wphase = fv_cdiv(d->cout, t.bn) * t.bn * a.Kpad;
+    if (const int bn = subpix_halo_bn(d)) {
+      // halo-staged phases: the low-res (TR + 2) x 66 window is staged once per 32 channels
+      // for the phase's 4 taps (conv3_halo_fwd<..., SUBP>)
+      a.lgtw = 6;
+      a.ntn = d->cout / bn;
+      const int nblk = 4 * a.ntn * d->n * (a.H / 4) * (a.W / 64);
+      const unsigned xb = (unsigned)((long)d->n * a.Hin * a.Win * d->cin * 2);
+      if (bn == 128)
+        hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4, true>), dim3(nblk), dim3(512), 0, s, a, xb);
+      else
+        hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4, true>), dim3(nblk), dim3(256), 0, s, a, xb);
+      return fv_check_launch("conv2d_fwd_subpix_halo");
+    }
     const int nblk2 = 4 * a.ntn * (a.P / t2.bm);
     const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
     st = launch_v2(a, 2, t2, 2, nblk2, (unsigned)xb, s);
