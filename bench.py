@@ -75,18 +75,18 @@ def cpu_baseline(args, cfg):
 PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
 
 
-def pmc_traffic(cfg, B, dtype, avg_ms):
+def pmc_traffic(cfg, B, dtype, fam, avg_ms):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes
     (tools/gpu_pmc.sh -> profiles/r1_pmc_traffic.json; (2 x FETCH_SIZE + WRITE_SIZE) KiB,
     the gfx950 correction of MI355X_MICROARCH.md).  Measured on the default 256x256, B=32
     bf16 configuration only; other configurations report null."""
     if not (cfg.H == 256 and B == 32 and dtype == torch.bfloat16 and os.path.exists(PMC_FILE)):
         return {}
-    dom = json.load(open(PMC_FILE)).get("dominant")
+    dom = (json.load(open(PMC_FILE)).get("dominant") or {}).get(fam)
     if not dom:
         return {}
     t = dom["hbm_bytes_per_launch"]
-    return {"traffic": round(t), "traffic_unit": "bytes/launch (PMC, profiles/r1_pmc_traffic.json)",
+    return {"traffic": round(t), "traffic_unit": f"bytes/launch (PMC, profiles/r1_pmc_traffic.json, {dom['kernel']})",
             "traffic_gbs_at_avg": round(t / (avg_ms * 1e-3) / 1e9, 1),
             "algorithmic_bytes": 2 * (B * cfg.latent_hw ** 2 * cfg.up_seq[0] * 2) + cfg.up_seq[0] ** 2 * 9 * 2}
 
@@ -167,7 +167,7 @@ def main():
                 "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "avg_ms": round(fam[dom], 4), "flop_per_launch": f_launch, "traffic": None,
                 "families_avg_ms": {k: round(v, 4) for k, v in fam.items()}}
-        roof.update(pmc_traffic(cfg, B, dtype, fam[dom]))
+        roof.update(pmc_traffic(cfg, B, dtype, dom, fam[dom]))
     from oracle.facevae_cpu import OracleConfig, flops_per_image
     _, f_img = flops_per_image(OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent,
                                             n_res=cfg.n_res, up_seq=cfg.up_seq))

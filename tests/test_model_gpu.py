@@ -170,6 +170,46 @@ def test_full256_step_matches_oracle(full_oracle, dtype):
         assert dev["image"] < 5e-2 and dev["R"] < 1e-2 and dev["K"] < 1e-2
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_full512_step_matches_oracle(dtype):
+    """BASELINE config C4 (512x512 high-res VAE): every spatial extent doubles (latent 128x128,
+    AFE.in_conv / UpBlock2 at 512x512), so each kernel runs at shapes the 256 case never
+    reaches.  One step at B=1 vs the CPU oracle (fp32 mode 1e-3; bf16 reported, loose bound),
+    plus the step-2 losses (after Adam on the GPU vs Adam on the oracle)."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ocfg = O.OracleConfig(H=512)
+    torch.manual_seed(0)
+    cfg = fv.FaceVAEConfig.hires()
+    m = fv.FaceVAE(cfg)
+    init = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.cuda().train().set_compute_dtype(dtype)
+    opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
+    x = torch.rand(1, 3, 512, 512, generator=torch.Generator().manual_seed(1234))
+    eps = torch.randn(1, 256, 128, 128, generator=torch.Generator().manual_seed(1235))
+    sd = O.prepare_state(init)
+    ost = O.adam_init(sd)
+    outs = []
+    for _ in range(2):
+        o, _ = O.train_step(sd, ost, x, eps, ocfg)
+        outs.append({k: v.detach() for k, v in o.items()})
+    xc, ec = x.cuda(), eps.cuda()
+    res = []
+    for _ in range(2):
+        y, mu, R, K, _ = _step(m, opt, xc, ec, cfg)
+        res.append((y.detach().cpu(), R.item(), K.item()))
+    torch.cuda.synchronize()
+    dev = {
+        "image": max(rel(res[i][0], outs[i]["y"]) for i in range(2)),
+        "R": max(abs(res[i][1] - outs[i]["R"].item()) / outs[i]["R"].item() for i in range(2)),
+        "K": max(abs(res[i][2] - outs[i]["K"].item()) / abs(outs[i]["K"].item()) for i in range(2)),
+    }
+    print(f"\n[{dtype}] 512x512 B=1 deviation vs oracle over 2 steps: {dev}")
+    if dtype == torch.float32:
+        assert dev["image"] < 1e-3 and dev["R"] < 1e-3 and dev["K"] < 1e-3
+    else:
+        assert dev["image"] < 5e-2 and dev["R"] < 1e-2 and dev["K"] < 1e-2
+
+
 def test_trainer_surface(tmp_path):
     cfg = fv.FaceVAEConfig.toy()
     batch = [(torch.rand(2, 3, 64, 64),) * 4 for _ in range(2)]

@@ -4,8 +4,10 @@ half the bytes of a wide coalesced stream, so reads = 2 x FETCH_SIZE.
 
     python tools/pmc_traffic.py gpurun_out/pmc_FETCH_SIZE gpurun_out/pmc_WRITE_SIZE > profiles/rN_pmc_traffic.json
 
-Reports the bench's dominant kernel (the 256->256 3x3 res conv: conv_fwd_v2 256x256 tile,
-512 workgroups at 64x64, B=32) and every kernel family's mean per dispatch.
+Reports the bench's dominant kernels -- the 256->256 3x3 res conv at 64x64, B=32, per family
+the bench's KernelTimer names (fwd and dgrad: conv3_halo_fwd2 256-co tile, 512 workgroups;
+wgrad: conv_wgrad_v2 256x256 tile, 252 workgroups) -- and every kernel family's mean per
+dispatch.
 """
 import collections
 import csv
@@ -14,8 +16,12 @@ import json
 import re
 import sys
 
-DOM = re.compile(r"conv_fwd_v2<3, 4, 2, 4, 8, 0, 64>")
-DOM_GRID = 512 * 512
+# bench family -> (kernel-name pattern, total grid size in work-items) of the res-conv launch
+DOMS = {
+    "fwd": (re.compile(r"conv3_halo_fwd2<4, 2, 4, 8, 2>"), 512 * 512),
+    "dgrad": (re.compile(r"conv3_halo_fwd2<4, 2, 4, 8, 2>"), 512 * 512),
+    "wgrad": (re.compile(r"conv_wgrad_v2<3, 256, 256, 2, 4, 64, 2, false, false>"), 252 * 512),
+}
 
 
 def rows(d):
@@ -30,14 +36,16 @@ def family(name):
 
 def collect(d, counter):
     per = collections.defaultdict(list)
-    dom = []
+    dom = collections.defaultdict(list)
     for r in rows(d):
         if r["Counter_Name"] != counter:
             continue
         v = float(r["Counter_Value"])
         per[family(r["Kernel_Name"])].append(v)
-        if DOM.search(r["Kernel_Name"]) and int(r.get("Grid_Size", 0) or 0) == DOM_GRID:
-            dom.append(v)
+        grid = int(r.get("Grid_Size", 0) or 0)
+        for fam, (pat, g) in DOMS.items():
+            if pat.search(r["Kernel_Name"]) and grid == g:
+                dom[fam].append(v)
     return per, dom
 
 
@@ -47,12 +55,13 @@ def main(fdir, wdir):
     mean = lambda v: sum(v) / len(v) if v else None
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes over bench.py --steps 2 --warmup 1",
            "correction": "bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts half of a wide stream)",
-           "dominant": None, "families": {}}
-    if fdom and wdom:
-        rd, wr = 2 * mean(fdom) * 1024, mean(wdom) * 1024
-        out["dominant"] = {"kernel": "conv_fwd_v2<3,4,2,4,8,0,64> @64x64 B=32 (res conv fwd/dgrad)",
-                           "dispatches": [len(fdom), len(wdom)], "read_bytes": rd, "write_bytes": wr,
-                           "hbm_bytes_per_launch": rd + wr}
+           "dominant": {}, "families": {}}
+    for fam, (pat, g) in DOMS.items():
+        if fdom.get(fam) and wdom.get(fam):
+            rd, wr = 2 * mean(fdom[fam]) * 1024, mean(wdom[fam]) * 1024
+            out["dominant"][fam] = {"kernel": f"{pat.pattern} grid {g} @64x64 B=32 (res conv {fam})",
+                                    "dispatches": [len(fdom[fam]), len(wdom[fam])], "read_bytes": rd,
+                                    "write_bytes": wr, "hbm_bytes_per_launch": rd + wr}
     for k in sorted(set(fper) | set(wper)):
         f, w = mean(fper.get(k, [])), mean(wper.get(k, []))
         out["families"][k] = {"dispatches": len(fper.get(k, [])),
