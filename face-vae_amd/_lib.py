@@ -57,6 +57,9 @@ _SIGS = {
     "fv_conv2d_wgrad_bias_slab_elems": (c_size_t, [D]),
     "fv_conv2d_bwd_weight": (c_int, [D, P, P, P, P, c_int, P, P, P]),
     "fv_conv2d_wgrad_reduce": (c_int, [D, P, P, P, P, P]),
+    "fv_convt_supported": (c_int, [D]),
+    "fv_convt_weight_prep": (c_int, [D, P, c_int, c_float, P, P, P, P]),
+    "fv_convt_wgrad_reduce": (c_int, [D, P, P, P, c_int, c_float, P, P, P, P]),
     "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),
     "fv_spectral_norm_fwd": (c_int, [P, c_int, c_int, P, P, P, c_int, P, P]),
     "fv_spectral_norm_bwd": (c_int, [P, P, c_int, c_int, P, P, P, P, P, P]),

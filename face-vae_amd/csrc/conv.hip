@@ -3514,3 +3514,175 @@ int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float
 }
 
 }  // extern "C"
+
+// ----------------------------------------------------------------------------------------
+// ConvTranspose2dELR, kernel 4 / stride 2 / padding 1 (models_utils.py:404-516).
+// out[o] = sum_j x[j] W[ci][co][o + 1 - 2j]: output phase pa (o = 2i + pa) reads the two
+// low-res rows {i - 1, i} (pa = 0) or {i, i + 1} (pa = 1) -- the same 2x2 window per phase as
+// the sub-pixel decomposition of nearest-x2 + 3x3 (weight_prep_subpix_kernel), with tap
+// t = 3 - pa - 2 r' selected instead of folded.  So the transposed conv runs on the
+// upsample-conv kernels unchanged (descriptor upsample = 1, ksize = 3, h/w = output size):
+// forward = the sub-pixel phases, data gradient = the low-res stride-2 4x4 conv over dy
+// (wt[ci][(tr*4 + tc)*cin_t + co] = Weff[ci][co][tr][tc]), weight gradient = the per-phase
+// 2x2 slabs, mapped back to 4x4 taps here.  Weff = gain * W (* 1/max(||W[:, co]||, 1e-12)
+// with norm == "demod", F.normalize over dims [0, 2, 3]: models_utils.py:461-470).
+// ----------------------------------------------------------------------------------------
+namespace {
+
+// one wave per output channel: inv[co] = 1 / max(||W[:, co, :, :]||_2, 1e-12)
+__global__ void convt_norm_kernel(const float* __restrict__ w, int cin, int cout, float* inv) {
+  const int co = blockIdx.x, l = threadIdx.x;
+  float s = 0.f;
+  for (int e = l; e < cin * 16; e += 64) {
+    const float v = w[((long)(e >> 4) * cout + co) * 16 + (e & 15)];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if (l == 0) inv[co] = 1.f / fmaxf(sqrtf(s), 1e-12f);
+}
+
+__device__ __forceinline__ float convt_scale(const float* inv, int co, float gain) {
+  return inv ? gain * inv[co] : gain;
+}
+
+// wk [4][rows][Kpad] (k = (r'*2 + s')*cin + ci) and wt [rows_t][16*cin_t] (k = (tr*4 + tc)*cin_t + co)
+__global__ void convt_weight_prep_kernel(const float* __restrict__ w, const float* __restrict__ inv, float gain,
+                                         bf16* wk, int rows, int Kpad, int lgCin, bf16* wt, int rows_t,
+                                         int lgCt, int cin_valid, int cout) {
+  const long nk = wk ? 4L * rows * Kpad : 0;
+  const long nt = wt ? (long)rows_t * (16L << lgCt) : 0;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < nk + nt; e += (long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (e < nk) {
+      const long per = (long)rows * Kpad;
+      const int ph = (int)(e / per);
+      const long e2 = e - ph * per;
+      const int co = (int)(e2 / Kpad), k = (int)(e2 - (long)co * Kpad);
+      const int tap = k >> lgCin, ci = k & ((1 << lgCin) - 1);
+      if (tap < 4 && co < cout && ci < cin_valid) {
+        const int tr = 3 - (ph >> 1) - 2 * (tap >> 1), tc = 3 - (ph & 1) - 2 * (tap & 1);
+        v = w[((long)ci * cout + co) * 16 + tr * 4 + tc] * convt_scale(inv, co, gain);
+      }
+      wk[e] = (bf16)v;
+    } else {
+      const long e2 = e - nk;
+      const int Kt = 16 << lgCt;
+      const int ci = (int)(e2 / Kt), k = (int)(e2 - (long)ci * Kt);
+      const int tap = k >> lgCt, co = k & ((1 << lgCt) - 1);
+      if (ci < cin_valid && co < cout)
+        v = w[((long)ci * cout + co) * 16 + tap] * convt_scale(inv, co, gain);
+      wt[e2] = (bf16)v;
+    }
+  }
+}
+
+// phase slabs [4][nsplit][CW][KW] (rows co, k = ((r'*2 + s') << lgCin) + ci) -> G [ci][co][4][4]
+// = dL/dWeff, one wave per 64 outputs, 4 lanes per output summing interleaved splits; + db.
+__global__ void convt_wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab, float* dw,
+                                          float* db, int nsplit, int CW, int KW, int cout, int cin_valid, int lgCin,
+                                          int nb_main) {
+  const int sg = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __shared__ float red[4][64];
+  float g = 0.f;
+  long dst = -1;
+  if ((int)blockIdx.x < nb_main) {
+    const long e = (long)blockIdx.x * 64 + l;
+    if (e < (long)cin_valid * cout * 16) {
+      dst = e;
+      const int t = (int)(e & 15), co = (int)((e >> 4) % cout), ci = (int)((e >> 4) / cout);
+      const int tr = t >> 2, tc = t & 3;
+      const int ph = (1 - (tr & 1)) * 2 + (1 - (tc & 1));
+      const int tap = (tr < 2) * 2 + (tc < 2);
+      for (int sp = sg; sp < nsplit; sp += 4)
+        g += slab[((long)(ph * nsplit + sp) * CW + co) * KW + ((tap << lgCin) + ci)];
+    }
+  } else {
+    const int co = ((int)blockIdx.x - nb_main) * 64 + l;
+    if (co < cout) {
+      dst = co;
+      for (int t = sg; t < 4 * nsplit; t += 4) g += bslab[(long)t * CW + co];
+    }
+  }
+  red[sg][l] = g;
+  __syncthreads();
+  if (sg == 0 && dst >= 0) {
+    const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    if ((int)blockIdx.x < nb_main) dw[dst] = v;
+    else db[dst] = v;
+  }
+}
+
+// in place, one wave per co: G = dL/dWeff -> dL/dW.  demod: Wn = W * inv,
+// dW = gain * inv * (G - Wn <Wn, G>) (the max(norm, eps) clamp: dW = gain * inv * G); else gain * G.
+__global__ void convt_weight_bwd_kernel(const float* __restrict__ w, const float* __restrict__ inv, float gain,
+                                        float* g, int cin, int cout) {
+  const int co = blockIdx.x, l = threadIdx.x;
+  const float iv = inv ? inv[co] : 1.f;
+  float dot = 0.f;
+  if (inv && iv < 1e12f) {
+    for (int e = l; e < cin * 16; e += 64) {
+      const long a = ((long)(e >> 4) * cout + co) * 16 + (e & 15);
+      dot += w[a] * iv * g[a];
+    }
+    dot = wave_sum(dot);
+  }
+  for (int e = l; e < cin * 16; e += 64) {
+    const long a = ((long)(e >> 4) * cout + co) * 16 + (e & 15);
+    g[a] = gain * iv * (g[a] - (inv ? w[a] * iv * dot : 0.f));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int fv_convt_supported(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  if (!d->upsample || d->ksize != 3 || d->dtype != FV_BF16 || d->pro_act || d->epi_sigmoid || d->out_nchw_f32 ||
+      pad_pow2_8(d->cout) != d->cout || d->ldy != d->cout)
+    return 0;
+  return (use_subpix(d) && use_dgrad_lowres(d) && plan_wgrad(d).sub) ? 1 : 0;
+}
+
+int fv_convt_weight_prep(const fv_conv_desc* d, const float* w, int demod, float gain, float* inv, void* wk,
+                         void* wt, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fv_convt_supported(d), "conv_transpose2d k4 s2 p1: unsupported descriptor (cin=%d cout=%d %dx%d)",
+             d->cin, d->cout, d->h, d->w);
+  FV_REQUIRE(w && (!demod || inv), "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (demod) {
+    hipLaunchKernelGGL(convt_norm_kernel, dim3(d->cout), dim3(64), 0, s, w, d->cin_valid, d->cout, inv);
+    if ((st = fv_check_launch("convt_norm"))) return st;
+  }
+  const FwdTile tk = fwd_tile(d->cout), tt = fwd_tile(d->cin);
+  const int cin_t = pad_pow2_8(d->cout);
+  const int rows = fv_cdiv(d->cout, tk.bn) * tk.bn, Kp = kpad_of(2, d->cin);
+  const int rows_t = fv_cdiv(d->cin, tt.bn) * tt.bn;
+  const long tot = (wk ? 4L * rows * Kp : 0) + (wt ? (long)rows_t * 16 * cin_t : 0);
+  const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
+  hipLaunchKernelGGL(convt_weight_prep_kernel, dim3(nb), dim3(256), 0, s, w, demod ? inv : nullptr, gain, (bf16*)wk,
+                     rows, Kp, fv_ilog2(d->cin), (bf16*)wt, rows_t, fv_ilog2(cin_t), d->cin_valid, d->cout);
+  return fv_check_launch("convt_weight_prep");
+}
+
+int fv_convt_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab, const float* w,
+                          int demod, float gain, const float* inv, float* dw, float* db, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fv_convt_supported(d), "conv_transpose2d k4 s2 p1: unsupported descriptor");
+  FV_REQUIRE(slab && w && dw && (!demod || inv) && (!db || bias_slab), "null pointer");
+  const WgPlan t = plan_wgrad(d);
+  hipStream_t s = (hipStream_t)stream;
+  const int nb_main = fv_cdiv((long)d->cout * d->cin_valid * 16, 64);
+  const int nb_bias = db ? fv_cdiv(d->cout, 64) : 0;
+  hipLaunchKernelGGL(convt_wgrad_reduce_kernel, dim3(nb_main + nb_bias), dim3(256), 0, s, slab, bias_slab, dw, db,
+                     t.nsplit, t.CW, t.KW, d->cout, d->cin_valid, fv_ilog2(d->cin), nb_main);
+  if ((st = fv_check_launch("convt_wgrad_reduce"))) return st;
+  hipLaunchKernelGGL(convt_weight_bwd_kernel, dim3(d->cout), dim3(64), 0, s, w, demod ? inv : nullptr, gain, dw,
+                     d->cin_valid, d->cout);
+  return fv_check_launch("convt_weight_bwd");
+}
+
+}  // extern "C"

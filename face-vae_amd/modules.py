@@ -217,3 +217,72 @@ class Conv2d(_Conv):
 
     def forward(self, x, sigmoid=False):
         return ops.ConvFn.apply(x, self.weight, self.bias, self, self.compute_dtype(), int(sigmoid))
+
+
+class ConvTranspose2dELR(nn.Module):
+    """Drop-in for `ConvTranspose2dELR` (models_utils.py:404-516): a transposed conv with an
+    equalised-learning-rate gain and optional per-output-channel weight demodulation, same
+    constructor, parameter names (`weight` [inch, outch, k, k], `bias`) and init RNG draw
+    (`blockinit(randn(inch, outch, k//s, k//s), s)`, models_utils.py:283-288, 435-436).
+
+    Computed by the HIP sub-pixel kernels for kernel_size 4, stride 2, padding 1 (the
+    upsampling configuration), bf16 operands / fp32 accumulation; other geometries and the
+    per-sample affine modulation (wsize > 0 with a style input) raise.  The untied bias (ub)
+    and the optional activation module are applied after the kernel, as the reference does
+    (models_utils.py:507-514)."""
+
+    def __init__(self, inch, outch, kernel_size, stride, padding, wsize=0, affinelrmult=1., norm=None, ub=None,
+                 act=None):
+        super().__init__()
+        self.inch, self.outch = inch, outch
+        self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
+        self.wsize, self.norm, self.ub, self.act = wsize, norm, ub, act
+        if wsize > 0:
+            raise NotImplementedError("ConvTranspose2dELR: per-sample affine modulation (wsize > 0) is not on the "
+                                      "FaceVAE path (SURVEY.md §8a-a15)")
+        # models_utils.py:420-433: gain from the activation, then the init gain
+        try:
+            if isinstance(act, nn.LeakyReLU):
+                actgain = nn.init.calculate_gain("leaky_relu", act.negative_slope)
+            elif isinstance(act, nn.ReLU):
+                actgain = nn.init.calculate_gain("relu")
+            else:
+                actgain = nn.init.calculate_gain(act)
+        except Exception:
+            actgain = 1.
+        fan_in = inch * (kernel_size ** 2 / (stride ** 2))
+        initgain = stride if norm == "demod" else 1. / math.sqrt(fan_in)
+        self.weightgain = actgain * initgain
+        k = kernel_size // stride
+        w = torch.randn(inch, outch, k, k)
+        self.weight = nn.Parameter(w.repeat_interleave(stride, dim=2).repeat_interleave(stride, dim=3).contiguous())
+        self.bias = nn.Parameter(torch.zeros(outch, ub[0], ub[1]) if ub is not None else torch.zeros(outch))
+        self.affine = None
+        self.fused = False
+
+    def extra_repr(self):
+        return (f"inch={self.inch}, outch={self.outch}, kernel_size={self.kernel_size}, stride={self.stride}, "
+                f"padding={self.padding}, wsize={self.wsize}, norm={self.norm}, ub={self.ub}, act={self.act}")
+
+    def fuse(self):
+        """Bake gain (and demodulation) into `weight` (models_utils.py:474-478)."""
+        with torch.no_grad():
+            w = self.weight
+            if self.norm == "demod":
+                w = F.normalize(w, dim=[0, 2, 3])
+            self.weight.data = (w * self.weightgain).contiguous()
+        self.fused = True
+
+    def forward(self, x, w=None):
+        if (self.kernel_size, self.stride, self.padding) != (4, 2, 1):
+            raise NotImplementedError("ConvTranspose2dELR: only kernel_size=4, stride=2, padding=1 runs on the "
+                                      "HIP kernels")
+        demod = self.norm == "demod" and not self.fused
+        gain = 1.0 if self.fused else self.weightgain
+        tied = self.bias.dim() == 1
+        out = ops.ConvTranspose2dFn.apply(x, self.weight, self.bias if tied else None, demod, gain)
+        if not tied:
+            out = out + self.bias[None].to(out.dtype)
+        if self.act is not None:
+            out = self.act(out)
+        return out

@@ -658,3 +658,54 @@ def reparameterise(h, eps, dtype):
     mu, ls, z = ReparamFn.apply(h, eps, dtype, holder)
     mu._fv_kl = (ls, holder["kl"], mu._version, ls._version)
     return mu, ls, z
+
+
+class ConvTranspose2dFn(torch.autograd.Function):
+    """F.conv_transpose2d(x, gain * [demod-normalised] W, stride=2, padding=1) + bias with a
+    4x4 kernel (ConvTranspose2dELR.getweight/forward, models_utils.py:454-505), on the
+    sub-pixel upsample-conv kernels (include/facevae.h, "transposed conv").  bf16 only."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, demod, gain):
+        dtype = torch.bfloat16
+        xb, cin_pad = to_nhwc(x, dtype)
+        N, inch, Hi, Wi = x.shape
+        outch = weight.shape[1]
+        if weight.dtype != F32 or not weight.is_contiguous():
+            raise RuntimeError("conv_transpose2d weights must be contiguous fp32")
+        d = desc(dtype, N, 2 * Hi, 2 * Wi, cin_pad, inch, outch, outch, 3, ups=1)
+        if not query("fv_convt_supported", ctypes.byref(d)):
+            raise RuntimeError(f"conv_transpose2d (k4 s2 p1): unsupported shape in={tuple(x.shape)} outch={outch} "
+                               "(needs inch > 32, outch a power of two >= 64, input height and width powers of two, width >= 64)")
+        dev = x.device
+        inv = torch.empty(outch, dtype=F32, device=dev)
+        wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, dev)
+        wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, dev) if ctx.needs_input_grad[0] else None
+        call("fv_convt_weight_prep", ctypes.byref(d), ptr(weight), int(demod), float(gain), ptr(inv), ptr(wk),
+             ptr(wt), stream())
+        y = torch.empty((N, outch, 2 * Hi, 2 * Wi), dtype=dtype, device=dev, memory_format=CL)
+        call("fv_conv2d_fwd", ctypes.byref(d), ptr(xb), ptr(wk), ptr(bias), None, None, None, ptr(y), None, stream())
+        ctx.d, ctx.demod, ctx.gain, ctx.wt, ctx.has_bias = d, int(demod), float(gain), wt, bias is not None
+        ctx.save_for_backward(x, xb, weight, inv)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xb, weight, inv = ctx.saved_tensors
+        d = ctx.d
+        dev = dy.device
+        dy = grad_in(dy, torch.bfloat16)
+        slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
+        bslab = _empty(query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), F32, dev)
+        call("fv_conv2d_bwd_weight", ctypes.byref(d), ptr(xb), None, None, ptr(dy), d.cout, ptr(slab), ptr(bslab),
+             stream())
+        dw = torch.empty_like(weight)
+        db = torch.empty(d.cout, dtype=F32, device=dev) if ctx.has_bias else None
+        call("fv_convt_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(weight), ctx.demod, ctx.gain,
+             ptr(inv), ptr(dw), ptr(db), stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dxb = torch.empty((d.n, d.cin, d.h // 2, d.w // 2), dtype=dy.dtype, device=dev, memory_format=CL)
+            call("fv_conv2d_bwd_data", ctypes.byref(d), ptr(dy), d.cout, ptr(ctx.wt), ptr(dxb), stream())
+            dx = from_nhwc(dxb, x)
+        return dx, dw, db, None, None

@@ -114,6 +114,25 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
 int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab,
                            float* dw_param, float* db, void* stream);
 
+/* ------------------------------------------- transposed conv (k4, s2, p1) ---- */
+/* ConvTranspose2dELR (models_utils.py:404-516; F.conv_transpose2d at :497-498) with
+ * kernel 4, stride 2, padding 1, run as the sub-pixel phases of an upsample descriptor:
+ * d->upsample = 1, d->ksize = 3, d->h/w = OUTPUT size, cin/cout = the module's inch/outch.
+ * Forward = fv_conv2d_fwd(d, x, wk, bias, ...); data gradient = fv_conv2d_bwd_data(d, dy,
+ * ldy, wt, dx) (dx at the input resolution); weight gradient = fv_conv2d_bwd_weight(d, ...)
+ * then fv_convt_wgrad_reduce.  w is the module parameter [cin][cout][4][4] fp32; the
+ * effective weight is gain * w, normalised per output channel over dims [0,2,3]
+ * (F.normalize, eps 1e-12: models_utils.py:461-470) when demod; inv [cout] receives
+ * 1/max(norm, eps) and is read back by the weight-gradient reduce.  bf16 only. */
+int fv_convt_supported(const fv_conv_desc* d);
+int fv_convt_weight_prep(const fv_conv_desc* d, const float* w, int demod, float gain, float* inv,
+                         void* wk, void* wt, void* stream);
+/* slabs of fv_conv2d_bwd_weight(d, ...) -> dw [cin][cout][4][4] = dL/dw (through gain and
+ * demod) and db [cout] (may be NULL). */
+int fv_convt_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab,
+                          const float* w, int demod, float gain, const float* inv, float* dw,
+                          float* db, void* stream);
+
 /* ------------------------------------------------------------- spectral norm ---- */
 size_t fv_spectral_norm_ws_bytes(int rows, int cols);
 /* one power iteration (u, v updated in place) when power_iter, then sigma = u.(W v) */

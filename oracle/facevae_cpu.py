@@ -310,3 +310,32 @@ def flops_per_image(cfg: OracleConfig) -> Tuple[float, float]:
             first = f
     del res
     return fwd, 3 * fwd - first
+
+
+# ----------------------------------------------------------------------------------------
+# ConvTranspose2dELR (models_utils.py:404-516) -- SURVEY.md §8a-a15 (off the FaceVAE graph)
+# ----------------------------------------------------------------------------------------
+
+def convt_elr_gain(inch, kernel_size, stride, norm, act_slope=None):
+    """weightgain of models_utils.py:420-433 (act: None, ReLU (slope 0) or LeakyReLU)."""
+    if act_slope is None:
+        actgain = 1.0
+    elif act_slope == 0.0:
+        actgain = math.sqrt(2.0)                                    # calculate_gain("relu")
+    else:
+        actgain = math.sqrt(2.0 / (1 + act_slope ** 2))             # calculate_gain("leaky_relu", slope)
+    fan_in = inch * (kernel_size ** 2 / (stride ** 2))
+    initgain = stride if norm == "demod" else 1.0 / math.sqrt(fan_in)
+    return actgain * initgain
+
+
+def convt_elr(x, weight, bias, stride, padding, norm, gain, act_slope=None):
+    """getweight (models_utils.py:454-472) + forward without modulation (:480-514):
+    F.normalize over dims [0, 2, 3] when demod, times gain; conv_transpose2d; + bias (tied
+    [outch] or untied [outch, H, W]); optional ReLU / LeakyReLU."""
+    w = F.normalize(weight, dim=[0, 2, 3]) if norm == "demod" else weight
+    out = F.conv_transpose2d(x, w * gain, None, stride=stride, padding=padding)
+    out = out + (bias[None, :, None, None] if bias.dim() == 1 else bias[None])
+    if act_slope is not None:
+        out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
+    return out

@@ -273,3 +273,52 @@ def test_error_is_reported_not_aborted():
     d = ops.desc(torch.float32, 1, 8, 8, 12, 12, 16, 16, 3)    # cin 12 is not a power of two
     with pytest.raises(L.FaceVAELibError, match="power of two"):
         L.call("fv_conv2d_fwd", ctypes.byref(d), 1, 1, None, None, None, None, 1, None, L.stream())
+
+
+@pytest.mark.parametrize("case", ["demod", "plain_untied", "demod_128to64"])
+def test_conv_transpose_elr(case):
+    """ConvTranspose2dELR k4 s2 p1 (models_utils.py:404-516) on the sub-pixel kernels vs the
+    oracle restatement (oracle.convt_elr, pinned to the reference by
+    tests/golden/convt_elr.pt) in fp32 on the CPU: output, input / weight / bias gradients at
+    bf16 tolerance.  No activation module here: a ReLU / LeakyReLU (a torch module applied
+    after the kernel, as in the reference) flips its mask on ~0.2 % of near-zero outputs
+    between a bf16 and an fp32 forward, which alone moves the gradients by ~3 %."""
+    from oracle import facevae_cpu as O      # checker only
+    inch, outch, norm, ub, slope, hw = {
+        "demod": (64, 64, "demod", None, None, (64, 64)),
+        "plain_untied": (64, 128, None, (128, 128), None, (64, 64)),
+        "demod_128to64": (128, 64, "demod", None, None, (32, 128)),
+    }[case]
+    act = None if slope is None else (torch.nn.ReLU() if slope == 0.0 else torch.nn.LeakyReLU(slope))
+    torch.manual_seed(0)
+    m = fv.ConvTranspose2dELR(inch, outch, 4, 2, 1, norm=norm, ub=ub, act=act)
+    with torch.no_grad():
+        m.bias.normal_(generator=gen(5))
+    if case == "demod":
+        gold = torch.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                                     "convt_elr.pt"), weights_only=True)["gpu_init"]
+        assert abs(m.weight.double().sum().item() - gold["sum"].item()) < 1e-9   # reference init
+    w0, b0 = m.weight.detach().clone(), m.bias.detach().clone()
+    x = torch.randn(2, inch, *hw, generator=gen(6))
+    g = torch.randn(2, outch, 2 * hw[0], 2 * hw[1], generator=gen(7))
+    m = m.cuda()
+    xc = x.cuda().requires_grad_(True)
+    y = m(xc)
+    y.float().backward(g.cuda())
+    torch.cuda.synchronize()
+    wr, br, xr = w0.clone().requires_grad_(True), b0.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    yr = O.convt_elr(xr, wr, br, 2, 1, norm, m.weightgain, slope)
+    yr.backward(g)
+    dev = {"y": rel(y.float(), yr.detach()), "dx": rel(xc.grad, xr.grad), "dw": rel(m.weight.grad, wr.grad),
+           "db": rel(m.bias.grad, br.grad)}
+    print(f"\n[convT {case}] rel-L2 vs oracle: {dev}")
+    assert max(dev.values()) < TOL[torch.bfloat16], dev
+
+
+def test_conv_transpose_elr_rejects_unsupported():
+    m = fv.ConvTranspose2dELR(16, 24, 4, 2, 1).cuda()
+    with pytest.raises(RuntimeError, match="unsupported"):
+        m(torch.randn(1, 16, 64, 64, device="cuda"))
+    m2 = fv.ConvTranspose2dELR(16, 64, 3, 1, 1).cuda()
+    with pytest.raises(NotImplementedError):
+        m2(torch.randn(1, 16, 64, 64, device="cuda"))

@@ -144,3 +144,47 @@ def test_block_cases(name):
     for k, v in c["state"].items():
         if v.is_floating_point():
             assert rel(sdp["m." + k].detach(), v) < 1e-6, k
+
+
+CONVT_CASES = {
+    "demod_leaky": (6, 8, 4, 2, 1, "demod", None, 0.2),
+    "plain_untied": (4, 8, 4, 2, 1, None, (10, 12), None),
+    "demod_relu_k3s1": (5, 8, 3, 1, 1, "demod", None, 0.0),
+}
+
+
+@pytest.mark.parametrize("name", list(CONVT_CASES))
+def test_convt_elr_oracle_matches_reference(name):
+    """ConvTranspose2dELR restatement (oracle.convt_elr) vs the reference module's forward /
+    backward (tests/golden/make_golden_convt.py)."""
+    g = load("convt_elr.pt")[name]
+    inch, outch, k, s, p, norm, ub, slope = CONVT_CASES[name]
+    gain = O.convt_elr_gain(inch, k, s, norm, slope)
+    assert abs(gain - g["weightgain"].item()) < 1e-12
+    w = g["weight"].clone().requires_grad_(True)
+    b = g["bias"].clone().requires_grad_(True)
+    x = g["x"].clone().requires_grad_(True)
+    y = O.convt_elr(x, w, b, s, p, norm, gain, slope)
+    y.backward(g["g"])
+    assert rel(y.detach(), g["y"]) < 1e-6
+    assert rel(x.grad, g["dx"]) < 1e-6
+    assert rel(w.grad, g["dweight"]) < 1e-5
+    assert rel(b.grad, g["dbias"]) < 1e-6
+
+
+def test_convt_elr_module_init_matches_reference():
+    """The product module draws the reference's init (blockinit of one randn) and gain."""
+    import fvamd  # noqa: F401
+    import facevae_amd as fv
+    gold = load("convt_elr.pt")
+    for i, (name, (inch, outch, k, s, p, norm, ub, slope)) in enumerate(CONVT_CASES.items()):
+        act = None if slope is None else (torch.nn.ReLU() if slope == 0.0 else torch.nn.LeakyReLU(slope))
+        torch.manual_seed(100 + i)
+        m = fv.ConvTranspose2dELR(inch, outch, k, s, p, norm=norm, ub=ub, act=act)
+        assert torch.equal(m.weight.detach(), gold[name]["weight"]), name
+        assert m.bias.shape == gold[name]["bias"].shape
+        assert abs(m.weightgain - gold[name]["weightgain"].item()) < 1e-12
+    torch.manual_seed(0)
+    m = fv.ConvTranspose2dELR(64, 64, 4, 2, 1, norm="demod")
+    assert torch.equal(m.weight.detach()[0, 0], gold["gpu_init"]["weight_00"])
+    assert abs(m.weight.double().sum().item() - gold["gpu_init"]["sum"].item()) < 1e-9
