@@ -356,8 +356,12 @@ def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, ne
         red = torch.empty(2 * C, dtype=F64, device=dev)
         call("fv_bn_act_bwd_reduce", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
              ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), ptr(red), ptr(ws), stream())
-        _sync(red, comm)
+        # dgamma / dbeta from this rank's sums (torch SyncBatchNorm: batch_norm_backward_reduce
+        # is local, only sum_dy / sum_dy_xmu are all-reduced -- _functions.py); the data-parallel
+        # gradient average then yields the global-batch value.  dx uses the global sums.
         call("fv_bn_bwd_finalize", ptr(red), C, int(r.count), ptr(dg), ptr(dbt), ptr(k), stream())
+        _sync(red, comm)
+        call("fv_bn_bwd_finalize", ptr(red), C, int(r.count), None, None, ptr(k), stream())
     dx = None
     if need_dx:
         dx = torch.empty((N, C, H, W), dtype=y.dtype, device=dev, memory_format=CL)
