@@ -40,8 +40,22 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-syncbn", action="store_true", help="per-rank BN statistics (labelled)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     return ap.parse_args()
+
+
+def usable_cores():
+    """(cores this process can run on, os.cpu_count()): the CPU affinity set capped by the
+    cgroup CPU quota (cpu.max), which is what a job on the GPU box actually gets -- there
+    os.cpu_count() shows the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return n, os.cpu_count()
 
 
 def conv_launch_flops(d):
@@ -49,46 +63,67 @@ def conv_launch_flops(d):
     return 2.0 * d.n * d.h * d.w * d.cout * d.cin_valid * d.ksize * d.ksize
 
 
-def cpu_baseline(args, cfg):
-    """The oracle (fp32 torch-CPU restatement of the reference step) on a bounded sample."""
+def cpu_baseline(args, cfg, B):
+    """The oracle (fp32 torch-CPU restatement of the reference step, math identical to the
+    reference trainer) at the per-GPU shape (B images at cfg.H), on every core this process
+    may use: one warm-up step at batch 2, then whole B-image steps until cpu_seconds."""
     from oracle import facevae_cpu as O   # checker / baseline only
-    torch.set_num_threads(args.cpu_threads)
+    cores, ncpu = usable_cores()
+    threads = args.cpu_threads or cores
+    torch.set_num_threads(threads)
     ocfg = O.OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent, n_res=cfg.n_res,
                           up_seq=cfg.up_seq)
-    B = 2
     sd = O.prepare_state(O.init_state(ocfg, 0))
     opt = O.adam_init(sd)
-    x = torch.rand(B, 3, cfg.H, cfg.H, generator=torch.Generator().manual_seed(1234))
-    eps = torch.randn(B, cfg.latent, cfg.latent_hw, cfg.latent_hw, generator=torch.Generator().manual_seed(1235))
-    O.train_step(sd, opt, x, eps, ocfg)                          # warm-up
+
+    def inputs(b):
+        x = torch.rand(b, 3, cfg.H, cfg.H, generator=torch.Generator().manual_seed(1234))
+        eps = torch.randn(b, cfg.latent, cfg.latent_hw, cfg.latent_hw, generator=torch.Generator().manual_seed(1235))
+        return x, eps
+    O.train_step(sd, opt, *inputs(2), ocfg)                      # warm-up
+    x, eps = inputs(B)
     n, t0 = 0, time.perf_counter()
     while True:
         O.train_step(sd, opt, x, eps, ocfg)
         n += 1
         dt = time.perf_counter() - t0
-        if dt >= args.cpu_seconds or n >= 50:
+        if dt >= args.cpu_seconds or n >= 20:
             break
     return {"value": round(n * B / dt, 4), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle fp32 step at {cfg.H}x{cfg.H}, batch {B}, {n} timed steps ({dt:.1f} s) after 1 warm-up"}
+            "os_cpu_count": ncpu, "usable_cores": cores,
+            "sample": f"oracle fp32 step at {cfg.H}x{cfg.H}, batch {B} (the per-GPU shape), {n} timed step(s) "
+                      f"({dt:.1f} s) after 1 warm-up step at batch 2; {torch.get_num_threads()} threads = the cores "
+                      f"this process may use (affinity {len(os.sched_getaffinity(0))} CPUs capped by the cgroup "
+                      f"quota; os.cpu_count() = {ncpu} is the whole machine)"}
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc.json")
 
 
-def pmc_traffic(cfg, B, dtype, fam, avg_ms):
-    """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (tools/gpu_pmc.sh -> profiles/r1_pmc_traffic.json; (2 x FETCH_SIZE + WRITE_SIZE) KiB,
-    the gfx950 correction of MI355X_MICROARCH.md).  Measured on the default 256x256, B=32
-    bf16 configuration only; other configurations report null."""
+def pmc_counters(cfg, B, dtype, fam, avg_ms):
+    """Counter figures of the dominant kernel from the committed PMC passes (tools/gpu_pmc.sh
+    -> profiles/r2_pmc.json, tools/pmc_collect.py): HBM bytes per launch ((2 x FETCH_SIZE +
+    WRITE_SIZE) KiB, the gfx950 correction of MI355X_MICROARCH.md), the MFMA busy fraction
+    (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)) and the effective clock.
+    Measured on the default 256x256, B=32 bf16 configuration only; others report null."""
     if not (cfg.H == 256 and B == 32 and dtype == torch.bfloat16 and os.path.exists(PMC_FILE)):
         return {}
-    dom = (json.load(open(PMC_FILE)).get("dominant") or {}).get(fam)
+    d = json.load(open(PMC_FILE))
+    dom = (d.get("dominant") or {}).get(fam)
     if not dom:
         return {}
-    t = dom["hbm_bytes_per_launch"]
-    return {"traffic": round(t), "traffic_unit": f"bytes/launch (PMC, profiles/r1_pmc_traffic.json, {dom['kernel']})",
-            "traffic_gbs_at_avg": round(t / (avg_ms * 1e-3) / 1e9, 1),
-            "algorithmic_bytes": 2 * (B * cfg.latent_hw ** 2 * cfg.up_seq[0] * 2) + cfg.up_seq[0] ** 2 * 9 * 2}
+    out = {"pmc_source": "profiles/r2_pmc.json (" + dom["kernel"] + ")"}
+    if "hbm_bytes_per_launch" in dom:
+        t = dom["hbm_bytes_per_launch"]
+        out.update({"traffic": round(t), "traffic_unit": "bytes/launch (PMC)",
+                    "traffic_gbs_at_avg": round(t / (avg_ms * 1e-3) / 1e9, 1),
+                    "algorithmic_bytes": 2 * (B * cfg.latent_hw ** 2 * cfg.up_seq[0] * 2) + cfg.up_seq[0] ** 2 * 9 * 2})
+    if "mfma_busy_frac" in dom:
+        out.update({"mfma_busy_counter": round(dom["mfma_busy_frac"], 4),
+                    "eff_clock_ghz": round(dom["eff_clock_ghz"], 3) if dom.get("eff_clock_ghz") else None,
+                    "mfma_busy_counter_step": round(d["step"]["mfma_busy_frac_all_kernels"], 4)
+                    if d.get("step") else None})
+    return out
 
 
 def main():
@@ -167,7 +202,7 @@ def main():
                 "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "avg_ms": round(fam[dom], 4), "flop_per_launch": f_launch, "traffic": None,
                 "families_avg_ms": {k: round(v, 4) for k, v in fam.items()}}
-        roof.update(pmc_traffic(cfg, B, dtype, dom, fam[dom]))
+        roof.update(pmc_counters(cfg, B, dtype, dom, fam[dom]))
     from oracle.facevae_cpu import OracleConfig, flops_per_image
     _, f_img = flops_per_image(OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent,
                                             n_res=cfg.n_res, up_seq=cfg.up_seq))
@@ -188,7 +223,7 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(args, cfg)
+        out["cpu_baseline"] = cpu_baseline(args, cfg, B)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

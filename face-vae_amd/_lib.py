@@ -11,7 +11,7 @@ from ctypes import POINTER, c_float, c_int, c_long, c_size_t, c_void_p
 
 import torch  # noqa: F401  (must be imported first: the HIP runtime is shared with torch)
 
-_HERE = os.path.dirname(os.path.abspath(__file__))
+_HERE = os.path.dirname(os.path.realpath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfacevae.so")
 
 FV_F32, FV_BF16, FV_F64 = 0, 1, 2
@@ -81,6 +81,7 @@ _SIGS = {
     "fv_bn_act_bwd_reduce": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_float,
                                      c_int, P, P, P]),
     "fv_bn_bwd_finalize": (c_int, [P, c_int, c_long, P, P, P, P]),
+    "fv_bn_bwd_finalize_dev": (c_int, [P, c_int, P, P, P, P, P]),
     "fv_bn_act_bwd_apply": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_float,
                                     c_int, P, P, P, P]),
     "fv_nchw_to_nhwc": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),

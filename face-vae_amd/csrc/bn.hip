@@ -334,15 +334,21 @@ __global__ void act_bwd_reduce_kernel(const T* __restrict__ dout, const T* __res
   }
 }
 
-__global__ void bwd_finalize_kernel(const double* red, int C, double count, float* dgamma, float* dbeta,
-                                    float* k) {
+// cnt (optional): per-channel element count on the device (row 0 of the all-reduced [3][C]
+// statistics record: the global count even with uneven per-rank batches); k may be NULL
+// (dgamma / dbeta only)
+__global__ void bwd_finalize_kernel(const double* red, int C, double count, const double* cnt, float* dgamma,
+                                    float* dbeta, float* k) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const double sg = red[c], sgy = red[C + c];
   if (dbeta) dbeta[c] = (float)sg;
   if (dgamma) dgamma[c] = (float)sgy;
-  k[c] = (float)(sg / count);
-  k[C + c] = (float)(sgy / count);
+  if (k) {
+    const double n = cnt ? cnt[c] : count;
+    k[c] = (float)(sg / n);
+    k[C + c] = (float)(sgy / n);
+  }
 }
 
 // single-process form: sum the level-1 records [split][2][C] and finalize (mapping of
@@ -589,10 +595,18 @@ int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, in
 
 int fv_bn_bwd_finalize(const double* red, int c, long count, float* dgamma, float* dbeta, float* k,
                        void* stream) {
-  FV_REQUIRE(red && k && count > 0, "bad args");
+  FV_REQUIRE(red && (k || dgamma || dbeta) && (!k || count > 0), "bad args");
   hipLaunchKernelGGL(bwd_finalize_kernel, dim3(fv_cdiv(c, NTH)), dim3(NTH), 0, (hipStream_t)stream, red, c,
-                     (double)count, dgamma, dbeta, k);
+                     (double)count, nullptr, dgamma, dbeta, k);
   return fv_check_launch("bn_bwd_finalize");
+}
+
+int fv_bn_bwd_finalize_dev(const double* red, int c, const double* count, float* dgamma, float* dbeta, float* k,
+                           void* stream) {
+  FV_REQUIRE(red && count && (k || dgamma || dbeta), "bad args");
+  hipLaunchKernelGGL(bwd_finalize_kernel, dim3(fv_cdiv(c, NTH)), dim3(NTH), 0, (hipStream_t)stream, red, c, 0.0,
+                     count, dgamma, dbeta, k);
+  return fv_check_launch("bn_bwd_finalize_dev");
 }
 
 int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h, int w, int c, int ldc,

@@ -1,14 +1,29 @@
-"""Data-parallel runtime: one process per GPU, RCCL over xGMI (replaces distributed.py:24-31's
-init_process_group("nccl") and the DDP + SyncBatchNorm wrapping of logger.py:54-58).
+"""Data-parallel runtime: one process per GPU, RCCL over xGMI (replaces distributed.py:9-31's
+init_seeds / init_process_group("nccl") and the DDP + SyncBatchNorm wrapping of
+logger.py:54-58).
 
-* `init_dist(local_rank, world_size)` — torch.distributed rendezvous (env://, used only to
-  exchange the RCCL unique id) + our own RCCL communicator (libfacevae `fv_comm_*`).
+* `init_dist(local_rank, world_size, backend="nccl")` — the reference signature
+  (distributed.py:24).  torch.distributed is initialised over env:// with gloo and used only
+  for the rendezvous (the RCCL unique id); `backend="nccl"` then creates our own RCCL
+  communicator (libfacevae `fv_comm_*`), `backend="gloo"` a TorchComm (CPU tests, or several
+  ranks sharing one GPU, which RCCL refuses).
+* `comm_from_process_group()` — the same, for a caller that initialised torch.distributed
+  itself (e.g. the reference `init_dist`): FaceVAETrainer calls it, so a reference-style
+  launch never trains unsynchronised.
 * `DataParallel(module)` — DDP replacement: broadcast of params/buffers from rank 0 once
-  (collective C2 of SURVEY.md §2), gradient all-reduce (AVG) in ~25 MB buckets launched
-  from post-accumulate-grad hooks on a dedicated comm stream so it overlaps the rest of
-  the backward pass (C4); the compute stream waits for the comm stream only at the end.
-* SyncBN: BN statistics ([3][C] fp64) and backward sums ([2][C] fp64) are all-reduced on
-  the compute stream between the stats and finalize kernels (C5/C6).
+  (collective C2 of SURVEY.md §2), gradient all-reduce (AVG) in buckets launched from
+  post-accumulate-grad hooks so it overlaps the rest of the backward pass (C4).  Bucketing
+  follows DDP: a small first bucket (1 MB, `_DEFAULT_FIRST_BUCKET_BYTES`) so the first
+  all-reduce starts as soon as the last layer's gradients exist, then `bucket_cap_mb` (25)
+  buckets; one dtype per bucket; optional bf16 gradient compression (`grad_dtype`).
+* SyncBN (C5/C6): BN statistics ([3][C] fp64, row 0 = the per-rank pixel count, so uneven
+  shards normalise correctly) and the backward sums ([2][C] fp64) are all-reduced in stream
+  order between the statistics and finalize kernels.
+
+Ordering: every RCCL collective of a process is issued on ONE comm stream per communicator
+(as torch's ProcessGroupNCCL does), fenced against the compute stream with stream waits, and
+every rank issues them in the same host order (the autograd engine walks the same graph on
+every rank).  No reliance on cross-stream ordering inside RCCL.
 
 `TorchComm` implements the same interface over torch.distributed (gloo) so the bucketing /
 averaging / SyncBN plumbing is testable on CPU with world_size 2.
@@ -17,17 +32,22 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import List, Optional
+import random
+from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
 _COMM = None          # installed communicator (RcclComm / TorchComm)
 _SYNCBN = True
 
+FIRST_BUCKET_MB = 1.0   # torch/nn/parallel/distributed.py _DEFAULT_FIRST_BUCKET_BYTES
+
 
 class RcclComm:
-    """fv_comm_* communicator bound to one GPU; collectives are stream-ordered."""
+    """fv_comm_* communicator bound to one GPU.  All of its collectives run on its own comm
+    stream, fenced against the caller's stream (see module docstring)."""
 
     def __init__(self, rank: int, world_size: int, device: int, uid: bytes):
         from . import _lib as L
@@ -37,6 +57,7 @@ class RcclComm:
         h = ctypes.c_void_p()
         L.call("fv_comm_init", ctypes.addressof(buf), world_size, rank, device, ctypes.byref(h))
         self._h = h
+        self.stream = torch.cuda.Stream(device=device)
 
     @staticmethod
     def unique_id() -> bytes:
@@ -45,18 +66,30 @@ class RcclComm:
         L.call("fv_comm_unique_id", ctypes.addressof(buf))
         return bytes(buf)
 
-    def allreduce_(self, t: torch.Tensor, op: str = "sum", stream=None):
-        L = self._L
-        s = stream.cuda_stream if stream is not None else L.stream()
-        L.call("fv_comm_allreduce", self._h, t.data_ptr(), t.numel(), L.dtype_code(t.dtype),
-               1 if op == "avg" else 0, s)
+    def _launch(self, fn, t: torch.Tensor, wait_back: bool):
+        cur = torch.cuda.current_stream(t.device)
+        self.stream.wait_stream(cur)
+        fn(self.stream.cuda_stream)
+        t.record_stream(self.stream)
+        if wait_back:
+            cur.wait_stream(self.stream)
         return t
 
-    def broadcast_(self, t: torch.Tensor, root: int = 0, stream=None):
+    def allreduce_(self, t: torch.Tensor, op: str = "sum", wait_back: bool = True):
+        """In-place all-reduce (op "sum" or "avg") on the comm stream; with wait_back the
+        caller's stream waits for it (SyncBN), otherwise the caller fences later (buckets)."""
         L = self._L
-        s = stream.cuda_stream if stream is not None else L.stream()
-        L.call("fv_comm_broadcast", self._h, t.data_ptr(), t.numel(), L.dtype_code(t.dtype), root, s)
-        return t
+        return self._launch(lambda s: L.call("fv_comm_allreduce", self._h, t.data_ptr(), t.numel(),
+                                             L.dtype_code(t.dtype), 1 if op == "avg" else 0, s), t, wait_back)
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0, wait_back: bool = True):
+        L = self._L
+        return self._launch(lambda s: L.call("fv_comm_broadcast", self._h, t.data_ptr(), t.numel(),
+                                             L.dtype_code(t.dtype), root, s), t, wait_back)
+
+    def fence(self, device=None):
+        """Make the caller's stream wait for every collective issued so far."""
+        torch.cuda.current_stream(device).wait_stream(self.stream)
 
     def destroy(self):
         if self._h:
@@ -65,22 +98,25 @@ class RcclComm:
 
 
 class TorchComm:
-    """Same interface over torch.distributed (gloo on CPU) — for the CPU tests."""
+    """Same interface over torch.distributed (gloo): synchronous, so no stream fencing."""
 
     def __init__(self, group=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
 
-    def allreduce_(self, t, op="sum", stream=None):
+    def allreduce_(self, t, op="sum", wait_back=True):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         if op == "avg":
             t.div_(self.world_size)
         return t
 
-    def broadcast_(self, t, root=0, stream=None):
+    def broadcast_(self, t, root=0, wait_back=True):
         dist.broadcast(t, src=root, group=self.group)
         return t
+
+    def fence(self, device=None):
+        pass
 
     def destroy(self):
         pass
@@ -102,6 +138,7 @@ def syncbn_comm():
 
 
 def get_rank() -> int:
+    """distributed.py:34-40: torch.distributed's rank (0 when not initialised)."""
     if _COMM is not None:
         return _COMM.rank
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
@@ -117,78 +154,131 @@ def is_master() -> bool:
     return get_rank() == 0
 
 
-def init_seeds(seed: int = 1):
-    """distributed.py:9-21 (the reference seeds every rank with 1: init_seeds runs before
-    init_dist, Appendix A.1)."""
-    import random
-    import numpy as np
+def init_seeds(cuda_deterministic: bool = True):
+    """distributed.py:9-21: seed = 1 + rank for python, numpy and torch (CPU and every GPU).
+    train.py:12 calls it BEFORE init_dist, so the rank is 0 and every rank seeds 1 (SURVEY.md
+    Appendix A.1).  The cuDNN flags have no counterpart here (no cuDNN on this path); the
+    HIP kernels are deterministic either way (no atomics, fixed reduction orders)."""
+    seed = 1 + get_rank()
     random.seed(seed)
     np.random.seed(seed)
     torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+    return seed
 
 
-def init_dist(local_rank: Optional[int] = None, world_size: Optional[int] = None, syncbn: bool = True):
-    """Rendezvous via env:// (MASTER_ADDR/PORT, RANK, WORLD_SIZE as torch.distributed.run
-    sets them) and create the RCCL communicator of this process's GPU."""
+def _rccl_from_group(local_rank: int) -> RcclComm:
+    rank, world = dist.get_rank(), dist.get_world_size()
+    obj = [RcclComm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return RcclComm(rank, world, local_rank, obj[0])
+
+
+def init_dist(local_rank: Optional[int] = None, world_size: Optional[int] = None, backend: str = "nccl",
+              syncbn: bool = True):
+    """distributed.py:24-31 with the reference signature.  Rendezvous via env:// (MASTER_ADDR /
+    MASTER_PORT; RANK defaults to local_rank as in the reference's mp.spawn launch), then
+    `backend` "nccl" -> our RCCL communicator on cuda:local_rank, "gloo" -> TorchComm.  The
+    reference also switches on torch.autograd anomaly detection here (distributed.py:26); it
+    changes no numerics and is left off."""
     if local_rank is None:
         local_rank = int(os.environ.get("LOCAL_RANK", 0))
     rank = int(os.environ.get("RANK", local_rank))
     if world_size is None:
         world_size = int(os.environ.get("WORLD_SIZE", 1))
-    torch.cuda.set_device(local_rank)
+    if backend not in ("nccl", "rccl", "gloo"):
+        raise ValueError(f"init_dist: backend {backend!r} (nccl/rccl or gloo)")
+    if torch.cuda.is_available():
+        # gloo: several ranks may share a GPU (RCCL needs one GPU per rank)
+        torch.cuda.set_device(local_rank if backend != "gloo" else local_rank % torch.cuda.device_count())
     if world_size > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", init_method="env://", world_size=world_size, rank=rank)
+    comm = None
     if world_size > 1:
-        obj = [RcclComm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm = RcclComm(rank, world_size, local_rank, obj[0])
-    else:
-        comm = None
+        comm = TorchComm() if backend == "gloo" else _rccl_from_group(local_rank)
     install(comm, syncbn)
     return comm
 
 
-class DataParallel(torch.nn.Module):
-    """DistributedDataParallel replacement with bucketed, overlapped gradient all-reduce."""
+def comm_from_process_group(syncbn: bool = True):
+    """Communicator for a process whose torch.distributed group was initialised elsewhere
+    (e.g. by the reference's init_dist with backend "nccl"): an RCCL communicator on the
+    current device for an nccl group, a TorchComm for gloo.  Installed and returned."""
+    if not (dist.is_available() and dist.is_initialized()):
+        raise RuntimeError("comm_from_process_group: torch.distributed is not initialised")
+    if dist.get_world_size() == 1:
+        install(None, syncbn)
+        return None
+    backend = str(dist.get_backend()).lower()
+    if backend in ("nccl", "rccl"):
+        comm = _rccl_from_group(torch.cuda.current_device())
+    elif backend == "gloo":
+        comm = TorchComm()
+    else:
+        raise RuntimeError(f"comm_from_process_group: unsupported torch.distributed backend {backend!r}")
+    install(comm, syncbn)
+    return comm
 
-    def __init__(self, module: torch.nn.Module, comm=None, bucket_cap_mb: float = 25.0):
+
+def plan_buckets(params, bucket_cap_mb: float = 25.0, first_bucket_mb: float = FIRST_BUCKET_MB):
+    """DDP bucket assignment: parameters in reverse registration order (~ the order their
+    gradients become ready in backward), one dtype per bucket, the first bucket capped at
+    `first_bucket_mb` and the rest at `bucket_cap_mb` (in bytes of the gradient dtype)."""
+    buckets: List[List[torch.nn.Parameter]] = []
+    cur: Dict[torch.dtype, List] = {}
+    size: Dict[torch.dtype, int] = {}
+
+    def cap_bytes():
+        return (first_bucket_mb if not buckets else bucket_cap_mb) * 1024 * 1024
+
+    for p in reversed(list(params)):
+        dt = p.dtype
+        nbytes = p.numel() * p.element_size()
+        if cur.get(dt) and size[dt] + nbytes > cap_bytes():
+            buckets.append(cur[dt])
+            cur[dt], size[dt] = [], 0
+        cur.setdefault(dt, []).append(p)
+        size[dt] = size.get(dt, 0) + nbytes
+    for dt, b in cur.items():
+        if b:
+            buckets.append(b)
+    return buckets
+
+
+class DataParallel(torch.nn.Module):
+    """DistributedDataParallel replacement with bucketed, overlapped gradient all-reduce.
+
+    grad_dtype: None (all-reduce in the parameter dtype, the reference's fp32) or
+    torch.bfloat16 (compressed: gradients cast into a bf16 flat buffer, averaged, cast back;
+    halves the xGMI bytes, labelled in bench output)."""
+
+    def __init__(self, module: torch.nn.Module, comm=None, bucket_cap_mb: float = 25.0,
+                 first_bucket_mb: float = FIRST_BUCKET_MB, grad_dtype: Optional[torch.dtype] = None):
         super().__init__()
         self.module = module
         self.comm = comm if comm is not None else _COMM
         self.world = self.comm.world_size if self.comm is not None else 1
         params = [p for p in module.parameters() if p.requires_grad]
         self._params = params
+        self.grad_dtype = grad_dtype
         if self.comm is not None and self.world > 1:
             with torch.no_grad():
                 for t in list(module.parameters()) + list(module.buffers()):
                     if t.is_floating_point():
                         self.comm.broadcast_(t.data, 0)
-        # buckets in reverse registration order (~ the order grads become ready)
-        cap = int(bucket_cap_mb * 1024 * 1024 / 4)
-        self.buckets: List[List[torch.nn.Parameter]] = []
-        cur, size = [], 0
-        for p in reversed(params):
-            if cur and size + p.numel() > cap:
-                self.buckets.append(cur)
-                cur, size = [], 0
-            cur.append(p)
-            size += p.numel()
-        if cur:
-            self.buckets.append(cur)
+        self.buckets = plan_buckets(params, bucket_cap_mb, first_bucket_mb)
         self._where = {}
-        self._flat = []
         for bi, b in enumerate(self.buckets):
             off = 0
             for p in b:
                 self._where[id(p)] = (bi, off)
                 off += p.numel()
-            self._flat.append(None)
-            self._flat_n = None
         self._sizes = [sum(p.numel() for p in b) for b in self.buckets]
+        self._flat: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._pending = [0] * len(self.buckets)
-        self._cuda = params[0].is_cuda if params else False
-        self._comm_stream = torch.cuda.Stream(device=params[0].device) if (self._cuda and self.world > 1) else None
+        self.launch_order: List[int] = []      # bucket indices in launch order, last backward
         self._hooks = []
         self._armed = False
         if self.world > 1:
@@ -198,12 +288,14 @@ class DataParallel(torch.nn.Module):
     def forward(self, *args, **kwargs):
         self._pending = [len(b) for b in self.buckets]
         self._armed = False
+        self.launch_order = []
         return self.module(*args, **kwargs)
 
     def _flat_buf(self, bi, like):
         f = self._flat[bi]
+        dt = self.grad_dtype or self.buckets[bi][0].dtype
         if f is None or f.device != like.device:
-            f = torch.empty(self._sizes[bi], dtype=torch.float32, device=like.device)
+            f = torch.empty(self._sizes[bi], dtype=dt, device=like.device)
             self._flat[bi] = f
         return f
 
@@ -216,34 +308,27 @@ class DataParallel(torch.nn.Module):
             self._armed = True
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
-            self._launch(bi)
-
-    def _launch(self, bi):
-        flat = self._flat[bi]
-        if self._comm_stream is not None:
-            cur = torch.cuda.current_stream(flat.device)
-            self._comm_stream.wait_stream(cur)
-            with torch.cuda.stream(self._comm_stream):
-                self.comm.allreduce_(flat, op="avg", stream=self._comm_stream)
-                flat.record_stream(self._comm_stream)
-        else:
-            self.comm.allreduce_(flat, op="avg")
+            self.launch_order.append(bi)
+            self.comm.allreduce_(self._flat[bi], op="avg", wait_back=False)
 
     def _finish(self):
         for bi, n in enumerate(self._pending):     # params that got no grad this step
             if n != 0 and n != len(self.buckets[bi]):
                 raise RuntimeError("DataParallel: a bucket was only partially reduced "
                                    "(unused parameters are not supported)")
-        if self._comm_stream is not None:
-            torch.cuda.current_stream(self._comm_stream.device).wait_stream(self._comm_stream)
+        if self._params:
+            self.comm.fence(self._params[0].device if self._params[0].is_cuda else None)
         for bi, b in enumerate(self.buckets):
             if self._pending[bi] != 0:
                 continue
             flat = self._flat[bi]
             for p in b:
                 _, off = self._where[id(p)]
-                p.grad = flat[off:off + p.numel()].view_as(p)
-        self._armed = False
+                v = flat[off:off + p.numel()].view_as(p)
+                if v.dtype == p.dtype:
+                    p.grad = v
+                else:
+                    p.grad.copy_(v)
 
     def sync_buffers(self):
         """Broadcast BN running stats / SN u, v from rank 0 (the reference's per-forward C3

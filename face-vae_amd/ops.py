@@ -101,6 +101,12 @@ class KernelTimer:
 
 TIMER: Optional[KernelTimer] = None
 
+# Test hook (tests/test_layers_gpu.py): called after every conv launch of the model path as
+# CHECK(kind, cs, **tensors) with kind in {"fwd", "dgrad", "wgrad"}, so a test can compare each
+# launch, at the exact shapes and data of a real step, with a torch fp32 reference of the
+# same op on the same (bf16) operands.  None in production.
+CHECK = None
+
 
 def _timed(kind, d, fn):
     return fn() if TIMER is None else TIMER.wrap(kind, d, fn)
@@ -214,6 +220,8 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
     psc, psh = (pro if pro is not None else (None, None))
     _timed("fwd", d, lambda: call("fv_conv2d_fwd", ctypes.byref(d), ptr(x), ptr(cs.wk), ptr(bias), ptr(psc),
                                   ptr(psh), ptr(res), ptr(y), ptr(part), stream()))
+    if CHECK is not None:
+        CHECK("fwd", cs, x=x, bias=bias, pro=pro, res=res, y=y)
     return part
 
 
@@ -229,6 +237,8 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
     dw = torch.empty_like(cs.w)
     db = torch.empty(d.cout, dtype=F32, device=dev) if need_db else None
     call("fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(dw), ptr(db), stream())
+    if CHECK is not None:
+        CHECK("wgrad", cs, x=x, dy=dy, ldd=ldd, dw=dw, db=db, pro=pro)
     if cs.conv.sn:
         spectral_norm_bwd(cs.w, dw, cs.u, cs.v, cs.sigma)
     dx = None
@@ -246,6 +256,8 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
             call("fv_upsample2x_bwd", L.dtype_code(dy.dtype), ptr(dx), d.n, d.h // 2, d.w // 2, d.cin, ptr(src),
                  stream())
             dx = src
+    if CHECK is not None and dx is not None:
+        CHECK("dgrad", cs, dy=dy, ldd=ldd, dx=dx)
     return dx, dw, db
 
 
@@ -254,16 +266,20 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
 # ----------------------------------------------------------------------------------------
 
 class BNResult:
-    __slots__ = ("mean", "invstd", "scale", "shift", "count")
+    """Per-forward BN state: save_mean / save_invstd / fused (scale, shift), and the element
+    count -- a host int in a single process, or `stats` (the all-reduced fp64 [3][C] record
+    whose row 0 is the global count) under SyncBN."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "count", "stats")
 
 
-def _bn_result(C, dev, count):
+def _bn_result(C, dev, count, stats=None):
     r = BNResult()
     r.mean = torch.empty(C, dtype=F32, device=dev)
     r.invstd = torch.empty(C, dtype=F32, device=dev)
     r.scale = torch.empty(C, dtype=F32, device=dev)
     r.shift = torch.empty(C, dtype=F32, device=dev)
     r.count = count
+    r.stats = stats
     return r
 
 
@@ -279,16 +295,17 @@ def bn_finalize(bn, stats, count, training):
     """stats [3][C] fp64 (already all-reduced for SyncBN) -> BNResult; updates running stats
     and num_batches_tracked (torch/nn/modules/batchnorm.py:744-840)."""
     C = bn.num_features
-    r = _bn_result(C, bn.weight.device, count)
+    r = _bn_result(C, bn.weight.device, count, stats)
     rm, rv, nbt = _running(bn, training)
     call("fv_bn_finalize", ptr(stats), C, ptr(bn.weight), ptr(bn.bias), float(bn.eps), float(bn.momentum),
          int(training), rm, rv, nbt, ptr(r.mean), ptr(r.invstd), ptr(r.scale), ptr(r.shift), stream())
     return r
 
 
-def _sync(stats, comm, dtype_code=L.FV_F64):
+def _sync(stats, comm):
+    """SyncBN all-reduce (sum) of an fp64 record, in stream order (distributed.py)."""
     if comm is not None:
-        comm.allreduce_(stats, op="sum")
+        comm.allreduce_(stats, op="sum", wait_back=True)
 
 
 def bn_from_partials(bn, part, d, training, comm):
@@ -308,8 +325,8 @@ def bn_from_partials(bn, part, d, training, comm):
         return r
     stats = torch.empty(3 * C, dtype=F64, device=dev)
     call("fv_bn_stats_from_partials", ptr(part), nb, bp, P, C, ptr(stats), ptr(ws), stream())
-    _sync(stats, comm)
-    return bn_finalize(bn, stats, P * comm.world_size, training)
+    _sync(stats, comm)                      # row 0 (count) is summed too: the global count
+    return bn_finalize(bn, stats, None, training)
 
 
 def bn_from_tensor(bn, x, training, comm):
@@ -327,15 +344,17 @@ def bn_from_tensor(bn, x, training, comm):
     stats = torch.empty(3 * C, dtype=F64, device=x.device)
     call("fv_bn_stats_tensor", L.dtype_code(x.dtype), ptr(x), N * H * W, C, C, ptr(stats), ptr(ws), stream())
     _sync(stats, comm)
-    return bn_finalize(bn, stats, N * H * W * comm.world_size, True)
+    return bn_finalize(bn, stats, None, True)
 
 
-def bn_act_forward(y, r: BNResult, slope, pool):
+def bn_act_forward(y, r: BNResult, slope, pool, bn=None):
     N, C, H, W = y.shape
     Ho, Wo = (H // 2, W // 2) if pool else (H, W)
     out = torch.empty((N, C, Ho, Wo), dtype=y.dtype, device=y.device, memory_format=CL)
     call("fv_bn_act_fwd", L.dtype_code(y.dtype), ptr(y), N, H, W, C, C, ptr(r.scale), ptr(r.shift), float(slope),
          int(pool), ptr(out), stream())
+    if CHECK is not None:
+        CHECK("bn_fwd", bn, y=y, r=r, slope=slope, pool=pool, out=out)
     return out
 
 
@@ -349,24 +368,33 @@ def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, ne
     dbt = torch.empty(C, dtype=F32, device=dev)
     k = torch.empty(2 * C, dtype=F32, device=dev)
     if comm is None:
+        # eval mode (running statistics, count 0): the normalisation is a fixed affine map, so
+        # the batch-statistics terms k vanish and dx = gamma * invstd * g
+        evalm = r.count == 0 and r.stats is None
         call("fv_bn_act_bwd_reduce_finalize", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
-             ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), int(r.count), ptr(dg), ptr(dbt), ptr(k), ptr(ws),
-             stream())
+             ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), 1 if evalm else int(r.count), ptr(dg), ptr(dbt),
+             ptr(k), ptr(ws), stream())
+        if evalm:
+            k.zero_()
     else:
         red = torch.empty(2 * C, dtype=F64, device=dev)
         call("fv_bn_act_bwd_reduce", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
              ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), ptr(red), ptr(ws), stream())
         # dgamma / dbeta from this rank's sums (torch SyncBatchNorm: batch_norm_backward_reduce
-        # is local, only sum_dy / sum_dy_xmu are all-reduced -- _functions.py); the data-parallel
-        # gradient average then yields the global-batch value.  dx uses the global sums.
-        call("fv_bn_bwd_finalize", ptr(red), C, int(r.count), ptr(dg), ptr(dbt), ptr(k), stream())
-        _sync(red, comm)
-        call("fv_bn_bwd_finalize", ptr(red), C, int(r.count), None, None, ptr(k), stream())
+        # is local, only sum_dy / sum_dy_xmu are all-reduced, and only when the input needs a
+        # gradient -- _functions.py); the data-parallel gradient average then yields the
+        # global-batch value.  dx uses the global sums over the global count (stats row 0).
+        call("fv_bn_bwd_finalize", ptr(red), C, 0, ptr(dg), ptr(dbt), None, stream())
+        if need_dx:
+            _sync(red, comm)
+            call("fv_bn_bwd_finalize_dev", ptr(red), C, ptr(r.stats), None, None, ptr(k), stream())
     dx = None
     if need_dx:
         dx = torch.empty((N, C, H, W), dtype=y.dtype, device=dev, memory_format=CL)
         call("fv_bn_act_bwd_apply", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
              ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), ptr(k), ptr(addend), ptr(dx), stream())
+    if CHECK is not None and comm is None:
+        CHECK("bn_bwd", bn, dout=dout, y=y, r=r, slope=slope, pool=pool, addend=addend, dx=dx, dg=dg, dbt=dbt)
     return dx, dg, dbt
 
 
@@ -399,7 +427,7 @@ class ConvBNActFn(torch.autograd.Function):
         part = conv_forward(cs, xb, bias, y=y, stats=training)
         comm = blk.bn_comm()
         r = bn_from_partials(bn, part, d, True, comm) if training else bn_finalize(bn, None, 0, False)
-        z = bn_act_forward(y, r, blk.slope, blk.pool)
+        z = bn_act_forward(y, r, blk.slope, blk.pool, bn)
         cs.release()
         ctx.blk, ctx.cs, ctx.r, ctx.comm = blk, cs, r, comm
         ctx.save_for_backward(x, xb, y)
@@ -432,13 +460,13 @@ class ResBlockFn(torch.autograd.Function):
         comm = blk.bn_comm()
         c1, c2 = blk.conv1, blk.conv2
         r1 = bn_from_tensor(blk.bn1, xb, training, comm)
-        a1 = bn_act_forward(xb, r1, 0.0, False)
+        a1 = bn_act_forward(xb, r1, 0.0, False, blk.bn1)
         d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size)
         cs1 = ConvState(c1, d1, dtype, x.device, training, True)
         t1 = torch.empty_like(xb)
         part = conv_forward(cs1, a1, b1, y=t1, stats=training)
         r2 = bn_from_partials(blk.bn2, part, d1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
-        a2 = bn_act_forward(t1, r2, 0.0, False)
+        a2 = bn_act_forward(t1, r2, 0.0, False, blk.bn2)
         d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size)
         cs2 = ConvState(c2, d2, dtype, x.device, training, True)
         out = torch.empty_like(xb)
@@ -479,7 +507,7 @@ class NACFn(torch.autograd.Function):
             raise RuntimeError("NAC block output channels must be a multiple of 8")
         comm = blk.bn_comm()
         r = bn_from_tensor(blk.bn, xb, blk.training, comm)
-        a = bn_act_forward(xb, r, blk.slope, False)
+        a = bn_act_forward(xb, r, blk.slope, False, blk.bn)
         d = desc(dtype, N, H, W, C, C, cout, cout, conv.kernel_size)
         cs = ConvState(conv, d, dtype, x.device, blk.training, need_wt=True)
         y = torch.empty((N, cout, H, W), dtype=dtype, device=x.device, memory_format=CL)

@@ -15,6 +15,7 @@ from typing import Dict, Optional
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import config as _config
 from . import distributed
@@ -26,7 +27,7 @@ from .optim import Adam
 class FaceVAETrainer:
     def __init__(self, ckp_dir, vis_dir, dataloader, lr, checkpoint_freq=1, visualizer_params=None, zfill_num=8,
                  log_file_name="log_facevae.txt", cfg: Optional[_config.FaceVAEConfig] = None,
-                 compute_dtype: Optional[torch.dtype] = None, seed: Optional[int] = 0):
+                 compute_dtype: Optional[torch.dtype] = None, seed: Optional[int] = None):
         self.cfg = cfg or _config.FaceVAEConfig(lr=lr)
         self.ckp_dir, self.vis_dir = ckp_dir, vis_dir
         self.dataloader = dataloader
@@ -40,13 +41,19 @@ class FaceVAETrainer:
             if vis_dir:
                 os.makedirs(vis_dir, exist_ok=True)
             self.log_file = open(log_file_name, "a")
-        if seed is not None:
+        if seed is not None:          # the reference seeds in train.py (init_seeds), not here
             torch.manual_seed(seed)
         self.model = FaceVAE(self.cfg).cuda()
         if compute_dtype is not None:
             self.model.set_compute_dtype(compute_dtype)
+        # a process group initialised by the caller (e.g. the reference's init_dist, which
+        # uses torch.distributed directly) gets its communicator here: the model is never
+        # trained unsynchronised under a multi-rank launch
         self.comm = distributed.get_comm()
-        self.ddp = distributed.DataParallel(self.model, self.comm) if self.comm is not None else None
+        if self.comm is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self.comm = distributed.comm_from_process_group(self.cfg.syncbn)
+        multi = self.comm is not None and self.comm.world_size > 1
+        self.ddp = distributed.DataParallel(self.model, self.comm) if multi else None
         self.net = self.ddp if self.ddp is not None else self.model
         # one Adam per model as logger.py:60 (elementwise: identical to one over all params)
         self.g_models = {"afe": self.model.afe, "generator": self.model.generator}

@@ -200,9 +200,14 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
                          int ldc, const float* mean, const float* invstd, const float* gamma,
                          const float* beta, float slope, int pool, double* red, void* ws,
                          void* stream);
-/* dgamma/dbeta (accumulated) and the two BN-backward coefficients k [2][c] */
+/* dgamma/dbeta and the two BN-backward coefficients k [2][c] = red / count (k may be NULL:
+ * dgamma/dbeta only; dgamma/dbeta may be NULL) */
 int fv_bn_bwd_finalize(const double* red, int c, long count, float* dgamma, float* dbeta,
                        float* k, void* stream);
+/* the same with the element count read per channel from device memory (row 0 of the
+ * all-reduced [3][c] statistics record: the global count, also for uneven per-rank batches) */
+int fv_bn_bwd_finalize_dev(const double* red, int c, const double* count, float* dgamma,
+                           float* dbeta, float* k, void* stream);
 /* single-process form of fv_bn_act_bwd_reduce + fv_bn_bwd_finalize (two launches) */
 int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
                                   int ldc, const float* mean, const float* invstd, const float* gamma,

@@ -35,7 +35,7 @@ class _Net(torch.nn.Module):
         return self.b(torch.tanh(self.a(x)))
 
 
-def _worker(rank, world, port, bucket_mb, q):
+def _worker(rank, world, port, bucket_mb, q, grad_dtype=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -47,7 +47,8 @@ def _worker(rank, world, port, bucket_mb, q):
         net.running.fill_(float(rank + 1))
         comm = D.TorchComm()
         D.install(comm, syncbn=True)
-        dp = D.DataParallel(net, comm, bucket_cap_mb=bucket_mb)
+        dp = D.DataParallel(net, comm, bucket_cap_mb=bucket_mb, first_bucket_mb=min(bucket_mb, 1.0),
+                            grad_dtype=grad_dtype)
         # C2: parameters and buffers now equal rank 0's
         flat = torch.cat([p.detach().reshape(-1) for p in net.parameters()] + [net.running])
         g = torch.Generator().manual_seed(7)
@@ -60,16 +61,16 @@ def _worker(rank, world, port, bucket_mb, q):
             loss = ((dp(x) - y) ** 2).mean()
             loss.backward()
         grads = torch.cat([p.grad.reshape(-1) for p in net.parameters()])
-        q.put((rank, flat, grads, len(dp.buckets), D.syncbn_comm() is comm))
+        q.put((rank, flat, grads, len(dp.buckets), D.syncbn_comm() is comm, list(dp.launch_order)))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, bucket_mb):
+def _run(world, bucket_mb, grad_dtype=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q, grad_dtype)) for r in range(world)]
     for p in ps:
         p.start()
     out = [q.get(timeout=120) for _ in ps]
@@ -82,13 +83,16 @@ def _run(world, bucket_mb):
 @pytest.mark.parametrize("bucket_mb", [25.0, 1e-6])
 def test_dataparallel_gloo_world2(bucket_mb):
     out = _run(2, bucket_mb)
-    (_, f0, g0, nb0, sb0), (_, f1, g1, nb1, sb1) = out
+    (_, f0, g0, nb0, sb0, lo0), (_, f1, g1, nb1, sb1, lo1) = out
     assert torch.equal(f0, f1), "rank-0 broadcast of params/buffers"
     assert sb0 and sb1, "SyncBN communicator installed"
     if bucket_mb < 1:
         assert nb0 == 4, "tiny cap: one bucket per parameter"
+        # buckets hold the parameters in reverse registration order and launch in the order
+        # their gradients complete (b.bias / b.weight first: the last layer's grads are ready first)
+        assert lo0 == lo1 and sorted(lo0) == [0, 1, 2, 3] and set(lo0[:2]) == {0, 1}
     else:
-        assert nb0 == 1
+        assert nb0 == 1 and lo0 == [0]
     assert torch.allclose(g0, g1, atol=0, rtol=0), "identical averaged gradients on every rank"
     # reference: the same model on the global batch (mean loss) in one process
     torch.manual_seed(100)
@@ -100,3 +104,39 @@ def test_dataparallel_gloo_world2(bucket_mb):
     loss.backward()
     gr = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
     assert torch.allclose(g0, gr, rtol=1e-5, atol=1e-6)
+
+
+def test_dataparallel_bf16_grad_compression_world2():
+    """grad_dtype=bf16: gradients averaged in a bf16 flat buffer, written back into fp32 .grad
+    (the parameter dtype contract holds); equal on both ranks, within bf16 rounding of the
+    fp32 global-batch gradient."""
+    out = _run(2, 25.0, torch.bfloat16)
+    (_, f0, g0, *_), (_, f1, g1, *_) = out
+    assert g0.dtype == torch.float32 and torch.equal(g0, g1)
+    torch.manual_seed(100)
+    ref = _Net()
+    g = torch.Generator().manual_seed(7)
+    xs = torch.randn(4, 6, generator=g)
+    ys = torch.randn(4, 3, generator=g)
+    ((ref(xs) - ys) ** 2).mean().backward()
+    gr = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+    assert ((g0 - gr).norm() / gr.norm()).item() < 1e-2
+
+
+def test_bucket_plan_faceva_sizes():
+    """DDP bucketing of the real FaceVAE parameter set (8,633,091 fp32 params, 34.5 MB):
+    a <= 1 MB first bucket holding the last layers (Generator.out_conv ...), then <= 25 MB
+    buckets, every parameter exactly once, reverse registration order."""
+    import fvamd  # noqa: F401
+    from facevae_amd import FaceVAE, FaceVAEConfig
+    from facevae_amd.distributed import plan_buckets
+    m = FaceVAE(FaceVAEConfig())
+    params = [p for p in m.parameters()]
+    assert sum(p.numel() for p in params) == 8633091
+    bs = plan_buckets(params, 25.0, 1.0)
+    sizes = [sum(p.numel() * 4 for p in b) for b in bs]
+    assert sizes[0] <= 1 << 20 and all(s <= 25 << 20 for s in sizes[1:])
+    assert len(bs) == 3
+    flat = [p for b in bs for p in b]
+    assert [id(p) for p in flat] == [id(p) for p in reversed(params)]
+    assert bs[0][0] is m.generator.out_conv.bias

@@ -1,0 +1,156 @@
+"""Parity at the configurations the benchmark times (BASELINE.json C2: 256x256, B=32, bf16;
+C4: 512x512, B=8), two ways:
+
+1. Every conv launch of one real training step (forward, data gradient, weight + bias
+   gradient of all 15 convs: every kernel family at its exact B=32 / B=8 launch plan --
+   split counts, block counts, XCD remaps) is compared, right after it runs, with a torch
+   fp32 reference of the same op on the same bf16 operands (tests/conv_reference.py).
+   Gates: rel-L2 <= 5e-3 (bf16 outputs) / 1e-4 (fp32 weight gradients vs an fp64 reference)
+   and an ELEMENTWISE bound (bf16 output rounding + 2e-3 RMS; for the gradient sums 2^-14 of
+   the sum of |terms|) whose worst ratio must stay <= 1 -- a single bad tile fails it.
+2. The whole step against the CPU oracle (fp32 restatement of the reference) at B=32:
+   fp32 mode at the north_star bar (1e-3 relative on image, R, K), bf16 mode reported with
+   its deviation (bf16 activations: ~2e-2 image rel-L2 by construction).
+"""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+import facevae_amd as fv  # noqa: E402
+from facevae_amd import ops  # noqa: E402
+from oracle import facevae_cpu as O  # noqa: E402  (checker only)
+from conv_reference import LaunchChecker  # noqa: E402
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _inputs(B, H, latent=256, hw=None):
+    hw = hw or H // 4
+    x = torch.rand(B, 3, H, H, generator=torch.Generator().manual_seed(1234))
+    eps = torch.randn(B, latent, hw, hw, generator=torch.Generator().manual_seed(1235))
+    return x, eps
+
+
+def _gpu_step(cfg, dtype, x, eps, checker=None):
+    torch.manual_seed(0)
+    m = fv.FaceVAE(cfg)
+    init = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.cuda().train().set_compute_dtype(dtype)
+    if checker is not None:
+        checker = checker(m)
+    opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
+    xc, ec = x.cuda(), eps.cuda()
+    ops.CHECK = checker
+    try:
+        opt.zero_grad(set_to_none=True)
+        y, mu, logstd = m(xc, ec)
+        R = fv.ReconLoss()((xc, y))
+        K = fv.KLDivergenceLoss()((mu, logstd))
+        (cfg.w_R * R + cfg.w_K * K).backward()
+    finally:
+        ops.CHECK = None
+    grads = {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
+    opt.step()
+    torch.cuda.synchronize()
+    state = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    return init, y.detach().cpu(), R.item(), K.item(), grads, state, checker
+
+
+@pytest.mark.parametrize("H,B", [(256, 32), (512, 8)])
+def test_every_conv_launch_of_the_timed_step(H, B):
+    cfg = fv.FaceVAEConfig(H=H)
+    x, eps = _inputs(B, H)
+    *_, chk = _gpu_step(cfg, torch.bfloat16, x, eps, lambda m: LaunchChecker(m, torch.bfloat16))
+    print(f"\n[{H}x{H} B={B} bf16] per-launch deviation vs torch fp32 on the same bf16 operands\n" + chk.report())
+    kinds = {(r["layer"], r["kind"]) for r in chk.rows}
+    # 21 convs (AFE 4, Generator 17): fwd + wgrad + bgrad each, dgrad for all but AFE.in_conv
+    assert len([k for k in kinds if k[1] == "fwd"]) == 21
+    assert len([k for k in kinds if k[1] == "wgrad"]) == 21
+    assert len([k for k in kinds if k[1] == "dgrad"]) == 20
+    # 18 BatchNorm layers: forward apply (+ batch statistics), backward sums and data gradient
+    assert len({r["layer"] for r in chk.rows if r["kind"] == "bn_fwd"}) == 18
+    assert len({r["layer"] for r in chk.rows if r["kind"] == "dgamma"}) == 18
+    gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 5e-3,   # bgrad: dead biases cancel to ~0
+            "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
+    bad = [r for r in chk.rows if not (r["rel_l2"] <= gate[r["kind"]] and r["worst"] <= 1.0)]
+    assert not bad, bad
+
+
+@pytest.fixture(scope="module")
+def oracle_b32():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = O.OracleConfig()
+    init = O.init_state(cfg, 0)
+    sd = O.prepare_state(init)
+    x, eps = _inputs(32, 256)
+    out, grads = O.train_step(sd, O.adam_init(sd), x, eps, cfg)
+    return x, eps, {k: v.detach() for k, v in out.items()}, grads, {k: v.detach() for k, v in sd.items()}
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_b32_step_matches_oracle(oracle_b32, dtype):
+    x, eps, oo, og, osd = oracle_b32
+    init, y, R, K, grads, state, _ = _gpu_step(fv.FaceVAEConfig(), dtype, x, eps)
+    dev = {"image": rel(y, oo["y"]), "R": abs(R - oo["R"].item()) / oo["R"].item(),
+           "K": abs(K - oo["K"].item()) / abs(oo["K"].item())}
+    gdev = {k: rel(grads[k], og[k]) for k in og if not (k.endswith(".bias") and og[k].abs().max() < 1e-4)}
+    bn = {k: rel(state[k], osd[k]) for k in osd if k.endswith("running_mean") or k.endswith("running_var")}
+    for k in sorted(gdev, key=gdev.get):
+        print(f"   grad {k:50s} {gdev[k]:.2e}")
+    print(f"\n[{dtype}] 256x256 B=32 one step vs oracle: {dev}; worst grad rel-L2 "
+          f"{max(gdev.values()):.2e} ({max(gdev, key=gdev.get)}); worst BN running-stat rel-L2 {max(bn.values()):.2e}")
+    if dtype == torch.float32:
+        assert dev["image"] < 1e-3 and dev["R"] < 1e-3 and dev["K"] < 1e-3
+        # gradients are not under the north_star bar (image / R / K); a BN affine gradient sums
+        # 131k products with heavy cancellation, where the fp32 oracle's own error is ~1e-3
+        assert max(gdev.values()) < 1e-2 and max(bn.values()) < 1e-4
+    else:
+        # bf16 activations: ~2^-9 relative noise per layer.  The per-op checks above gate every
+        # kernel on its own bf16 operands at output-rounding accuracy; end to end the image and
+        # the losses must stay close to the fp32 reference.  Parameter gradients are reported
+        # and gated loosely: at this (random-init) point the backward pass through the 13 BN
+        # layers of the Generator trunk is ill-conditioned -- even between two fp32
+        # computations (fp32 mode above vs the fp32 CPU oracle) the deviation grows from 1e-6 at
+        # out_conv to 4e-3 at Generator.in_conv, and the bf16 storage noise grows the same way,
+        # ~60x larger (5e-3 at out_conv to ~0.25 at Generator.in_conv).
+        gs = sorted(gdev.values())
+        assert dev["image"] < 2e-2 and dev["R"] < 1e-3 and dev["K"] < 1e-3
+        assert gs[len(gs) // 2] < 0.2 and gs[-1] < 0.5 and max(bn.values()) < 2e-2
+
+
+def test_bn_eval_mode_matches_oracle():
+    """Inference path: BatchNorm with running statistics (modules.py:19 in .eval()), spectral
+    norm without the power iteration; forward and input gradient in fp32 mode vs the oracle's
+    training=False forward (toy config, after one training step so the running stats are
+    non-trivial)."""
+    cfg = fv.FaceVAEConfig.toy()
+    ocfg = O.OracleConfig.toy()
+    x, eps = _inputs(2, 64, cfg.latent, cfg.latent_hw)
+    torch.manual_seed(0)
+    m = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(torch.float32)
+    opt = fv.Adam(m.parameters(), lr=1e-3, betas=cfg.betas)
+    y, mu, ls = m(x.cuda(), eps.cuda())
+    (fv.ReconLoss()((x.cuda(), y)) + fv.KLDivergenceLoss()((mu, ls))).backward()
+    opt.step()
+    m.eval()
+    sd = O.prepare_state({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    xr = x.clone().requires_grad_(True)
+    oo = O.forward(sd, xr, eps, ocfg, training=False)
+    g = torch.randn(oo["y"].shape, generator=torch.Generator().manual_seed(3))
+    (oo["y"] * g).sum().backward()
+    xc = x.cuda().requires_grad_(True)
+    y2, _, _ = m(xc, eps.cuda())
+    (y2 * g.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    assert rel(y2, oo["y"]) < 1e-4
+    assert rel(xc.grad, xr.grad) < 1e-3
+    after = m.state_dict()
+    for k, v in sd.items():                      # eval: no running-stat / SN-buffer update
+        if not O.is_param(k):
+            assert torch.equal(after[k].cpu(), v.detach().cpu() if v.is_floating_point() else v), k

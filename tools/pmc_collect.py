@@ -1,0 +1,129 @@
+"""Per-kernel hardware counters of bench.py from rocprofv3 --pmc passes (one counter group per
+pass, as gpurun and the PMC slot limits require), corrected as MI355X_MICROARCH.md prescribes:
+
+* HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  (KiB counters; gfx950 FETCH_SIZE tallies
+  half the bytes of a wide coalesced stream);
+* MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024): the busy cycles
+  summed over all 1024 SIMDs against the active cycles of one XCD (rocprofv3 sums
+  GRBM_GUI_ACTIVE over the 8 XCDs) times the SIMD count -- the `MfmaUtil` expression of
+  counter_defs.yaml, DVFS-independent;
+* effective clock = GRBM_GUI_ACTIVE / 8 / kernel duration (duration from a separate
+  --kernel-trace run of the same command);
+* executed MFMA FLOP = busy cycles * 1024 FLOP per SIMD-cycle (bf16 16x16x32: 16384 FLOP in
+  16 cycles), cross-checked against the algorithmic FLOP of the dominant launch.
+
+    python tools/pmc_collect.py --trace <kernel-trace dir> --pass <dir> [--pass <dir> ...] > profiles/rN_pmc.json
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import re
+
+# bench family -> (kernel-name pattern, total grid size in work-items) of the 256->256 res conv
+# at 64x64, B=32 (bench.py's dominant kernel)
+DOMS = {
+    "fwd": (re.compile(r"conv3_halo_fwd2<4, 2, 4, 8, 2>"), 512 * 512),
+    "dgrad": (re.compile(r"conv3_halo_fwd2<4, 2, 4, 8, 2>"), 512 * 512),
+    "wgrad": (re.compile(r"conv_wgrad_v2<3, 256, 256, 2, 4, 64, 2, false, false>"), 252 * 512),
+}
+RES_FLOP = 2.0 * 32 * 64 * 64 * 256 * 256 * 9     # one res-conv launch, B=32 (154.6 GFLOP)
+SIMDS = 1024
+XCDS = 8
+
+
+def family(name):
+    m = re.search(r"(\w+)(<[^()]*>)?\(", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+
+
+def dom_of(name, grid):
+    return [f for f, (pat, g) in DOMS.items() if pat.search(name) and grid == g]
+
+
+def counters(dirs):
+    """(family, counter) -> [values], ('dom:'+fam, counter) -> [values]"""
+    out = collections.defaultdict(list)
+    for d in dirs:
+        for p in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(p)):
+                v = float(r["Counter_Value"])
+                c = r["Counter_Name"]
+                out[(family(r["Kernel_Name"]), c)].append(v)
+                for f in dom_of(r["Kernel_Name"], int(r.get("Grid_Size", 0) or 0)):
+                    out[("dom:" + f, c)].append(v)
+    return out
+
+
+def durations(d):
+    out = collections.defaultdict(list)
+    for p in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(p)):
+            ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            grid = int(r.get("Grid_Size", 0) or r.get("Grid_Size_X", 0) or 0)
+            out[family(r["Kernel_Name"])].append(ns)
+            for f in dom_of(r["Kernel_Name"], grid):
+                out["dom:" + f].append(ns)
+    return out
+
+
+def mean(v):
+    return sum(v) / len(v) if v else None
+
+
+def summarize(cnt, dur, key):
+    f = mean(cnt.get((key, "FETCH_SIZE"), []))
+    w = mean(cnt.get((key, "WRITE_SIZE"), []))
+    busy = mean(cnt.get((key, "SQ_VALU_MFMA_BUSY_CYCLES"), []))
+    gui = mean(cnt.get((key, "GRBM_GUI_ACTIVE"), []))
+    ns = mean(dur.get(key, []))
+    s = {"dispatches": len(dur.get(key, [])) or len(cnt.get((key, "GRBM_GUI_ACTIVE"), [])),
+         "avg_us": ns / 1e3 if ns else None}
+    if f is not None and w is not None:
+        s["read_bytes"] = 2 * f * 1024
+        s["write_bytes"] = w * 1024
+        s["hbm_bytes_per_launch"] = s["read_bytes"] + s["write_bytes"]
+    if busy is not None and gui:
+        s["mfma_busy_cycles"] = busy
+        s["active_cycles_per_xcd"] = gui / XCDS
+        s["mfma_busy_frac"] = busy / (gui / XCDS * SIMDS)
+        s["executed_mfma_flop"] = busy * 1024
+        if ns:
+            s["eff_clock_ghz"] = gui / XCDS / ns
+    return s
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--pass", dest="passes", action="append", required=True)
+    ap.add_argument("--label", default="bench.py --steps 2 --warmup 1 --cpu-seconds 0")
+    a = ap.parse_args()
+    cnt = counters(a.passes)
+    dur = durations(a.trace)
+    out = {"source": f"rocprofv3 --pmc passes {a.passes} and --kernel-trace {a.trace} over {a.label}",
+           "corrections": __doc__.split("\n\n")[0], "dominant": {}, "families": {}, "step": {}}
+    for fam, (pat, g) in DOMS.items():
+        s = summarize(cnt, dur, "dom:" + fam)
+        s["kernel"] = f"{pat.pattern} grid {g} @64x64 B=32 (res conv {fam})"
+        s["algorithmic_flop"] = RES_FLOP
+        out["dominant"][fam] = s
+    fams = sorted({k for k, _ in cnt if not k.startswith("dom:")} | {k for k in dur if not k.startswith("dom:")})
+    tot_busy = tot_gui = tot_ns = 0.0
+    for k in fams:
+        s = summarize(cnt, dur, k)
+        out["families"][k] = s
+        b = sum(cnt.get((k, "SQ_VALU_MFMA_BUSY_CYCLES"), []))
+        gsum = sum(cnt.get((k, "GRBM_GUI_ACTIVE"), []))
+        tot_busy += b
+        tot_gui += gsum
+        tot_ns += sum(dur.get(k, []))
+    if tot_gui:
+        out["step"] = {"mfma_busy_frac_all_kernels": tot_busy / (tot_gui / XCDS * SIMDS),
+                       "eff_clock_ghz_all_kernels": (tot_gui / XCDS) / tot_ns if tot_ns else None}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
