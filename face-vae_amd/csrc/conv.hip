@@ -2016,6 +2016,194 @@ conv3_halo_wgrad(H3WgArgs a) {
 }
 
 // ----------------------------------------------------------------------------------------
+// Sliding-row weight gradient of a 3x3 conv with 64 input channels (AFE.down1 64 -> 128 at
+// full resolution), each operand byte read from HBM once: a block owns 128 co x ALL 9 taps x
+// 64 ci (= 128 x 576, 36 accumulators per wave) and walks the rows [h0, h1) of one 64-column
+// strip of one image.  Per row h it needs dy row h and x rows h-1, h, h+1; dy rows stream
+// through a 3-deep ring, x rows through a 5-deep ring where each row lands once and stays for
+// the three rows that read it (conv3_halo_wgrad restaged dy per 32-channel k-tile and a fresh
+// 3-row halo per segment: 2.76x the algorithmic bytes).  A "group" i = {dy row h0+i, x row
+// h0+i+1} is issued two rows ahead; a wave's DMAs of a group are counted (wave 0 issues 4 of
+// the 25 pieces, the others 3) so the wait for group i leaves group i+1 in flight.
+//   8 waves = 2 (64 co) x 4 (9 of the 36 k-tiles of 16 = (tap, 16 ci)).
+// Output: slab [block][cout][576] (k = tap * 64 + ci: wgrad_reduce_kernel's layout) and the
+// bias slab [block][cout] (sum of dy by an all-ones MFMA operand, k-wave 0).
+// ----------------------------------------------------------------------------------------
+struct H3Wg2Args {
+  const void* x;
+  const void* dy;
+  float* slab;
+  float* bslab;
+  int H, W, Cout, ldd, nseg, rows, nct;
+  unsigned xbytes, dybytes;
+};
+
+template <int AHEAD>
+__global__ void __launch_bounds__(512, 1)
+conv3_halo_wgrad2(H3Wg2Args a) {
+  // AHEAD groups in flight: group i + AHEAD is issued in row step i (HBM latency under load
+  // is several row steps of MFMA work); rings: dy AHEAD + 1 deep, x AHEAD + 3 deep
+  constexpr int BC = 128, NSD = AHEAD + 1, NSX = AHEAD + 3;
+  constexpr int DYB = 64 * BC * 2;                    // 16 KB, 16 pieces
+  constexpr int XQ = (66 * 128 + 1023) / 1024;        // 9 pieces per x row (66 px x 64 ci)
+  constexpr int XB = XQ * 1024;
+  constexpr int NPC = 16 + XQ;                        // pieces per group (25)
+  __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB];
+  char* dyr = smem;
+  char* xr_ = smem + NSD * DYB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave & 1, wk = wave >> 1;
+  const int li = lane & 15, g = lane >> 4;
+  const int strips = a.W >> 6;
+  const int blk = blockIdx.x;
+  const int tc = blk % a.nct;
+  const int rest = blk / a.nct;
+  const int seg = rest % a.nseg, strip = (rest / a.nseg) % strips, n = rest / (a.nseg * strips);
+  const int co0 = tc * BC, w0 = strip * 64;
+  const int h0 = seg * a.rows, h1 = min(a.H, h0 + a.rows);
+  const int nrow = h1 - h0;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), 0, (int)a.dybytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+
+  // per-lane constants of this wave's pieces: piece q = wave + 8 j of a group (q < 16: dy,
+  // else x piece q - 16); source offsets relative to the row start (0x80000000: outside)
+  const int npw = wave == 0 ? 4 : 3;                  // pieces of a group this wave issues
+  unsigned poff[4];
+  int pisx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = wave + 8 * j;
+    pisx[j] = q >= 16;
+    if (q < 16) {
+      const int o = q * 1024 + lane * 16;
+      const int px = o / (BC * 2), b = o - px * (BC * 2);
+      const int co = ((((b >> 5) ^ tswz<BC>(px)) << 4) | (((b >> 4) & 1) << 3));
+      poff[j] = (unsigned)((px * a.ldd + co0 + co) * 2);          // + row base * ldd * 2
+    } else if (q < NPC) {
+      const int o = (q - 16) * 1024 + lane * 16;
+      const int px = o >> 7, b = o & 127;
+      const int ci = ((((b >> 5) ^ tswz<64>(px)) << 4) | (((b >> 4) & 1) << 3));
+      const int iw = w0 - 1 + px;
+      poff[j] = (px < 66 && iw >= 0 && iw < a.W) ? (unsigned)((iw * 64 + ci) * 2) : 0x80000000u;
+    } else {
+      poff[j] = 0x80000000u;
+    }
+  }
+  // x row y (image row, may be outside) -> ring slot (y - h0 + 1) % NSX; dy row h -> (h - h0) % NSD
+  auto issue_x = [&](int y, int j) {          // the wave's j-th piece when it is an x piece
+    const int slot = (y - h0 + 1) % NSX;
+    const int q = wave + 8 * j - 16;
+    const bool rok = y >= 0 && y < a.H;               // wave-uniform (the column test is in poff)
+    dma16s(xr, sbase + NSD * DYB + slot * XB + q * 1024, rok ? poff[j] : 0x80000000u,
+           rok ? (unsigned)(((n * a.H + y) * a.W) * 64 * 2) : 0u);
+  };
+  auto issue_group = [&](int i) {             // dy row h0 + i, x row h0 + i + 1
+    const int h = h0 + i;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < npw) {
+        if (!pisx[j]) {
+          const int q = wave + 8 * j;
+          dma16s(dr, sbase + (i % NSD) * DYB + q * 1024, poff[j],
+                 (unsigned)((((n * a.H + h) * a.W + w0) * a.ldd) * 2));
+        } else {
+          issue_x(h + 1, j);
+        }
+      }
+    }
+  };
+  auto issue_xonly = [&](int y) {             // prologue rows h0 - 1, h0
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < npw && pisx[j]) issue_x(y, j);
+  };
+
+  issue_xonly(h0 - 1);
+  issue_xonly(h0);
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i)
+    if (i < nrow) issue_group(i);
+  // the wave's k-wave index as a compile-time constant (its 9 k-tiles, and the bias MFMAs of
+  // k-wave 0, then need no registers)
+  with_const<0, 4>(wk, [&](auto wkc) {
+    constexpr int WK = decltype(wkc)::value;
+    constexpr bool BIAS_W = WK == 0;
+    f32x4 acc[4][9];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 9; ++j) acc[q][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 accb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) accb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = BIAS_W && a.bslab;
+    bf16x8 ones;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+    for (int i = 0; i < nrow; ++i) {
+      // group i landed; the younger groups issued so far (up to AHEAD - 1) may stay in flight
+      const int younger = min(AHEAD - 1, nrow - 1 - i);
+      wait_vm_dyn(younger * npw);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (i + AHEAD < nrow) issue_group(i + AHEAD);
+      const char* dys = dyr + (i % NSD) * DYB;
+      const char* xrow[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) xrow[r] = xr_ + ((i + r) % NSX) * XB;     // x rows h - 1, h, h + 1
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) af[q] = tfrag<BC>(dys, kk * 32, wc * 64 + q * 16, lane);
+        // x fragment of k-tile j (tap row / column constant after unrolling); the next one is
+        // read before the current one's 4 MFMAs so the LDS latency hides under them
+        auto xfrag = [&](int j) {
+          const int kt = 9 * WK + j, tap = kt >> 2;
+          return tfrag<64>(xrow[tap / 3], kk * 32 + tap % 3, (kt & 3) * 16, lane);
+        };
+        bf16x8 bcur = xfrag(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          bf16x8 bnext = bcur;
+          if (j + 1 < 9) bnext = xfrag(j + 1);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bcur, acc[q][j], 0, 0, 0);
+          bcur = bnext;
+        }
+        if (do_bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) accb[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], ones, accb[q], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // slab[blk][co][tap * 64 + ci]: lane holds D[co = 4g + jj][k-col = li]
+    float* sl = a.slab + (long)blk / a.nct * a.Cout * 576;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int kt = 9 * WK + j, tap = kt >> 2;
+      const int kcol = tap * 64 + (kt & 3) * 16 + li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) sl[(long)(co0 + wc * 64 + q * 16 + 4 * g + jj) * 576 + kcol] = acc[q][j][jj];
+    }
+    if (do_bias && li == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          a.bslab[(long)(blk / a.nct) * a.Cout + co0 + wc * 64 + q * 16 + 4 * g + jj] = accb[q][jj];
+    }
+  });
+}
+
+// ----------------------------------------------------------------------------------------
 // Weight gradient of the 7x7 64 -> <= 4 channel conv (Generator.out_conv), "row taps in N":
 //   D[(s, ci)][(r, co)] = sum_{x row h, column w} x[h][w + s - 3][ci] * dy[h - r + 3][w][co]
 //                      = dW[co][ci][r][s]
@@ -2761,7 +2949,9 @@ bool use_c7n(const fv_conv_desc* d) {
          (long)d->n * d->h * d->w * 64 * 2 < (1L << 31);
 }
 
-// 3x3 weight gradient with the halo-staged input (conv3_halo_wgrad)
+// 3x3 weight gradient with the halo-staged input: conv3_halo_wgrad2 (sliding rows, default)
+// or conv3_halo_wgrad (FV_H3W_V1=1, for A/B)
+static const int g_h3w_v1 = getenv("FV_H3W_V1") && atoi(getenv("FV_H3W_V1")) != 0;
 static int g_disable_h3w = -1;
 bool use_h3w(const fv_conv_desc* d) {
   if (g_disable_h3w < 0) {
@@ -2881,6 +3071,23 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
     p.CW = 32;
     p.KW = 448;
     p.ntk = p.ntc = 1;
+    return p;
+  }
+  // 3x3 sliding-row wgrad (v2 == 5, conv3_halo_wgrad2): blocks = (image, 64-column strip,
+  // row segment) x co tiles of 128, ~1 block per CU; splits = image x strip x segment
+  if (p.v2 && use_h3w(d) && !g_h3w_v1) {
+    const int strips = d->w / 64;
+    p.v2 = 5;
+    p.ntc = d->cout / 128;
+    p.ntk = 1;
+    int nseg = (256 / p.ntc + d->n * strips / 2) / (d->n * strips);
+    if (nseg < 1) nseg = 1;
+    if (nseg > d->h / 4) nseg = d->h / 4 > 0 ? d->h / 4 : 1;
+    p.sps = fv_cdiv(d->h, nseg);                  // rows per segment
+    p.nsteps = fv_cdiv(d->h, p.sps);              // segments
+    p.nsplit = d->n * strips * p.nsteps;
+    p.CW = d->cout;
+    p.KW = K;
     return p;
   }
   // 3x3 halo wgrad (v2 == 4): tiles of 128 co x (9 taps x 64 ci), ~1 block per CU
@@ -3393,6 +3600,17 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
   const WgPlan t = plan_wgrad(d);
   const int Hin = d->upsample ? d->h / 2 : d->h, Win = d->upsample ? d->w / 2 : d->w;
   const long P = (long)d->n * d->h * d->w;
+  if (t.v2 == 5) {
+    FV_REQUIRE(P * ldy_dy * 2 < (1L << 31) && P * d->cin * 2 < (1L << 31), "wgrad: operand larger than 2 GB");
+    H3Wg2Args a{};
+    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+    a.H = d->h; a.W = d->w; a.Cout = d->cout; a.ldd = ldy_dy;
+    a.nseg = t.nsteps; a.rows = t.sps; a.nct = t.ntc;
+    a.xbytes = (unsigned)(P * d->cin * 2);
+    a.dybytes = (unsigned)(P * ldy_dy * 2);
+    hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    return fv_check_launch("conv2d_bwd_weight_halo3s");
+  }
   if (t.v2 == 4) {
     FV_REQUIRE(P * ldy_dy * 2 < (1L << 31) && P * d->cin * 2 < (1L << 31), "wgrad: operand larger than 2 GB");
     H3WgArgs a{};
