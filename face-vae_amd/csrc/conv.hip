@@ -631,8 +631,8 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     }
   };
   // s_setprio(1) around each MFMA cluster keeps hipcc from moving MFMAs across the raw
-  // barriers into the DMA / fragment-read sections (guide T5); FV_CONV_DBG bit 5 disables it
-  const bool prio = !(a.dbg & 32);
+  // barriers into the DMA / fragment-read sections (guide T5)
+  constexpr bool prio = true;
   auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
     if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -642,7 +642,7 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     if (prio) __builtin_amdgcn_s_setprio(0);
   };
 
-  if (BKS == 64 && !(a.dbg & 8)) {
+  if (BKS == 64) {
     // Software-pipelined k loop: the fragments of the next half-step are read while the
     // MFMAs of the current one run, and the per-step barrier sits between the two MFMA
     // groups of a step, so after it the matrix pipe has the second group (already in
@@ -657,43 +657,38 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     __syncthreads();
     if (nks > 1) issue(1, 1);
     load_frags(fa0, fb0, 0, 0);
-    for (int ks = 0; ks < nks; ++ks) {
+    // steady state without branches around the fragment reads (a read on one path only
+    // makes the compiler drain every LDS read before the next MFMA group)
+    for (int ks = 0; ks + 1 < nks; ++ks) {
       const int buf = ks & 1;
-      if (!(a.dbg & 64)) load_frags(fa1, fb1, buf, 1);    // bit 6: MFMA on stale fragments (experiment)
+      load_frags(fa1, fb1, buf, 1);
       mfma_all(fa0, fb0);
-      if (ks + 1 < nks) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (ks + 2 < nks && !(a.dbg & 2)) issue(ks + 2, buf);
-        if (!(a.dbg & 64)) load_frags(fa0, fb0, buf ^ 1, 0);
-      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (ks + 2 < nks) issue(ks + 2, buf);
+      load_frags(fa0, fb0, buf ^ 1, 0);
       mfma_all(fa1, fb1);
     }
+    load_frags(fa1, fb1, (nks - 1) & 1, 1);
+    mfma_all(fa0, fb0);
+    mfma_all(fa1, fb1);
   } else {
-    // one barrier per step, fragments read per 32-deep half-step (the BKS = 32 loop, and the
-    // reference loop of FV_CONV_DBG bit 3)
+    // one barrier per step, fragments read per 32-deep half-step (the BKS = 32 loop)
     issue(0, 0);
     for (int ks = 0; ks < nks; ++ks) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      const int nxt = (ks + 1 < nks && !(a.dbg & 2)) ? ks + 1 : -1;
-      if (nxt >= 0) issue(nxt, nxt & 1);
-      if (!(a.dbg & 1)) {
+      if (ks + 1 < nks) issue(ks + 1, (ks + 1) & 1);
 #pragma unroll
-        for (int kk = 0; kk < BKS / 32; ++kk) {
-          Frag<bf16> af[RN], bfm[RM];
-          load_frags(af, bfm, ks & 1, kk);
-          mfma_all(af, bfm);
-        }
+      for (int kk = 0; kk < BKS / 32; ++kk) {
+        Frag<bf16> af[RN], bfm[RM];
+        load_frags(af, bfm, ks & 1, kk);
+        mfma_all(af, bfm);
       }
     }
   }
   __syncthreads();
-  if (a.dbg & 4) {   // experiment: skip the epilogue (keep one store so the MFMAs stay live)
-    if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.y)[tid] = acc[RN - 1][RM - 1][3];
-    return;
-  }
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, MODE == 2 ? tm * 4 + phase : tm, wn, wm, lane,
                                              tid);
 }
@@ -822,7 +817,7 @@ conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
     for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nch = a.Cin >> 5, nks = NT * nch;
-  const bool prio = !(a.dbg & 32);
+  constexpr bool prio = true;
   issue_b(0);
   issue_halo(0);
   for (int ks = 0; ks < nks; ++ks) {
@@ -968,7 +963,7 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   for (int i = 0; i < RN; ++i)
 #pragma unroll
     for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool prio = !(a.dbg & 32);
+  constexpr bool prio = true;
   auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
     if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -999,9 +994,12 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   load_frags(fa0, fb0, 0, 0);
   int hn = 2, hstep = (9 * 2 - 10) / 2;         // next halo chunk and the step that issues it
   int bj = 0;                                   // buffer of stage j
+  // No branch around the fragment reads: a read issued on one path only makes the compiler
+  // drain ALL LDS reads (lgkmcnt(0)) before the next MFMA group, exposing the F1 read latency
+  // every step.  An odd last tap re-reads a valid tap and skips its MFMAs.
   for (int j = 0; j < nsteps; ++j) {
     const bool two = 2 * j + 1 < ntap;
-    if (two) load_frags(fa1, fb1, 2 * j + 1, bj);
+    load_frags(fa1, fb1, two ? 2 * j + 1 : 2 * j, bj);
     mfma_all(fa0, fb0);
     const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
     if (j + 1 < nsteps) {

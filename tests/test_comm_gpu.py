@@ -20,15 +20,16 @@ def test_rccl_world1_collectives():
     assert len(uid) == 128 and any(uid)
     comm = D.RcclComm(0, 1, 0, uid)
     try:
-        side = torch.cuda.Stream()
+        # collectives run on the communicator's own stream, fenced against the caller's
+        # stream: a kernel queued just before must be seen, the caller sees the result after
+        # wait_back (SyncBN) or after fence() (gradient buckets)
         for dt in (torch.float32, torch.bfloat16, torch.float64):
-            t = torch.randn(1 << 20, device="cuda").to(dt)
-            ref = t.clone()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                comm.allreduce_(t, op="sum", stream=side)
-                comm.allreduce_(t, op="avg", stream=side)
-            torch.cuda.current_stream().wait_stream(side)
+            t = torch.zeros(1 << 20, device="cuda").to(dt)
+            ref = torch.randn(1 << 20, device="cuda").to(dt)
+            t.copy_(ref)                                      # queued on the caller's stream
+            comm.allreduce_(t, op="sum")                      # wait_back=True
+            comm.allreduce_(t, op="avg", wait_back=False)
+            comm.fence()
             assert torch.equal(t, ref), dt                   # one rank: sum and avg are identities
         b = torch.arange(1000, dtype=torch.float32, device="cuda")
         comm.broadcast_(b, 0)
