@@ -27,6 +27,7 @@ from facevae_amd import ops  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2516.6   # 256 CU x 2.4 GHz x 4096 FLOP/clk (dense), MI355X_MICROARCH.md
 PEAK_F32_TFLOPS = 157.3
+PEAK_FP8_TFLOPS = 5033.2    # dense e4m3 (scaled 16x16x128: 2x bf16 per clock), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 
 
@@ -37,7 +38,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32, help="images per GPU")
     ap.add_argument("--res", type=int, default=256)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8: the 3x3 128-multiple-channel convs' fwd + dgrad on e4m3 (config C5)")
     ap.add_argument("--no-syncbn", action="store_true", help="per-rank BN statistics (labelled)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
@@ -134,7 +136,7 @@ def main():
     if world > 1:
         fv.distributed.init_dist(local, world, syncbn=not args.no_syncbn)
     torch.cuda.set_device(local)
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp8": torch.float8_e4m3fn}[args.dtype]
     cfg = fv.FaceVAEConfig(H=args.res)
     torch.manual_seed(0)
     model = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(dtype)
@@ -194,7 +196,8 @@ def main():
     f_launch = 2.0 * P * res_c * res_c * 9
     fam = {k: sum(v) / len(v) for k, v in ev.items() if v}
     dom = max(fam, key=lambda k: fam[k] * len(ev[k])) if fam else None
-    peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
+    peak = {torch.bfloat16: PEAK_BF16_TFLOPS, torch.float32: PEAK_F32_TFLOPS,
+            torch.float8_e4m3fn: PEAK_FP8_TFLOPS}[dtype]
     roof = None
     if dom is not None:
         ach = f_launch / (fam[dom] * 1e-3) / 1e12

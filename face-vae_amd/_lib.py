@@ -60,6 +60,17 @@ _SIGS = {
     "fv_convt_supported": (c_int, [D]),
     "fv_convt_weight_prep": (c_int, [D, P, c_int, c_float, P, P, P, P]),
     "fv_convt_wgrad_reduce": (c_int, [D, P, P, P, c_int, c_float, P, P, P, P]),
+    "fv_fp8_ws_bytes": (c_size_t, []),
+    "fv_quantize_fp8": (c_int, [c_int, P, c_long, P, P, P, P]),
+    "fv_conv2d_fp8_supported": (c_int, [D]),
+    "fv_conv_fp8_wk_bytes": (c_size_t, [D]),
+    "fv_conv_fp8_wt_bytes": (c_size_t, [D]),
+    "fv_conv_weight_prep_fp8": (c_int, [D, P, P, P, P, P, P, P]),
+    "fv_conv2d_fwd_fp8": (c_int, [D, P, P, P, P, P, P, P, P, P]),
+    "fv_conv2d_bwd_data_fp8": (c_int, [D, P, P, P, P, P, P]),
+    "fv_conv2d_fp8_stats_blocks": (c_int, [D]),
+    "fv_conv2d_fp8_stats_block_pixels": (c_int, [D]),
+    "fv_fp8_mfma_probe": (c_int, [P, P, P, P]),
     "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),
     "fv_spectral_norm_fwd": (c_int, [P, c_int, c_int, P, P, P, c_int, P, P]),
     "fv_spectral_norm_bwd": (c_int, [P, P, c_int, c_int, P, P, P, P, P, P]),

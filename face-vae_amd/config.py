@@ -13,11 +13,16 @@ def compute_dtype() -> torch.dtype:
     return _COMPUTE_DTYPE
 
 
+COMPUTE_MODES = (torch.float32, torch.bfloat16, torch.float8_e4m3fn)
+
+
 def set_compute_dtype(dtype: torch.dtype) -> None:
-    """torch.float32 = exact-fp32 MFMA parity mode; torch.bfloat16 = bf16 MFMA (default)."""
+    """torch.float32 = exact-fp32 MFMA parity mode; torch.bfloat16 = bf16 MFMA (default);
+    torch.float8_e4m3fn = bf16 activations with the 3x3 convs' forward and data gradient on
+    per-tensor scaled e4m3 operands (BASELINE config C5)."""
     global _COMPUTE_DTYPE
-    if dtype not in (torch.float32, torch.bfloat16):
-        raise ValueError("compute dtype must be torch.float32 or torch.bfloat16")
+    if dtype not in COMPUTE_MODES:
+        raise ValueError("compute dtype must be torch.float32, torch.bfloat16 or torch.float8_e4m3fn")
     _COMPUTE_DTYPE = dtype
 
 

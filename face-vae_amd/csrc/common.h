@@ -104,6 +104,11 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<0x140>(v);   // row_mirror
   return v;
 }
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

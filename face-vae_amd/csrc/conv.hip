@@ -48,6 +48,8 @@ struct ConvArgs {
   int sub;        // 0 = none, else 1 + 2 * pa + pb (set per block)
   int lgw, lghw, Ho, Wo;
   int wphase;     // elements per phase block of the weight buffer (MODE 2)
+  const float* dq0;   // fp8 path: per-tensor dequant factors of the two operands (device)
+  const float* dq1;
 };
 
 // output pixel of tile-space pixel p (identity unless a sub-pixel phase is set)
@@ -3922,6 +3924,401 @@ int fv_convt_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float*
   hipLaunchKernelGGL(convt_weight_bwd_kernel, dim3(d->cout), dim3(64), 0, s, w, demod ? inv : nullptr, gain, dw,
                      d->cin_valid, d->cout);
   return fv_check_launch("convt_weight_bwd");
+}
+
+}  // extern "C"
+
+// ========================================================================================
+// fp8 (OCP e4m3) conv path: per-tensor scaled operands on v_mfma_scale_f32_16x16x128_f8f6f4
+// (BASELINE config C5).  Forward and data gradient of the 3x3 convs with 128-multiple channel
+// counts (ResBlock2D x 12 + Generator.in_conv: 58 % of the step's FLOPs) run on fp8 operands
+// with fp32 accumulation; the weight gradient stays bf16 (its operands, the bf16 activations
+// and gradients, are kept for it anyway).
+//   Scaling: every fp8 tensor carries a power-of-two scale s = 2^floor(log2(448 / amax)) so
+//   that |v * s| <= 448 (e4m3 max); dq = 1 / s is stored on the device and the conv epilogue
+//   multiplies the fp32 accumulators by dq_x * dq_w (exact: powers of two).
+// ========================================================================================
+namespace {
+
+constexpr int FP8_NPART = 1024;   // amax partials (blocks of the amax pass)
+
+__device__ __forceinline__ float pow2_scale_of(float amax) {
+  // largest power of two s with amax * s <= 448
+  if (!(amax > 0.f) || !isfinite(amax)) return 1.f;
+  return exp2f(floorf(log2f(448.f / amax)));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, long n, float* part) {
+  float m = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i * 8 < n; i += (long)gridDim.x * 256) {
+    const long e = i * 8;
+    if (e + 8 <= n) {
+      Chunk8<T> c;
+      c.load(x + e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(c.get(j)));
+    } else {
+      for (long j = e; j < n; ++j) m = fmaxf(m, fabsf(Elt<T>::to_f(x[j])));
+    }
+  }
+  m = wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// every block reduces the partials itself (1024 floats from L2), block 0 publishes dq
+__device__ __forceinline__ float amax_of_parts(const float* part, int np, float* sh) {
+  float m = 0.f;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) m = fmaxf(m, part[i]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float r = 0.f;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r = fmaxf(r, sh[w]);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) quantize_fp8_kernel(const T* __restrict__ x, long n, const float* part, int np,
+                                                           uint8_t* __restrict__ y, float* dq) {
+  __shared__ float sh[4];
+  const float s = pow2_scale_of(amax_of_parts(part, np, sh));
+  if (blockIdx.x == 0 && threadIdx.x == 0) dq[0] = 1.f / s;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i * 8 < n; i += (long)gridDim.x * 256) {
+    const long e = i * 8;
+    if (e + 8 <= n) {
+      Chunk8<T> c;
+      c.load(x + e);
+      uint2 o;
+      o.x = pack4_fp8(c.get(0) * s, c.get(1) * s, c.get(2) * s, c.get(3) * s);
+      o.y = pack4_fp8(c.get(4) * s, c.get(5) * s, c.get(6) * s, c.get(7) * s);
+      *reinterpret_cast<uint2*>(y + e) = o;
+    } else {
+      for (long j = e; j < n; ++j) {
+        const int v = __builtin_amdgcn_cvt_pk_fp8_f32(Elt<T>::to_f(x[j]) * s, 0.f, 0, false);
+        y[j] = (uint8_t)(v & 0xff);
+      }
+    }
+  }
+}
+
+// fp8 weights: wk [rows][9 cin] (k = tap * cin + ci) and / or the transposed, flipped wt
+// [rows_t][9 cout] (k = tap' * cout + co), both scaled by s = pow2 scale of amax(|w| / sigma);
+// dq[0] = 1 / s.  The amax partials of |w| come from amax_kernel<float> over w_param.
+__global__ void __launch_bounds__(256) weight_prep_fp8_kernel(const float* __restrict__ wp, const float* sigma,
+                                                              const float* part, int np, uint8_t* wk, int rows,
+                                                              uint8_t* wt, int rows_t, int cout, int cin, float* dq) {
+  __shared__ float sh[4];
+  const float inv = sigma ? 1.f / sigma[0] : 1.f;
+  const float s = pow2_scale_of(amax_of_parts(part, np, sh) * inv);
+  if (blockIdx.x == 0 && threadIdx.x == 0) dq[0] = 1.f / s;
+  const long nk = wk ? (long)rows * 9 * cin : 0, nt = wt ? (long)rows_t * 9 * cout : 0;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < nk + nt; e += (long)gridDim.x * 256) {
+    float v = 0.f;
+    uint8_t* dst;
+    if (e < nk) {
+      const int row = (int)(e / (9 * cin)), k = (int)(e - (long)row * 9 * cin);
+      const int tap = k / cin, ci = k - tap * cin;
+      if (row < cout) v = wp[((long)row * cin + ci) * 9 + tap];
+      dst = wk + e;
+    } else {
+      const long e2 = e - nk;
+      const int row = (int)(e2 / (9 * cout)), k = (int)(e2 - (long)row * 9 * cout);
+      const int tap = k / cout, co = k - tap * cout;
+      if (row < cin) v = wp[((long)co * cin + row) * 9 + (8 - tap)];
+      dst = wt + e2;
+    }
+    const int q = __builtin_amdgcn_cvt_pk_fp8_f32(v * inv * s, 0.f, 0, false);
+    *dst = (uint8_t)(q & 0xff);
+  }
+}
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mma_f8(const v8i& a, const v8i& b, f32x4 c) {
+  // OCP e4m3 x e4m3 (cbsz = blgp = 0), unit block scales (e8m0 127 = 2^0)
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// one 16 x 16 x 128 tile, fragments in the layout the conv kernel uses: lane (r = l & 15,
+// g = l >> 4) holds k {16g .. 16g+15} U {64+16g .. 64+16g+15} of A row r and of B column r.
+// a [16][128], b [16][128] (b stored column-major: b[col][k]); c [16][16] row-major.
+__global__ void fp8_mfma_probe_kernel(const uint8_t* a, const uint8_t* b, float* c) {
+  const int l = threadIdx.x, r = l & 15, g = l >> 4;
+  v8i fa, fb;
+  const uint4 a0 = *reinterpret_cast<const uint4*>(a + r * 128 + 16 * g);
+  const uint4 a1 = *reinterpret_cast<const uint4*>(a + r * 128 + 64 + 16 * g);
+  const uint4 b0 = *reinterpret_cast<const uint4*>(b + r * 128 + 16 * g);
+  const uint4 b1 = *reinterpret_cast<const uint4*>(b + r * 128 + 64 + 16 * g);
+  fa = v8i{(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+  fb = v8i{(int)b0.x, (int)b0.y, (int)b0.z, (int)b0.w, (int)b1.x, (int)b1.y, (int)b1.z, (int)b1.w};
+  f32x4 acc = mma_f8(fa, fb, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[(4 * g + i) * 16 + r] = acc[i];
+}
+
+// fp8 3x3 conv, halo-staged input (the structure of conv3_halo_fwd with a 128-channel k step):
+//   k step ks = (128-channel chunk c = ks / 9, tap t = ks % 9);
+//   weights stage [BN rows][128 B] (one tap x 128 ci), 16-B chunks XOR swz8(row): fragment
+//   chunks g and 4 + g (the conflict-free pattern of conv_fwd_v2's 128-B rows);
+//   halo of chunk c = two images (ci 0-63 / 64-127) of [(TR+2) x 66 px][64 B], h3swz chunk
+//   swizzle (conflict-free fragment reads from any start), double-buffered across chunks.
+// Block: BN = 128 co x BM = 256 px (4 rows x 64), 8 waves 2 (co) x 4 (px), wave 64 x 64.
+template <int WN, int WM, int RN, int RM>
+__global__ void __launch_bounds__(64 * WN * WM, 1)
+conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
+  constexpr int NW = WN * WM;
+  constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
+  constexpr int HP = (TR + 2) * 66, HQ = (HP + 15) / 16;      // pieces per 64-B halo image
+  constexpr int HALO = 2 * HQ * 1024;                          // both images of one chunk
+  constexpr int QH = 2 * HQ, JH = (QH + NW - 1) / NW;
+  constexpr int BST = BN * 128, QB = BN / 8, JB = QB / NW;
+  static_assert(QB % NW == 0, "weight pieces per wave");
+  constexpr int MAIN = 2 * HALO + 2 * BST, EPI = BM * BN * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tn = lid % a.ntn, tm = lid / a.ntn;
+  const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
+  const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
+  const int co0 = tn * BN;
+  const int p0 = (n * a.H + th * TR) * a.W + tw * 64;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+
+  // halo pieces of this wave: piece q -> image q / HQ, 16 pixels (q % HQ) * 16 + lane / 4,
+  // 16-B chunk lane % 4 (source chunk XOR h3swz)
+  unsigned hoff[JH];
+#pragma unroll
+  for (int j = 0; j < JH; ++j) {
+    const int q = wave + j * NW;
+    const int img = q / HQ, hp = (q - img * HQ) * 16 + (lane >> 2), lchk = lane & 3;
+    const int hr = hp / 66, hc = hp - (hp / 66) * 66;
+    const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
+    const bool ok = q < QH && hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+    hoff[j] = ok ? (unsigned)(((n * a.H + ih) * a.W + iw) * a.Cin + img * 64 + ((lchk ^ h3swz(hp)) << 4))
+                 : 0x80000000u;
+  }
+  const int nh = (QH - wave + NW - 1) / NW;        // halo pieces this wave issues (JH or JH - 1)
+  unsigned wbase[JB];
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    const int row = (wave + j * NW) * 8 + (lane >> 3);
+    wbase[j] = (unsigned)((co0 + row) * a.Kpad + (((lane & 7) ^ swz8(row)) << 4));
+  }
+  auto issue_b = [&](int ks) {
+    const int c = ks / 9, t = ks - c * 9;
+    const unsigned Bs = sbase + 2 * HALO + (ks & 1) * BST;
+    const unsigned k0 = (unsigned)(t * a.Cin + c * 128);
+#pragma unroll
+    for (int j = 0; j < JB; ++j) dma16s(wr, Bs + (wave + j * NW) * 1024, wbase[j], k0);
+  };
+  auto issue_halo = [&](int c) {
+    const unsigned Hs = sbase + (c & 1) * HALO;
+#pragma unroll
+    for (int j = 0; j < JH; ++j)
+      if (j < JH - 1 || wave + j * NW < QH) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], (unsigned)(c * 128));
+  };
+
+  const int lr = lane & 15, lh = lane >> 4;
+  int hpb[RM];
+#pragma unroll
+  for (int m = 0; m < RM; ++m) {
+    const int loc = wm * RM * 16 + m * 16 + lr;
+    hpb[m] = (loc >> 6) * 66 + (loc & 63);
+  }
+  f32x4 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.Cin >> 7, nks = 9 * nch;
+  issue_b(0);
+  issue_halo(0);
+  for (int ks = 0; ks < nks; ++ks) {
+    const int c = ks / 9, t = ks - c * 9;
+    // step 9c+1 may leave the halo of chunk c+1 (issued last, at step 9c) in flight
+    if (t == 1 && c + 1 < nch) {
+      if (nh == JH) wait_vm<JH>();
+      else wait_vm<(JH > 0 ? JH - 1 : 0)>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (ks + 1 < nks) issue_b(ks + 1);
+    if (t == 0 && c + 1 < nch) issue_halo(c + 1);
+    const int r = t / 3, s3 = t - (t / 3) * 3;
+    const char* Hs = smem + (c & 1) * HALO;
+    const char* Bs = smem + 2 * HALO + (ks & 1) * BST;
+    v8i fa[RN], fb[RM];
+#pragma unroll
+    for (int i = 0; i < RN; ++i) {
+      const int row = wn * RN * 16 + i * 16 + lr;
+      const uint4 u0 = *reinterpret_cast<const uint4*>(Bs + row * 128 + ((lh ^ swz8(row)) << 4));
+      const uint4 u1 = *reinterpret_cast<const uint4*>(Bs + row * 128 + (((4 + lh) ^ swz8(row)) << 4));
+      fa[i] = v8i{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
+    }
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int hp = hpb[m] + r * 66 + s3;
+      const int off = hp * 64 + ((lh ^ h3swz(hp)) << 4);
+      const uint4 u0 = *reinterpret_cast<const uint4*>(Hs + off);
+      const uint4 u1 = *reinterpret_cast<const uint4*>(Hs + HQ * 1024 + off);
+      fb[m] = v8i{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[i][m] = mma_f8(fa[i], fb[m], acc[i][m]);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  const float dq = a.dq0[0] * a.dq1[0];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int m = 0; m < RM; ++m) acc[i][m] *= dq;
+  __syncthreads();
+  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+}
+
+// fp8 conv eligibility: 3x3, stride 1, 'same', channel counts multiples of 128 (in and out),
+// W % 64 == 0, H % 4 == 0, bf16 NHWC output, operands < 2 GB
+bool fp8_ok(const fv_conv_desc* d) {
+  return d->ksize == 3 && !d->upsample && !d->pro_act && !d->epi_sigmoid && !d->out_nchw_f32 && d->cin % 128 == 0 &&
+         d->cin_valid == d->cin && d->cout % 128 == 0 && d->ldy == d->cout && d->w % 64 == 0 && d->h % 4 == 0 &&
+         (long)d->n * d->h * d->w * d->cin < (1L << 31) && (long)d->n * d->h * d->w * d->cout * 2 < (1L << 31);
+}
+
+int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, const float* dq_x, const uint8_t* w8,
+                 const float* dq_w, const float* bias, const void* res, void* y, float* stats, hipStream_t s) {
+  ConvArgs a{};
+  a.x = x8; a.w = w8; a.bias = bias; a.res = res; a.y = y; a.stats = stats;
+  a.dq0 = dq_x; a.dq1 = dq_w;
+  a.N = d->n; a.H = d->h; a.W = d->w; a.Hin = d->h; a.Win = d->w;
+  a.P = d->n * d->h * d->w;
+  a.Cin = cin; a.lgCin = fv_ilog2(cin);
+  a.Cout = cout; a.ldy = cout;
+  a.K = 9 * cin; a.Kpad = 9 * cin;
+  a.lgtw = 6;
+  a.ntn = cout / 128;
+  const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
+  const unsigned xb = (unsigned)((long)d->n * d->h * d->w * cin);
+  hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+  return fv_check_launch("conv2d_fp8");
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t fv_fp8_ws_bytes(void) { return FP8_NPART * sizeof(float); }
+
+int fv_quantize_fp8(int dtype_in, const void* x, long count, uint8_t* y, float* dq, void* ws, void* stream) {
+  FV_REQUIRE(x && y && dq && ws && count > 0, "quantize_fp8: bad args");
+  FV_REQUIRE(dtype_in == FV_BF16 || dtype_in == FV_F32, "quantize_fp8: input must be bf16 or f32");
+  hipStream_t s = (hipStream_t)stream;
+  const long chunks = (count + 7) / 8;
+  const int nb = (int)std::min<long>(FP8_NPART, std::max<long>(1, (chunks + 255) / 256));
+  if (dtype_in == FV_BF16) {
+    hipLaunchKernelGGL(amax_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)x, count, (float*)ws);
+    hipLaunchKernelGGL(quantize_fp8_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)x, count, (const float*)ws,
+                       nb, y, dq);
+  } else {
+    hipLaunchKernelGGL(amax_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)x, count, (float*)ws);
+    hipLaunchKernelGGL(quantize_fp8_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)x, count,
+                       (const float*)ws, nb, y, dq);
+  }
+  return fv_check_launch("quantize_fp8");
+}
+
+int fv_conv2d_fp8_supported(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  return fp8_ok(d) ? 1 : 0;
+}
+
+size_t fv_conv_fp8_wk_bytes(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK || !fp8_ok(d)) return 0;
+  return (size_t)d->cout * 9 * d->cin;
+}
+
+size_t fv_conv_fp8_wt_bytes(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK || !fp8_ok(d)) return 0;
+  return (size_t)d->cin * 9 * d->cout;
+}
+
+int fv_conv_weight_prep_fp8(const fv_conv_desc* d, const float* w_param, const float* sigma, uint8_t* wk,
+                            uint8_t* wt, float* dq, void* ws, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fp8_ok(d), "fp8 conv: unsupported descriptor (k=%d cin=%d cout=%d %dx%d)", d->ksize, d->cin, d->cout,
+             d->h, d->w);
+  FV_REQUIRE(w_param && (wk || wt) && dq && ws, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const long nw = (long)d->cout * d->cin * 9;
+  const int nb = (int)std::min<long>(FP8_NPART, std::max<long>(1, (nw / 8 + 255) / 256));
+  hipLaunchKernelGGL(amax_kernel<float>, dim3(nb), dim3(256), 0, s, w_param, nw, (float*)ws);
+  const long tot = (wk ? nw : 0) + (wt ? nw : 0);
+  const int nb2 = (int)std::min<long>(2048, fv_cdiv(tot, 256));
+  hipLaunchKernelGGL(weight_prep_fp8_kernel, dim3(nb2), dim3(256), 0, s, w_param, sigma, (const float*)ws, nb, wk,
+                     d->cout, wt, d->cin, d->cout, d->cin, dq);
+  return fv_check_launch("weight_prep_fp8");
+}
+
+int fv_conv2d_fwd_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_dq, const uint8_t* wk,
+                      const float* w_dq, const float* bias, const void* res, void* y, float* stats, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fp8_ok(d), "fp8 conv: unsupported descriptor");
+  FV_REQUIRE(x8 && x_dq && wk && w_dq && y, "null pointer");
+  FV_REQUIRE(!(res && stats), "fp8 conv: residual and BN statistics in one call are not supported");
+  return conv_fp8_run(d, d->cin, d->cout, x8, x_dq, wk, w_dq, bias, res, y, stats, (hipStream_t)stream);
+}
+
+int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const float* dy_dq, const uint8_t* wt,
+                           const float* wt_dq, void* dx, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fp8_ok(d), "fp8 conv: unsupported descriptor");
+  FV_REQUIRE(dy8 && dy_dq && wt && wt_dq && dx, "null pointer");
+  return conv_fp8_run(d, d->cout, d->cin, dy8, dy_dq, wt, wt_dq, nullptr, nullptr, dx, nullptr, (hipStream_t)stream);
+}
+
+// BN-statistics records of fv_conv2d_fwd_fp8: one per wave row of the 128 co x 256 px tile
+// (WM = 4 rows of 64 pixels)
+int fv_conv2d_fp8_stats_block_pixels(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK || !fp8_ok(d)) return 0;
+  return 64;
+}
+
+int fv_conv2d_fp8_stats_blocks(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK || !fp8_ok(d)) return 0;
+  return fv_cdiv((long)d->n * d->h * d->w, 64);
+}
+
+int fv_fp8_mfma_probe(const uint8_t* a, const uint8_t* b, float* c, void* stream) {
+  FV_REQUIRE(a && b && c, "null pointer");
+  hipLaunchKernelGGL(fp8_mfma_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, c);
+  return fv_check_launch("fp8_mfma_probe");
 }
 
 }  // extern "C"

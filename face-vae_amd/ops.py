@@ -25,6 +25,24 @@ from ._lib import call, ptr, query, stream
 CL = torch.channels_last
 F32 = torch.float32
 F64 = torch.float64
+# fp8 compute mode (BASELINE config C5): activations and gradients stay bf16 in HBM; the 3x3
+# convs the fp8 kernels support run forward and data gradient on per-tensor scaled OCP e4m3
+# operands (fv_*_fp8), everything else as in bf16 mode
+FP8 = torch.float8_e4m3fn
+
+
+def storage(mode: torch.dtype) -> torch.dtype:
+    """HBM dtype of activations / gradients for a compute mode."""
+    return torch.bfloat16 if mode == FP8 else mode
+
+
+def quantize_fp8(t: torch.Tensor):
+    """(uint8 e4m3 copy of a dense tensor, dq = 1 / scale as a 1-element device tensor)."""
+    y = _empty(t.numel(), torch.uint8, t.device)
+    dq = _empty(1, F32, t.device)
+    ws = _empty(query("fv_fp8_ws_bytes") // 4, F32, t.device)
+    call("fv_quantize_fp8", L.dtype_code(t.dtype), ptr(t), t.numel(), ptr(y), ptr(dq), ptr(ws), stream())
+    return y, dq
 
 
 def pad_pow2(c: int) -> int:
@@ -183,9 +201,11 @@ class SNBatch:
 
 
 class ConvState:
-    """Per-forward state of one conv: descriptor, prepared weights, SN snapshot."""
+    """Per-forward state of one conv: descriptor, prepared weights, SN snapshot.  With fp8
+    (and a descriptor the fp8 kernels support) the prepared weights are e4m3 with one
+    per-tensor scale (wdq) and forward / data gradient run on the fp8 kernels."""
 
-    def __init__(self, conv, d, dtype, device, training, need_wt):
+    def __init__(self, conv, d, dtype, device, training, need_wt, fp8=False):
         self.conv = conv
         self.d = d
         w = conv.weight_param()
@@ -202,6 +222,15 @@ class ConvState:
                 self.sigma = spectral_norm_fwd(w, conv.weight_u, conv.weight_v, training)
                 self.u = conv.weight_u.clone()
                 self.v = conv.weight_v.clone()
+        self.fp8 = bool(fp8) and bool(query("fv_conv2d_fp8_supported", ctypes.byref(d)))
+        if self.fp8:
+            self.wk = _empty(query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), torch.uint8, device)
+            self.wt = _empty(query("fv_conv_fp8_wt_bytes", ctypes.byref(d)), torch.uint8, device) if need_wt else None
+            self.wdq = _empty(1, F32, device)
+            ws = _empty(query("fv_fp8_ws_bytes") // 4, F32, device)
+            call("fv_conv_weight_prep_fp8", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
+                 ptr(self.wdq), ptr(ws), stream())
+            return
         self.wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
         self.wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if need_wt else None
         call("fv_conv_weight_prep", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
@@ -211,13 +240,28 @@ class ConvState:
         self.wk = None
 
 
+def stats_geometry(cs: ConvState):
+    """(records, pixels per record) of the BN partials the forward launch of cs writes."""
+    d = ctypes.byref(cs.d)
+    if cs.fp8:
+        return query("fv_conv2d_fp8_stats_blocks", d), query("fv_conv2d_fp8_stats_block_pixels", d)
+    return query("fv_conv2d_stats_blocks", d), query("fv_conv2d_stats_block_pixels", d)
+
+
 def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False):
     d = cs.d
     part = None
     if stats:
-        nb = query("fv_conv2d_stats_blocks", ctypes.byref(d))
+        nb, _ = stats_geometry(cs)
         part = _empty(nb * 2 * d.cout, F32, x.device)
     psc, psh = (pro if pro is not None else (None, None))
+    if cs.fp8:
+        x8, xdq = quantize_fp8(x)
+        _timed("fwd", d, lambda: call("fv_conv2d_fwd_fp8", ctypes.byref(d), ptr(x8), ptr(xdq), ptr(cs.wk),
+                                      ptr(cs.wdq), ptr(bias), ptr(res), ptr(y), ptr(part), stream()))
+        if CHECK is not None:
+            CHECK("fwd", cs, x=x, bias=bias, pro=pro, res=res, y=y, q8=(x8, xdq))
+        return part
     _timed("fwd", d, lambda: call("fv_conv2d_fwd", ctypes.byref(d), ptr(x), ptr(cs.wk), ptr(bias), ptr(psc),
                                   ptr(psh), ptr(res), ptr(y), ptr(part), stream()))
     if CHECK is not None:
@@ -242,6 +286,14 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
     if cs.conv.sn:
         spectral_norm_bwd(cs.w, dw, cs.u, cs.v, cs.sigma)
     dx = None
+    if need_dx and cs.fp8:
+        dy8, dydq = quantize_fp8(dy)
+        dx = torch.empty((d.n, d.cin, d.h, d.w), dtype=dy.dtype, device=dev, memory_format=CL)
+        _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data_fp8", ctypes.byref(d), ptr(dy8), ptr(dydq), ptr(cs.wt),
+                                        ptr(cs.wdq), ptr(dx), stream()))
+        if CHECK is not None:
+            CHECK("dgrad", cs, dy=dy, ldd=ldd, dx=dx, q8=(dy8, dydq))
+        return dx, dw, db
     if need_dx and d.upsample and query("fv_conv2d_dgrad_lowres", ctypes.byref(d)):
         # gradient of the upsample's (low-res) input in one stride-2 pass
         dx = torch.empty((d.n, d.cin, d.h // 2, d.w // 2), dtype=dy.dtype, device=dev, memory_format=CL)
@@ -308,12 +360,12 @@ def _sync(stats, comm):
         comm.allreduce_(stats, op="sum", wait_back=True)
 
 
-def bn_from_partials(bn, part, d, training, comm):
+def bn_from_partials(bn, part, cs, training, comm):
+    d = cs.d
     C = d.cout
     dev = part.device
     P = d.n * d.h * d.w
-    nb = query("fv_conv2d_stats_blocks", ctypes.byref(d))
-    bp = query("fv_conv2d_stats_block_pixels", ctypes.byref(d))
+    nb, bp = stats_geometry(cs)
     ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, dev)
     if comm is None:
         # single process: statistics + finalize in two launches
@@ -412,7 +464,8 @@ class ConvBNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, blk):
-        dtype = blk.compute_dtype()
+        mode = blk.compute_dtype()
+        dtype = storage(mode)
         conv, bn = blk.conv, blk.bn
         xb, cin_pad = to_nhwc(x, dtype)
         N, _, Hi, Wi = x.shape
@@ -422,11 +475,11 @@ class ConvBNActFn(torch.autograd.Function):
             raise RuntimeError("CNA block output channels must be a multiple of 8")
         training = blk.training
         d = desc(dtype, N, H, W, cin_pad, conv.in_channels, cout, cout, conv.kernel_size, ups=blk.upsample)
-        cs = ConvState(conv, d, dtype, x.device, training, need_wt=ctx.needs_input_grad[0])
+        cs = ConvState(conv, d, dtype, x.device, training, need_wt=ctx.needs_input_grad[0], fp8=mode == FP8)
         y = torch.empty((N, cout, H, W), dtype=dtype, device=x.device, memory_format=CL)
         part = conv_forward(cs, xb, bias, y=y, stats=training)
         comm = blk.bn_comm()
-        r = bn_from_partials(bn, part, d, True, comm) if training else bn_finalize(bn, None, 0, False)
+        r = bn_from_partials(bn, part, cs, True, comm) if training else bn_finalize(bn, None, 0, False)
         z = bn_act_forward(y, r, blk.slope, blk.pool, bn)
         cs.release()
         ctx.blk, ctx.cs, ctx.r, ctx.comm = blk, cs, r, comm
@@ -451,7 +504,8 @@ class ResBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, blk):
-        dtype = blk.compute_dtype()
+        mode = blk.compute_dtype()
+        dtype = storage(mode)
         xb, C = to_nhwc(x, dtype)
         if C != x.shape[1]:
             raise RuntimeError("ResBlock2D channels must be a power of two >= 8")
@@ -462,13 +516,13 @@ class ResBlockFn(torch.autograd.Function):
         r1 = bn_from_tensor(blk.bn1, xb, training, comm)
         a1 = bn_act_forward(xb, r1, 0.0, False, blk.bn1)
         d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size)
-        cs1 = ConvState(c1, d1, dtype, x.device, training, True)
+        cs1 = ConvState(c1, d1, dtype, x.device, training, True, fp8=mode == FP8)
         t1 = torch.empty_like(xb)
         part = conv_forward(cs1, a1, b1, y=t1, stats=training)
-        r2 = bn_from_partials(blk.bn2, part, d1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
+        r2 = bn_from_partials(blk.bn2, part, cs1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
         a2 = bn_act_forward(t1, r2, 0.0, False, blk.bn2)
         d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size)
-        cs2 = ConvState(c2, d2, dtype, x.device, training, True)
+        cs2 = ConvState(c2, d2, dtype, x.device, training, True, fp8=mode == FP8)
         out = torch.empty_like(xb)
         conv_forward(cs2, a2, b2, res=xb, y=out)
         cs1.release()
@@ -496,7 +550,8 @@ class NACFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, blk):
-        dtype = blk.compute_dtype()
+        mode = blk.compute_dtype()
+        dtype = storage(mode)
         xb, C = to_nhwc(x, dtype)
         if C != x.shape[1]:
             raise RuntimeError("NAC block input channels must be a power of two >= 8")
@@ -509,7 +564,7 @@ class NACFn(torch.autograd.Function):
         r = bn_from_tensor(blk.bn, xb, blk.training, comm)
         a = bn_act_forward(xb, r, blk.slope, False, blk.bn)
         d = desc(dtype, N, H, W, C, C, cout, cout, conv.kernel_size)
-        cs = ConvState(conv, d, dtype, x.device, blk.training, need_wt=True)
+        cs = ConvState(conv, d, dtype, x.device, blk.training, need_wt=True, fp8=mode == FP8)
         y = torch.empty((N, cout, H, W), dtype=dtype, device=x.device, memory_format=CL)
         conv_forward(cs, a, bias, y=y)
         cs.release()
@@ -532,13 +587,14 @@ class ConvFn(torch.autograd.Function):
     """Plain nn.Conv2d (+ optional fused sigmoid with NCHW fp32 output: models.py:1099,1110)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, conv, dtype, sigmoid):
+    def forward(ctx, x, weight, bias, conv, mode, sigmoid):
+        dtype = storage(mode)
         xb, cin_pad = to_nhwc(x, dtype)
         N, _, H, W = x.shape
         cout = conv.out_channels
         nchw = bool(sigmoid) or (cout % 8 != 0)
         d = desc(dtype, N, H, W, cin_pad, conv.in_channels, cout, cout, conv.kernel_size, sig=sigmoid, nchw=nchw)
-        cs = ConvState(conv, d, dtype, x.device, conv.training, need_wt=ctx.needs_input_grad[0])
+        cs = ConvState(conv, d, dtype, x.device, conv.training, need_wt=ctx.needs_input_grad[0], fp8=mode == FP8)
         if nchw:
             y = torch.empty((N, cout, H, W), dtype=F32, device=x.device)
         else:
@@ -685,7 +741,8 @@ def kl_loss(mu, logstd):
     return KLFn.apply(mu, logstd)
 
 
-def reparameterise(h, eps, dtype):
+def reparameterise(h, eps, mode):
+    dtype = storage(mode)
     holder = {}
     mu, ls, z = ReparamFn.apply(h, eps, dtype, holder)
     mu._fv_kl = (ls, holder["kl"], mu._version, ls._version)

@@ -133,6 +133,37 @@ int fv_convt_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float*
                           const float* w, int demod, float gain, const float* inv, float* dw,
                           float* db, void* stream);
 
+/* ------------------------------------------------- fp8 conv path (config C5) ---- */
+/* OCP e4m3 operands with per-tensor power-of-two scales: a tensor v is stored as
+ * fp8(v * s), s = 2^floor(log2(448 / amax|v|)), with dq = 1 / s (a device float) beside it.
+ * fv_conv2d_fwd_fp8 / fv_conv2d_bwd_data_fp8 are the forward and data gradient of a 3x3 conv
+ * (fv_conv2d_fp8_supported: channel counts multiples of 128, w % 64 == 0, h % 4 == 0) on
+ * v_mfma_scale_f32_16x16x128_f8f6f4 with fp32 accumulation, the epilogue multiplying by
+ * dq_x * dq_w; output bf16 NHWC as fv_conv2d_fwd (bias, residual, BN partials alike).  They
+ * replace the same F.conv2d calls as fv_conv2d_fwd / fv_conv2d_bwd_data (modules.py:32). */
+size_t fv_fp8_ws_bytes(void);
+/* y[i] = fp8(x[i] * s) for count elements (bf16 or f32 input), dq[0] = 1 / s */
+int fv_quantize_fp8(int dtype_in, const void* x, long count, uint8_t* y, float* dq, void* ws,
+                    void* stream);
+int fv_conv2d_fp8_supported(const fv_conv_desc* d);
+size_t fv_conv_fp8_wk_bytes(const fv_conv_desc* d);
+size_t fv_conv_fp8_wt_bytes(const fv_conv_desc* d);
+/* w_param [cout][cin][3][3] fp32 (/ sigma when given) -> wk [cout][9 cin] and/or the
+ * transposed, flipped wt [cin][9 cout] (k = tap * channels + c), one scale: dq[0] */
+int fv_conv_weight_prep_fp8(const fv_conv_desc* d, const float* w_param, const float* sigma,
+                            uint8_t* wk, uint8_t* wt, float* dq, void* ws, void* stream);
+int fv_conv2d_fwd_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_dq, const uint8_t* wk,
+                      const float* w_dq, const float* bias, const void* res, void* y, float* stats,
+                      void* stream);
+/* BN partial records written by fv_conv2d_fwd_fp8 (as fv_conv2d_stats_blocks / _pixels) */
+int fv_conv2d_fp8_stats_blocks(const fv_conv_desc* d);
+int fv_conv2d_fp8_stats_block_pixels(const fv_conv_desc* d);
+/* dx [n][h][w][cin] bf16 from dy8 [n][h][w][cout] fp8 and wt */
+int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const float* dy_dq,
+                           const uint8_t* wt, const float* wt_dq, void* dx, void* stream);
+/* layout probe: c[16][16] = a[16][128] . b[16][128]^T through one scaled fp8 MFMA tile */
+int fv_fp8_mfma_probe(const uint8_t* a, const uint8_t* b, float* c, void* stream);
+
 /* ------------------------------------------------------------- spectral norm ---- */
 size_t fv_spectral_norm_ws_bytes(int rows, int cols);
 /* one power iteration (u, v updated in place) when power_iter, then sigma = u.(W v) */

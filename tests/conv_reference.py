@@ -179,7 +179,7 @@ class LaunchChecker:
     def __init__(self, model, dtype):
         from facevae_amd import _lib as L
         import ctypes
-        self.dtype = dtype
+        self.dtype = torch.bfloat16 if dtype == torch.float8_e4m3fn else dtype
         # which formulation the library runs for an upsample conv (the sub-pixel phases have a
         # 4 x [rows][Kpad(2x2)] weight buffer; the low-res data gradient is reported directly)
         def subpix(d):
@@ -259,7 +259,27 @@ class LaunchChecker:
         w = eff_weight(cs, self.dtype)
         bf = self.dtype == torch.bfloat16
         with torch.no_grad():
-            if kind == "fwd":
+            if kind == "fwd" and t.get("q8") is not None:        # fp8 kernel: dequantized operands
+                x8, xdq = t["q8"]
+                N, Cp, H, W = t["x"].shape
+                xq = x8.view(torch.float8_e4m3fn).float().view(N, H, W, Cp).permute(0, 3, 1, 2) * xdq
+                wq = cs.wk.view(torch.float8_e4m3fn).float().view(d.cout, 3, 3, d.cin).permute(0, 3, 1, 2) * cs.wdq
+                ref = conv_fwd_ref(xq.contiguous(), wq.contiguous(), t["bias"], 3, False)
+                aux = None
+                if t.get("res") is not None:
+                    aux = t["res"][:, :d.cout].float()
+                    ref = ref + aux
+                rl2, worst = compare(t["y"][:, :d.cout].float(), ref, aux, out_bf16=True)
+                self._add(name, "fwd8", d, rl2, worst)
+            elif kind == "dgrad" and t.get("q8") is not None:
+                dy8, dydq = t["q8"]
+                N, Co, H, W = t["dy"].shape
+                dyq = dy8.view(torch.float8_e4m3fn).float().view(N, H, W, Co).permute(0, 3, 1, 2) * dydq
+                wtq = cs.wt.view(torch.float8_e4m3fn).float().view(d.cin, 3, 3, d.cout).permute(0, 3, 1, 2) * cs.wdq
+                ref = conv_fwd_ref(dyq.contiguous(), wtq.contiguous(), None, 3, False)
+                rl2, worst = compare(t["dx"].float(), ref, out_bf16=True)
+                self._add(name, "dgrad8", d, rl2, worst)
+            elif kind == "fwd":
                 x = t["x"][:, :d.cin_valid].float()
                 x = pro_input(x, t.get("pro"), d.pro_slope, self.dtype)
                 if ups and self.subpix(d):

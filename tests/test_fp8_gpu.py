@@ -1,0 +1,111 @@
+"""fp8 (OCP e4m3) conv path (BASELINE config C5): conversion, the scaled-MFMA fragment layout,
+and the fp8 forward / data-gradient conv kernels against torch fp32 on the dequantized
+operands (the products of two e4m3 values are exact in fp32, so kernel and reference differ
+only by fp32 summation order and the bf16 rounding of the output)."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+import facevae_amd as fv  # noqa: E402
+from facevae_amd import _lib as L  # noqa: E402
+from facevae_amd import ops  # noqa: E402
+
+CL = torch.channels_last
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def quant(x):
+    """library quantization of a contiguous bf16/f32 tensor -> (uint8 tensor, dq tensor)"""
+    y = torch.empty(x.numel(), dtype=torch.uint8, device="cuda")
+    dq = torch.empty(1, device="cuda")
+    ws = torch.empty(L.query("fv_fp8_ws_bytes") // 4, device="cuda")
+    L.call("fv_quantize_fp8", L.dtype_code(x.dtype), x.data_ptr(), x.numel(), y.data_ptr(), dq.data_ptr(),
+           ws.data_ptr(), L.stream())
+    return y, dq
+
+
+def deq(y8, dq, shape):
+    return y8.view(torch.float8_e4m3fn).float().view(shape) * dq
+
+
+def test_quantize_matches_torch_e4m3():
+    g = torch.Generator().manual_seed(1)
+    x = (torch.randn(100003, generator=g) * 3.7).cuda()
+    x[17] = 0.0
+    y8, dq = quant(x)
+    torch.cuda.synchronize()
+    s = 1.0 / dq.item()
+    amax = x.abs().max().item()
+    assert s * amax <= 448 and s * amax > 224 and s == 2.0 ** round(torch.log2(torch.tensor(s)).item())
+    ref = (x * s).to(torch.float8_e4m3fn)            # torch: OCP e4m3fn, round to nearest even
+    assert torch.equal(y8.view(torch.float8_e4m3fn).view(torch.uint8), ref.view(torch.uint8))
+
+
+def test_fp8_mfma_fragment_layout():
+    g = torch.Generator().manual_seed(2)
+    a = torch.randn(16, 128, generator=g).to(torch.float8_e4m3fn)
+    b = torch.randn(16, 128, generator=g).to(torch.float8_e4m3fn)
+    c = torch.empty(16, 16, device="cuda")
+    ac, bc = a.view(torch.uint8).cuda(), b.view(torch.uint8).cuda()
+    L.call("fv_fp8_mfma_probe", ac.data_ptr(), bc.data_ptr(), c.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    ref = a.double() @ b.double().t()
+    assert rel(c, ref) < 1e-4      # (the 128-term sum inside the scaled MFMA: ~1e-5 relative)
+
+
+CASES = [(256, 256, 8, 64, 2), (128, 256, 4, 128, 2), (256, 128, 12, 64, 1), (256, 256, 64, 64, 32)]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_conv_fp8_fwd_and_dgrad(case):
+    cin, cout, H, W, N = case
+    g = torch.Generator().manual_seed(3 + cin + H)
+    x = torch.randn(N, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    b = torch.randn(cout, generator=g)
+    dy = torch.randn(N, cout, H, W, generator=g)
+    xb = x.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    d = ops.desc(torch.bfloat16, N, H, W, cin, cin, cout, cout, 3)
+    assert L.query("fv_conv2d_fp8_supported", ctypes.byref(d))
+    x8, xdq = quant(xb)
+    wk = torch.empty(L.query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), dtype=torch.uint8, device="cuda")
+    wt = torch.empty(L.query("fv_conv_fp8_wt_bytes", ctypes.byref(d)), dtype=torch.uint8, device="cuda")
+    wdq = torch.empty(1, device="cuda")
+    ws = torch.empty(L.query("fv_fp8_ws_bytes") // 4, device="cuda")
+    wc = w.cuda().contiguous()
+    L.call("fv_conv_weight_prep_fp8", ctypes.byref(d), wc.data_ptr(), None, wk.data_ptr(), wt.data_ptr(),
+           wdq.data_ptr(), ws.data_ptr(), L.stream())
+    y = torch.empty(N, cout, H, W, dtype=torch.bfloat16, device="cuda", memory_format=CL)
+    nb = L.query("fv_conv2d_stats_blocks", ctypes.byref(d))
+    part = torch.empty(nb * 2 * cout, device="cuda")
+    L.call("fv_conv2d_fwd_fp8", ctypes.byref(d), x8.data_ptr(), xdq.data_ptr(), wk.data_ptr(), wdq.data_ptr(),
+           b.cuda().data_ptr(), None, y.data_ptr(), None, L.stream())
+    # data gradient
+    dyb = dy.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    dy8, dydq = quant(dyb)
+    dx = torch.empty(N, cin, H, W, dtype=torch.bfloat16, device="cuda", memory_format=CL)
+    L.call("fv_conv2d_bwd_data_fp8", ctypes.byref(d), dy8.data_ptr(), dydq.data_ptr(), wt.data_ptr(),
+           wdq.data_ptr(), dx.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    # references on the dequantized fp8 operands (NHWC byte order -> NCHW)
+    xq = deq(x8, xdq, (N, H, W, cin)).permute(0, 3, 1, 2)
+    wq = deq(wk, wdq, (cout, 3, 3, cin)).permute(0, 3, 1, 2)
+    ref = F.conv2d(xq.double().cpu(), wq.double().cpu(), b.double(), padding=1)
+    dyq = deq(dy8, dydq, (N, H, W, cout)).permute(0, 3, 1, 2)
+    refdx = torch.nn.grad.conv2d_input((N, cin, H, W), wq.double().cpu(), dyq.double().cpu(), padding=1)
+    for out, r in ((y, ref), (dx, refdx)):
+        dd = (out.double().cpu() - r).abs()
+        bound = 2.0 ** -7 * r.abs() + 2e-3 * r.pow(2).mean().sqrt()
+        assert (dd / bound).max().item() <= 1.0 and rel(out, r) < 5e-3
+    # the fp8 rounding itself vs the unquantized fp32 conv (reported: ~2^-5 relative per operand)
+    dev = rel(y, F.conv2d(x, w, b, padding=1))
+    print(f"\n[fp8 conv {case}] output rel-L2 vs unquantized fp32 conv: {dev:.3e}")
+    assert dev < 0.1

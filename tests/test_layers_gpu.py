@@ -154,3 +154,26 @@ def test_bn_eval_mode_matches_oracle():
     for k, v in sd.items():                      # eval: no running-stat / SN-buffer update
         if not O.is_param(k):
             assert torch.equal(after[k].cpu(), v.detach().cpu() if v.is_floating_point() else v), k
+
+
+def test_fp8_every_conv_launch_and_step_deviation(oracle_b32):
+    """fp8 mode (config C5's conv path) at 256x256, B=32: the 14 eligible convs (ResBlocks,
+    Generator.in_conv, AFE.down2) run forward and data gradient on e4m3 operands -- each such launch is
+    checked against torch fp32 on the same dequantized operands (fwd8 / dgrad8 rows), every
+    other launch as in bf16 mode; the step's deviation from the fp32 oracle is reported
+    (e4m3: 3 mantissa bits, ~2.6e-2 rel-L2 per conv output) and loosely gated."""
+    x, eps, oo, og, osd = oracle_b32
+    *_, chk = _gpu_step(fv.FaceVAEConfig(), torch.float8_e4m3fn, x, eps,
+                        lambda m: LaunchChecker(m, torch.float8_e4m3fn))
+    print("\n[256x256 B=32 fp8] per-launch deviation\n" + chk.report())
+    kinds = [r["kind"] for r in chk.rows]
+    assert kinds.count("fwd8") == 14 and kinds.count("dgrad8") == 14       # + AFE.down2 (128 -> 256)
+    gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 5e-3, "fwd8": 5e-3, "dgrad8": 5e-3,
+            "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
+    bad = [r for r in chk.rows if not (r["rel_l2"] <= gate[r["kind"]] and r["worst"] <= 1.0)]
+    assert not bad, bad
+    init, y, R, K, grads, state, _ = _gpu_step(fv.FaceVAEConfig(), torch.float8_e4m3fn, x, eps)
+    dev = {"image": rel(y, oo["y"]), "R": abs(R - oo["R"].item()) / oo["R"].item(),
+           "K": abs(K - oo["K"].item()) / abs(oo["K"].item())}
+    print(f"[fp8] 256x256 B=32 one step vs oracle: {dev}")
+    assert dev["image"] < 0.1 and dev["R"] < 2e-2 and dev["K"] < 1e-2

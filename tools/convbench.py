@@ -60,9 +60,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
-    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dtype", default="bf16", help="bf16 | fp32 | fp8 (fp8 rows added for eligible layers)")
     a = ap.parse_args()
-    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    fp8 = a.dtype == "fp8"
+    dtype = torch.bfloat16 if a.dtype in ("bf16", "fp8") else torch.float32
     kinds = a.only.split(",")
     sel = set(a.layers.split(",")) if a.layers else None
     B = a.batch
@@ -89,6 +90,34 @@ def main():
         part = torch.empty(nb * 2 * cout, device="cuda")
         flop = 2.0 * B * H * H * cout * cin * k * k
         row = {"layer": name, "k": k, "cin": cin, "cout": cout, "H": H, "ups": ups, "gflop": flop / 1e9}
+        if fp8 and L.query("fv_conv2d_fp8_supported", ctypes.byref(d)):
+            # fp8 operands (quantized once, outside the timed region) for fwd and dgrad
+            ws = torch.empty(L.query("fv_fp8_ws_bytes") // 4, device="cuda")
+            x8 = torch.empty(x.numel(), dtype=torch.uint8, device="cuda")
+            xdq, wdq, dydq = (torch.empty(1, device="cuda") for _ in range(3))
+            L.call("fv_quantize_fp8", L.dtype_code(dtype), x.data_ptr(), x.numel(), x8.data_ptr(), xdq.data_ptr(),
+                   ws.data_ptr(), L.stream())
+            wk8 = torch.empty(L.query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), dtype=torch.uint8, device="cuda")
+            wt8 = torch.empty(L.query("fv_conv_fp8_wt_bytes", ctypes.byref(d)), dtype=torch.uint8, device="cuda")
+            L.call("fv_conv_weight_prep_fp8", ctypes.byref(d), w.data_ptr(), None, wk8.data_ptr(), wt8.data_ptr(),
+                   wdq.data_ptr(), ws.data_ptr(), L.stream())
+            dyf = (torch.randn(B, cout, H, H, device="cuda") * 0.1).to(dtype).contiguous(memory_format=CL)
+            dy8 = torch.empty(dyf.numel(), dtype=torch.uint8, device="cuda")
+            L.call("fv_quantize_fp8", L.dtype_code(dtype), dyf.data_ptr(), dyf.numel(), dy8.data_ptr(),
+                   dydq.data_ptr(), ws.data_ptr(), L.stream())
+            if "fwd" in kinds:
+                us = timeit(lambda: L.call("fv_conv2d_fwd_fp8", ctypes.byref(d), x8.data_ptr(), xdq.data_ptr(),
+                                           wk8.data_ptr(), wdq.data_ptr(), None, None, y.data_ptr(), part.data_ptr(),
+                                           L.stream()), a.iters)
+                row["fp8_fwd_us"], row["fp8_fwd_tf"] = round(us, 1), round(flop / us / 1e6, 1)
+                us = timeit(lambda: L.call("fv_quantize_fp8", L.dtype_code(dtype), x.data_ptr(), x.numel(),
+                                           x8.data_ptr(), xdq.data_ptr(), ws.data_ptr(), L.stream()), a.iters)
+                row["fp8_quant_us"] = round(us, 1)
+            if "dgrad" in kinds:
+                dxf = torch.empty(B, cp, H, H, dtype=dtype, device="cuda", memory_format=CL)
+                us = timeit(lambda: L.call("fv_conv2d_bwd_data_fp8", ctypes.byref(d), dy8.data_ptr(), dydq.data_ptr(),
+                                           wt8.data_ptr(), wdq.data_ptr(), dxf.data_ptr(), L.stream()), a.iters)
+                row["fp8_dgrad_us"], row["fp8_dgrad_tf"] = round(us, 1), round(flop / us / 1e6, 1)
         if "fwd" in kinds:
             us = timeit(lambda: L.call("fv_conv2d_fwd", ctypes.byref(d), x.data_ptr(), wk.data_ptr(), None, None,
                                        None, None, y.data_ptr(), None if nchw else part.data_ptr(), L.stream()),
