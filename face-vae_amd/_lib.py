@@ -28,6 +28,11 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class Conv3dDesc(ctypes.Structure):
+    _fields_ = [("dtype", c_int), ("n", c_int), ("d", c_int), ("h", c_int), ("w", c_int),
+                ("cin", c_int), ("cout", c_int)]
+
+
 class SnLayer(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("u", c_void_p), ("v", c_void_p), ("sigma", c_void_p), ("usnap", c_void_p),
                 ("vsnap", c_void_p), ("rows", c_int), ("cols", c_int)]
@@ -40,6 +45,7 @@ class AdamTensor(ctypes.Structure):
 
 P = c_void_p
 D = POINTER(ConvDesc)
+D3 = POINTER(Conv3dDesc)
 # name -> (restype, argtypes)
 _SIGS = {
     "fv_abi_version": (c_int, []),
@@ -71,6 +77,15 @@ _SIGS = {
     "fv_conv2d_fp8_stats_blocks": (c_int, [D]),
     "fv_conv2d_fp8_stats_block_pixels": (c_int, [D]),
     "fv_fp8_mfma_probe": (c_int, [P, P, P, P]),
+    "fv_conv3d_wk_bytes": (c_size_t, [D3]),
+    "fv_conv3d_weight_prep": (c_int, [D3, P, P, P, P]),
+    "fv_conv3d_stats_blocks": (c_int, [D3]),
+    "fv_conv3d_stats_block_pixels": (c_int, [D3]),
+    "fv_conv3d_fwd": (c_int, [D3, P, P, P, P, P, P, P]),
+    "fv_conv3d_bwd_data": (c_int, [D3, P, P, P, P]),
+    "fv_conv3d_wgrad_ws_bytes": (c_size_t, [D3]),
+    "fv_conv3d_bwd_weight": (c_int, [D3, P, P, P, P, P, P]),
+    "fv_depth_split": (c_int, [c_int, P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),
     "fv_spectral_norm_fwd": (c_int, [P, c_int, c_int, P, P, P, c_int, P, P]),
     "fv_spectral_norm_bwd": (c_int, [P, P, c_int, c_int, P, P, P, P, P, P]),

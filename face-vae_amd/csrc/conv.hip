@@ -3055,8 +3055,10 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   const int K = d->ksize * d->ksize * d->cin;
   const long P = (long)d->n * d->h * d->w;
   const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
+  // 32-bit buffer offsets: x and dy (channel stride = cout padded to a power of two >= 8, as
+  // every caller passes; fv_conv2d_bwd_weight re-checks the real stride) must stay < 2 GB
   p.v2 = !g_disable_wg2 && d->dtype == FV_BF16 && !d->pro_act && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
-         P * 256 * 2 < (1L << 31);
+         P * pad_pow2_8(d->cout) * 2 < (1L << 31);
   // out_conv 7x7 64 -> <= 4 (v2 == 3): blocks = (image, 64-column strip, row segment), about
   // 4 per CU; slab [block][32 (r, co)][448 (s, ci)]
   if (p.v2 && use_c7w(d)) {

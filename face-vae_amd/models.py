@@ -8,24 +8,24 @@ from torch import nn
 
 from . import config as _config
 from . import ops
-from .modules import Conv2d, ConvBlock2D, DownBlock2D, ResBlock2D, UpBlock2D, _Block
+from . import ops3d
+from .modules import Conv2d, ConvBlock2D, DownBlock2D, ResBlock2D, ResBlock3D, UpBlock2D, _Block
 
 
 class AFE(_Block):
-    """Appearance-feature extractor (models.py:922-945).  The 2-D trunk (in_conv 7x7 CNA,
-    DownBlock2D chain, 1x1 mid_conv) is the FaceVAE encoder.  Its 3-D ResBlock3D trunk is
-    SURVEY.md §8(f) "next #1" and not built yet: n_res must be 0."""
+    """Appearance-feature extractor (models.py:922-945): in_conv 7x7 CNA, DownBlock2D chain,
+    1x1 mid_conv (the 2-D trunk = the FaceVAE encoder), then x.view(N, C, D, H, W) and n_res
+    ResBlock3D(C) (the 3-D trunk).  forward(x) -> [N, C, D, H/4, W/4] in the compute dtype,
+    NDHWC memory (torch.channels_last_3d)."""
 
     def __init__(self, use_weight_norm=False, down_seq=(64, 128, 256), n_res=6, C=32, D=16):
         super().__init__()
-        if n_res != 0:
-            raise NotImplementedError("AFE ResBlock3D trunk (SURVEY.md §8(f) next #1): use n_res=0")
         down_seq = list(down_seq)
         self.in_conv = ConvBlock2D("CNA", 3, down_seq[0], 7, 1, 3, use_weight_norm)
         self.down = nn.Sequential(*[DownBlock2D(down_seq[i], down_seq[i + 1], use_weight_norm)
                                     for i in range(len(down_seq) - 1)])
         self.mid_conv = Conv2d(down_seq[-1], C * D, 1, 1, 0)
-        self.res = nn.Sequential()
+        self.res = nn.Sequential(*[ResBlock3D(C, use_weight_norm) for _ in range(n_res)])
         self.C, self.D = C, D
 
     def forward_2d(self, x):
@@ -33,8 +33,10 @@ class AFE(_Block):
 
     def forward(self, x):
         h = self.forward_2d(x)
-        N, _, H, W = h.shape
-        return h.reshape(N, self.C, self.D, H, W)
+        if not x.is_cuda:
+            raise RuntimeError("facevae_amd ops run on the GPU only (HIP); got a CPU tensor")
+        fs = ops3d.depth_split(h, self.C, self.D, self.compute_dtype())
+        return self.res(fs)
 
 
 class Generator(_Block):
@@ -62,8 +64,7 @@ class Generator(_Block):
         if deformation is not None or occlusion is not None:
             raise NotImplementedError("Generator warp path (grid_sample/occlusion): SURVEY.md §8(f) next #2")
         if fs.dim() == 5:
-            N, C, D, H, W = fs.shape
-            fs = fs.reshape(N, C * D, H, W)
+            fs = ops3d.depth_merge(fs, self.compute_dtype())   # fs.view(N, -1, H, W), models.py:1103
         return self.forward_2d(fs)
 
 

@@ -203,6 +203,77 @@ class ResBlock2D(_Block):
                                     c2.weight_param(), c2.bias, self.bn2.weight, self.bn2.bias, self)
 
 
+class _Conv3(nn.Module):
+    """Parameter holder of one nn.Conv3d(in, out, 3, 1, 1): `weight` [out][in][3][3][3] + `bias`,
+    initialised as nn.Conv3d.reset_parameters (same RNG draws as the reference)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, bias=True):
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = in_channels, out_channels, kernel_size
+        self.sn = False
+        w = torch.empty(out_channels, in_channels, kernel_size, kernel_size, kernel_size)
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        self.weight = nn.Parameter(w)
+        if bias:
+            bound = 1.0 / math.sqrt(in_channels * kernel_size ** 3)
+            self.bias = nn.Parameter(torch.empty(out_channels).uniform_(-bound, bound))
+        else:
+            self.bias = None
+
+    def weight_param(self):
+        return self.weight
+
+    def extra_repr(self):
+        return f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}"
+
+
+class ConvBlock3D(_Block):
+    """_ConvBlock with dim=3 (modules.py:52-56): parameter / buffer holder with the reference
+    state-dict keys.  It runs inside ResBlock3D ("NAC", 3x3x3, stride 1, padding 1); spectral
+    norm and the other patterns raise."""
+
+    def __init__(self, pattern, in_channels, out_channels, kernel_size, stride, padding, use_weight_norm,
+                 activation_type="batch", nonlinearity_type="relu"):
+        super().__init__()
+        if (kernel_size, stride, padding) != (3, 1, 1) or pattern != "NAC" or use_weight_norm:
+            raise NotImplementedError("facevae_amd ConvBlock3D: the ResBlock3D form only (NAC, 3x3x3, s1, p1, "
+                                      "no spectral norm: AFE uses use_weight_norm=False, models.py:930)")
+        if activation_type != "batch" or nonlinearity_type != "relu":
+            raise NotImplementedError("facevae_amd ConvBlock3D: SyncBatchNorm + ReLU only")
+        self.pattern = pattern
+        mappings = {"C": _Conv3(in_channels, out_channels, kernel_size),
+                    "N": _BatchNorm(in_channels),
+                    "A": _Act(nonlinearity_type)}
+        self.layers = nn.Sequential(*[mappings[c] for c in pattern])
+        _ref(self, "conv", mappings["C"])
+        _ref(self, "bn", mappings["N"])
+
+    def forward(self, x):
+        raise NotImplementedError("ConvBlock3D runs inside ResBlock3D (ops3d.ResBlock3DFn)")
+
+
+class ResBlock3D(_Block):
+    """x + NAC(NAC(x)) over [N, C, D, H, W] (modules.py:116-126, 133-135): 3x3x3 convs on
+    the HIP kernels of conv3d.hip, BN/ReLU on the NHWC kernels over the NDHWC layout."""
+
+    def __init__(self, in_channels, use_weight_norm):
+        super().__init__()
+        self.layers = nn.Sequential(
+            ConvBlock3D("NAC", in_channels, in_channels, 3, 1, 1, use_weight_norm),
+            ConvBlock3D("NAC", in_channels, in_channels, 3, 1, 1, use_weight_norm),
+        )
+        _ref(self, "bn1", self.layers[0].bn)
+        _ref(self, "conv1", self.layers[0].conv)
+        _ref(self, "bn2", self.layers[1].bn)
+        _ref(self, "conv2", self.layers[1].conv)
+
+    def forward(self, x):
+        from . import ops3d
+        c1, c2 = self.conv1, self.conv2
+        return ops3d.ResBlock3DFn.apply(x, c1.weight, c1.bias, self.bn1.weight, self.bn1.bias,
+                                        c2.weight, c2.bias, self.bn2.weight, self.bn2.bias, self)
+
+
 class Conv2d(_Conv):
     """nn.Conv2d drop-in (stride 1, 'same' padding) with state-dict keys weight / bias."""
 

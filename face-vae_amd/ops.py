@@ -362,10 +362,13 @@ def _sync(stats, comm):
 
 def bn_from_partials(bn, part, cs, training, comm):
     d = cs.d
-    C = d.cout
-    dev = part.device
-    P = d.n * d.h * d.w
     nb, bp = stats_geometry(cs)
+    return bn_from_records(bn, part, nb, bp, d.n * d.h * d.w, d.cout, training, comm)
+
+
+def bn_from_records(bn, part, nb, bp, P, C, training, comm):
+    """BN statistics from nb (sum, sum of squares) records of bp pixels each (P in total)."""
+    dev = part.device
     ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, dev)
     if comm is None:
         # single process: statistics + finalize in two launches

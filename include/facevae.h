@@ -26,6 +26,7 @@
  *   fv_kl_*                  KLDivergenceLoss (losses.py:385-393).
  *   fv_mse_*                 ReconLoss / nn.MSELoss (losses.py:396-403).
  *   fv_l1_*                  PerceptualLoss pixel term nn.L1Loss (losses.py:128,135).
+ *   fv_conv3d_*             nn.Conv3d of ResBlock3D (modules.py:52-56,133-135; AFE models.py:935).
  *   fv_adam_step             torch.optim.Adam(lr, betas=(0.5,0.999)) (logger.py:60-61).
  *   fv_comm_*                distributed.py:24-31 init_process_group("nccl") + DDP's
  *                            gradient all-reduce (logger.py:55,58) + SyncBN collectives.
@@ -163,6 +164,40 @@ int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const floa
                            const uint8_t* wt, const float* wt_dq, void* dx, void* stream);
 /* layout probe: c[16][16] = a[16][128] . b[16][128]^T through one scaled fp8 MFMA tile */
 int fv_fp8_mfma_probe(const uint8_t* a, const uint8_t* b, float* c, void* stream);
+
+/* ------------------------------------------------ 3x3x3 conv (AFE ResBlock3D) ---- */
+/* nn.Conv3d(cin, cout, 3, 1, 1) of ConvBlock3D / ResBlock3D (modules.py:52-56, 133-135) in the
+ * AFE trunk (models.py:935, 943-944).  Activations NDHWC ([n][d][h][w][c], torch
+ * channels_last_3d), weights in the reference layout [cout][cin][3][3][3] fp32, re-laid out
+ * per forward by fv_conv3d_weight_prep (wk: forward, wt: data gradient; fv_conv3d_wk_bytes
+ * each).  bf16 with cin = cout = 32 and w = 64 runs the MFMA kernels (BN partials available:
+ * fv_conv3d_stats_blocks > 0); any other shape, and fp32 (parity mode), the direct kernels. */
+typedef struct fv_conv3d_desc {
+  int dtype;         /* FV_F32 or FV_BF16 */
+  int n, d, h, w;    /* spatial size (stride 1, padding 1: output == input) */
+  int cin, cout;     /* channels (dense, channel stride == count) */
+} fv_conv3d_desc;
+size_t fv_conv3d_wk_bytes(const fv_conv3d_desc* d);
+int fv_conv3d_weight_prep(const fv_conv3d_desc* d, const float* w_param, void* wk, void* wt, void* stream);
+/* BN partial records ([records][2][cout] (sum, sum of squares), block_pixels voxels each) that
+ * fv_conv3d_fwd writes when stats != NULL; 0 = not available for this shape */
+int fv_conv3d_stats_blocks(const fv_conv3d_desc* d);
+int fv_conv3d_stats_block_pixels(const fv_conv3d_desc* d);
+/* y = conv3d(x, wk) + bias [+ res] */
+int fv_conv3d_fwd(const fv_conv3d_desc* d, const void* x, const void* wk, const float* bias, const void* res,
+                  void* y, float* stats, void* stream);
+/* dx [n][d][h][w][cin] from dy [n][d][h][w][cout] and wt */
+int fv_conv3d_bwd_data(const fv_conv3d_desc* d, const void* dy, const void* wt, void* dx, void* stream);
+/* dw [cout][cin][3][3][3] fp32 and db [cout] (may be NULL), deterministic; ws of
+ * fv_conv3d_wgrad_ws_bytes bytes (0 = none needed) */
+size_t fv_conv3d_wgrad_ws_bytes(const fv_conv3d_desc* d);
+int fv_conv3d_bwd_weight(const fv_conv3d_desc* d, const void* x, const void* dy, float* dw, float* db, void* ws,
+                         void* stream);
+/* AFE.forward's x.view(N, C, D, H, W) of the mid_conv output (models.py:941-942) between the
+ * build's layouts: src NHWC [n][hw][c*d_count] -> dst NDHWC [n][d][hw][c] (inverse = 0), or back
+ * (inverse = 1: src NDHWC, dst NHWC) */
+int fv_depth_split(int dtype, const void* src, int n, int hw, int c, int d_count, int inverse, void* dst,
+                   void* stream);
 
 /* ------------------------------------------------------------- spectral norm ---- */
 size_t fv_spectral_norm_ws_bytes(int rows, int cols);

@@ -149,7 +149,10 @@ def _conv_weight(sd: Dict[str, torch.Tensor], prefix: str, training: bool) -> to
 
 
 def conv(sd, prefix, x, training):
+    """nn.Conv2d / nn.Conv3d (modules.py:15, 32), stride 1, 'same' padding."""
     w = _conv_weight(sd, prefix, training)
+    if w.dim() == 5:
+        return F.conv3d(x, w, sd[prefix + ".bias"], 1, w.shape[-1] // 2)
     return F.conv2d(x, w, sd[prefix + ".bias"], 1, w.shape[-1] // 2)
 
 
@@ -189,6 +192,29 @@ def encode(sd, x, cfg, training=True):
         h = conv_block(sd, f"afe.down.{i}.layers.0", h, "CNA", training)
         h = F.avg_pool2d(h, 2)
     return conv(sd, "afe.mid_conv", h, training)
+
+
+def res_block_3d(sd, prefix, x, training=True):
+    """ResBlock3D (modules.py:133-135 -> _ResBlock 116-126): x + NAC(NAC(x)), each NAC a
+    ConvBlock3D (modules.py:52-56) = SyncBatchNorm (5-D input) -> ReLU -> Conv3d 3x3x3."""
+    t = conv_block(sd, f"{prefix}.layers.0", x, "NAC", training)
+    t = conv_block(sd, f"{prefix}.layers.1", t, "NAC", training)
+    return x + t
+
+
+def encode_afe(sd, x, down_seq, C, D, n_res, training=True, prefix="afe"):
+    """The whole AFE (models.py:936-945): the 2-D trunk, x.view(N, C, D, H, W) (941-942), then
+    n_res ResBlock3D (943)."""
+    h = conv_block(sd, f"{prefix}.in_conv", x, "CNA", training)
+    for i in range(len(down_seq) - 1):
+        h = conv_block(sd, f"{prefix}.down.{i}.layers.0", h, "CNA", training)
+        h = F.avg_pool2d(h, 2)
+    h = conv(sd, f"{prefix}.mid_conv", h, training)
+    N, _, H, W = h.shape
+    h = h.view(N, C, D, H, W)
+    for i in range(n_res):
+        h = res_block_3d(sd, f"{prefix}.res.{i}", h, training)
+    return h
 
 
 def reparameterise(h, eps, latent):
