@@ -86,6 +86,19 @@ _SIGS = {
     "fv_conv3d_wgrad_ws_bytes": (c_size_t, [D3]),
     "fv_conv3d_bwd_weight": (c_int, [D3, P, P, P, P, P, P]),
     "fv_depth_split": (c_int, [c_int, P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "fv_grid_sample3d_fwd": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     P, P]),
+    "fv_grid_sample3d_bwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                     c_int, P, P, P]),
+    "fv_f32_to": (c_int, [c_int, P, P, c_long, P]),
+    "fv_occlusion_fwd": (c_int, [c_int, P, P, c_long, c_int, P, P]),
+    "fv_occlusion_bwd": (c_int, [c_int, P, P, P, c_long, c_int, P, P, P]),
+    "fv_sparse_motion_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "fv_sparse_motion_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "fv_heatmap_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_float, P, P]),
+    "fv_heatmap_bwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P, P, P]),
+    "fv_motion_mask_fwd": (c_int, [P, P, c_int, c_int, c_long, P, P, P]),
+    "fv_motion_mask_bwd": (c_int, [P, P, P, P, c_int, c_int, c_long, P, P, P]),
     "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),
     "fv_spectral_norm_fwd": (c_int, [P, c_int, c_int, P, P, P, c_int, P, P]),
     "fv_spectral_norm_bwd": (c_int, [P, P, c_int, c_int, P, P, P, P, P, P]),

@@ -1,0 +1,468 @@
+// Warp path of the Generator / MFE for gfx950: trilinear grid sampling, occlusion, and the
+// MFE motion assembly.  All of it is HBM / gather bound (no MFMA): channels-last rows make
+// every corner gather one contiguous row, lanes run along channels so the backward's
+// scattered float atomics leave as whole 64-256 B row segments.
+//
+// Reference behaviour replaced (file:line in Luh1124/face-vae):
+//   F.grid_sample(fs, deformation, align_corners=True) [trilinear, zeros]  models.py:1103
+//   fs * occlusion                                                            models.py:1106
+//   create_sparse_motions / create_heatmap_representations /
+//   create_deformed_source_image (utils.py:139-179, kp2gaussian_3d 123-129,
+//   make_coordinate_grid_3d 91-103), MFE mask softmax + deformation sum     models.py:1076-1078
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float ld(const float* p) { return *p; }
+__device__ __forceinline__ float ld(const bf16* p) { return (float)*p; }
+
+// align_corners=True source index: ((g + 1) / 2) * (size - 1)
+__device__ __forceinline__ float src_index(float g, int size) { return (g + 1.f) * 0.5f * (float)(size - 1); }
+
+// lanes per voxel LPV (power of two <= 64), lane q of a voxel handles channels q, q + LPV, ...
+template <typename T, int LPV>
+__global__ void __launch_bounds__(256) grid_sample3d_fwd(const T* __restrict__ in, const float* __restrict__ grid,
+                                                         T* __restrict__ out, int B, int Di, int Hi, int Wi, int Do,
+                                                         int Ho, int Wo, int C, int group) {
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long v = gid / LPV;
+  const int q = (int)(gid % LPV);
+  const long Vo = (long)Do * Ho * Wo;
+  if (v >= (long)B * Vo) return;
+  const int b = (int)(v / Vo);
+  const float* gp = grid + v * 3;
+  const float ix = src_index(gp[0], Wi), iy = src_index(gp[1], Hi), iz = src_index(gp[2], Di);
+  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+  const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+  const float tx = ix - fx, ty = iy - fy, tz = iz - fz;
+  const T* base = in + (long)(b / group) * Di * Hi * Wi * C;
+  for (int c = q; c < C; c += LPV) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+      const int xx = x0 + dx, yy = y0 + dy, zz = z0 + dz;
+      if ((unsigned)xx < (unsigned)Wi && (unsigned)yy < (unsigned)Hi && (unsigned)zz < (unsigned)Di) {
+        const float w = (dx ? tx : 1.f - tx) * (dy ? ty : 1.f - ty) * (dz ? tz : 1.f - tz);
+        acc += w * ld(base + (((long)zz * Hi + yy) * Wi + xx) * C + c);
+      }
+    }
+    out[v * C + c] = Elt<T>::from_f(acc);
+  }
+}
+
+// backward: gin (fp32, zeroed, the input's layout) += w * gout by float atomics; ggrid per
+// voxel = sum_c gout_c * d(out_c)/d(grid), reduced over the voxel's LPV lanes
+template <typename T, int LPV>
+__global__ void __launch_bounds__(256) grid_sample3d_bwd(const T* __restrict__ in, const float* __restrict__ grid,
+                                                         const T* __restrict__ gout, float* gin, float* ggrid,
+                                                         int B, int Di, int Hi, int Wi, int Do, int Ho, int Wo,
+                                                         int C, int group) {
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long v = gid / LPV;
+  const int q = (int)(gid % LPV);
+  const long Vo = (long)Do * Ho * Wo;
+  const bool live = v < (long)B * Vo;
+  const long vv = live ? v : 0;
+  const int b = (int)(vv / Vo);
+  const float* gp = grid + vv * 3;
+  const float ix = src_index(gp[0], Wi), iy = src_index(gp[1], Hi), iz = src_index(gp[2], Di);
+  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+  const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+  const float tx = ix - fx, ty = iy - fy, tz = iz - fz;
+  const long boff = (long)(b / group) * Di * Hi * Wi * C;
+  float gx = 0.f, gy = 0.f, gz = 0.f;
+  if (live) {
+    for (int c = q; c < C; c += LPV) {
+      const float g = ld(gout + vv * C + c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+        const int xx = x0 + dx, yy = y0 + dy, zz = z0 + dz;
+        if ((unsigned)xx < (unsigned)Wi && (unsigned)yy < (unsigned)Hi && (unsigned)zz < (unsigned)Di) {
+          const float wx = dx ? tx : 1.f - tx, wy = dy ? ty : 1.f - ty, wz = dz ? tz : 1.f - tz;
+          const long off = boff + (((long)zz * Hi + yy) * Wi + xx) * C + c;
+          if (gin) atomicAdd(gin + off, wx * wy * wz * g);
+          if (ggrid) {
+            const float val = ld(in + off) * g;
+            gx += (dx ? 1.f : -1.f) * wy * wz * val;
+            gy += (dy ? 1.f : -1.f) * wx * wz * val;
+            gz += (dz ? 1.f : -1.f) * wx * wy * val;
+          }
+        }
+      }
+    }
+  }
+  if (ggrid) {
+#pragma unroll
+    for (int o = 1; o < LPV; o <<= 1) {
+      gx += __shfl_xor(gx, o, 64);
+      gy += __shfl_xor(gy, o, 64);
+      gz += __shfl_xor(gz, o, 64);
+    }
+    if (live && q == 0) {
+      ggrid[vv * 3 + 0] = gx * 0.5f * (float)(Wi - 1);
+      ggrid[vv * 3 + 1] = gy * 0.5f * (float)(Hi - 1);
+      ggrid[vv * 3 + 2] = gz * 0.5f * (float)(Di - 1);
+    }
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) f32_to_kernel(const float* __restrict__ a, T* __restrict__ b, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) b[i] = Elt<T>::from_f(a[i]);
+}
+
+// occlusion: y[p][c] = x[p][c] * occ[p]; one wave per pixel (lanes along channels)
+template <typename T>
+__global__ void __launch_bounds__(256) occlusion_fwd(const T* __restrict__ x, const float* __restrict__ occ,
+                                                     T* __restrict__ y, long P, int C) {
+  const long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= P) return;
+  const float o = occ[p];
+  for (int c = threadIdx.x & 63; c < C; c += 64) y[p * C + c] = Elt<T>::from_f(ld(x + p * C + c) * o);
+}
+template <typename T>
+__global__ void __launch_bounds__(256) occlusion_bwd(const T* __restrict__ g, const T* __restrict__ x,
+                                                     const float* __restrict__ occ, T* dx, float* docc, long P,
+                                                     int C) {
+  const long p = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= P) return;
+  const float o = occ[p];
+  float s = 0.f;
+  for (int c = threadIdx.x & 63; c < C; c += 64) {
+    const float gv = ld(g + p * C + c);
+    if (dx) dx[p * C + c] = Elt<T>::from_f(gv * o);
+    s += gv * ld(x + p * C + c);
+  }
+  s = wave_sum(s);
+  if (docc && (threadIdx.x & 63) == 0) docc[p] = s;
+}
+
+// make_coordinate_grid_3d (utils.py:91-103): (x over W, y over H, z over D) in [-1, 1]
+__device__ __forceinline__ void ident(long v, int D, int H, int W, float& gx, float& gy, float& gz) {
+  const int w = (int)(v % W), h = (int)((v / W) % H), d = (int)(v / ((long)W * H));
+  gx = 2.f * ((float)w / (float)(W - 1)) - 1.f;
+  gy = 2.f * ((float)h / (float)(H - 1)) - 1.f;
+  gz = 2.f * ((float)d / (float)(D - 1)) - 1.f;
+}
+
+// create_sparse_motions (utils.py:139-152): out[n][0] = identity, out[n][k+1] = J (id - kp_d[k]) + kp_s[k]
+__global__ void __launch_bounds__(256) sparse_motion_fwd(const float* __restrict__ kps, const float* __restrict__ kpd,
+                                                         const float* __restrict__ J, float* __restrict__ out, int N,
+                                                         int K, int D, int H, int W) {
+  const long V = (long)D * H * W;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * (K + 1) * V) return;
+  const long v = i % V;
+  const int k = (int)((i / V) % (K + 1)), n = (int)(i / (V * (K + 1)));
+  float gx, gy, gz;
+  ident(v, D, H, W, gx, gy, gz);
+  float* o = out + i * 3;
+  if (k == 0) {
+    o[0] = gx; o[1] = gy; o[2] = gz;
+    return;
+  }
+  const float* kd = kpd + ((long)n * K + k - 1) * 3;
+  const float* ks = kps + ((long)n * K + k - 1) * 3;
+  const float* j = J + (long)n * 9;
+  const float c0 = gx - kd[0], c1 = gy - kd[1], c2 = gz - kd[2];
+  o[0] = j[0] * c0 + j[1] * c1 + j[2] * c2 + ks[0];
+  o[1] = j[3] * c0 + j[4] * c1 + j[5] * c2 + ks[1];
+  o[2] = j[6] * c0 + j[7] * c1 + j[8] * c2 + ks[2];
+}
+
+// per (n, k >= 1): sums over voxels of g (3) and g (x) c (9), c = id - kp_d; block reduction
+__global__ void __launch_bounds__(256) sparse_motion_bwd(const float* __restrict__ g, const float* __restrict__ kpd,
+                                                         float* __restrict__ sums, int N, int K, int D, int H, int W) {
+  const int k = blockIdx.x % K, n = blockIdx.x / K;
+  const long V = (long)D * H * W;
+  const float* gk = g + (((long)n * (K + 1) + k + 1) * V) * 3;
+  const float* kd = kpd + ((long)n * K + k) * 3;
+  float s[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) s[j] = 0.f;
+  for (long v = threadIdx.x; v < V; v += 256) {
+    float gx, gy, gz;
+    ident(v, D, H, W, gx, gy, gz);
+    const float c[3] = {gx - kd[0], gy - kd[1], gz - kd[2]};
+    const float gg[3] = {gk[v * 3], gk[v * 3 + 1], gk[v * 3 + 2]};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      s[a] += gg[a];
+#pragma unroll
+      for (int b = 0; b < 3; ++b) s[3 + 3 * a + b] += gg[a] * c[b];
+    }
+  }
+  __shared__ float red[4][12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const float t = wave_sum(s[j]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][j] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 12) sums[(long)blockIdx.x * 12 + threadIdx.x] =
+      red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// create_heatmap_representations (utils.py:130-137 with kp2gaussian_3d 123-129):
+// out[n][0] = 0, out[n][k+1] = G(kp_d[k]) - G(kp_s[k]), G(kp) = exp(-0.5 |id - kp|^2 / var)
+__device__ __forceinline__ float gauss(float gx, float gy, float gz, const float* kp, float var) {
+  const float a = gx - kp[0], b = gy - kp[1], c = gz - kp[2];
+  return expf(-0.5f * (a * a + b * b + c * c) / var);
+}
+__global__ void __launch_bounds__(256) heatmap_fwd(const float* __restrict__ kps, const float* __restrict__ kpd,
+                                                   float* __restrict__ out, int N, int K, int D, int H, int W,
+                                                   float var) {
+  const long V = (long)D * H * W;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * (K + 1) * V) return;
+  const long v = i % V;
+  const int k = (int)((i / V) % (K + 1)), n = (int)(i / (V * (K + 1)));
+  if (k == 0) {
+    out[i] = 0.f;
+    return;
+  }
+  float gx, gy, gz;
+  ident(v, D, H, W, gx, gy, gz);
+  out[i] = gauss(gx, gy, gz, kpd + ((long)n * K + k - 1) * 3, var) - gauss(gx, gy, gz, kps + ((long)n * K + k - 1) * 3, var);
+}
+// per (n, k): dkp_d = sum_v g G_d (id - kp_d) / var, dkp_s = -sum_v g G_s (id - kp_s) / var
+__global__ void __launch_bounds__(256) heatmap_bwd(const float* __restrict__ g, const float* __restrict__ kps,
+                                                   const float* __restrict__ kpd, float* dkps, float* dkpd, int N,
+                                                   int K, int D, int H, int W, float var) {
+  const int k = blockIdx.x % K, n = blockIdx.x / K;
+  const long V = (long)D * H * W;
+  const float* gk = g + ((long)n * (K + 1) + k + 1) * V;
+  const float* pd = kpd + ((long)n * K + k) * 3;
+  const float* ps = kps + ((long)n * K + k) * 3;
+  float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (long v = threadIdx.x; v < V; v += 256) {
+    float gx, gy, gz;
+    ident(v, D, H, W, gx, gy, gz);
+    const float gv = gk[v];
+    const float ed = gv * gauss(gx, gy, gz, pd, var) / var, es = gv * gauss(gx, gy, gz, ps, var) / var;
+    s[0] += ed * (gx - pd[0]);
+    s[1] += ed * (gy - pd[1]);
+    s[2] += ed * (gz - pd[2]);
+    s[3] -= es * (gx - ps[0]);
+    s[4] -= es * (gy - ps[1]);
+    s[5] -= es * (gz - ps[2]);
+  }
+  __shared__ float red[4][6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const float t = wave_sum(s[j]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][j] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (threadIdx.x < 3) dkpd[((long)n * K + k) * 3 + threadIdx.x] = t;
+    else dkps[((long)n * K + k) * 3 + threadIdx.x - 3] = t;
+  }
+}
+
+// MFE (models.py:1076-1078): p = softmax_k(logits[n][k][v]); def[n][v] = sum_k p_k sm[n][k][v]
+__global__ void __launch_bounds__(256) motion_mask_fwd(const float* __restrict__ logits, const float* __restrict__ sm,
+                                                       float* __restrict__ prob, float* __restrict__ def, int N,
+                                                       int K1, long V) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * V) return;
+  const long v = i % V;
+  const int n = (int)(i / V);
+  const float* l = logits + (long)n * K1 * V + v;
+  float m = -INFINITY;
+  for (int k = 0; k < K1; ++k) m = fmaxf(m, l[(long)k * V]);
+  float z = 0.f;
+  for (int k = 0; k < K1; ++k) z += expf(l[(long)k * V] - m);
+  const float iz = 1.f / z;
+  float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+  for (int k = 0; k < K1; ++k) {
+    const float p = expf(l[(long)k * V] - m) * iz;
+    if (prob) prob[((long)n * K1 + k) * V + v] = p;
+    const float* s = sm + (((long)n * K1 + k) * V + v) * 3;
+    d0 += p * s[0];
+    d1 += p * s[1];
+    d2 += p * s[2];
+  }
+  def[i * 3] = d0;
+  def[i * 3 + 1] = d1;
+  def[i * 3 + 2] = d2;
+}
+// backward: dsm = p g_def; dlogit_k = p_k (s_k - sum_j p_j s_j), s_k = g_def . sm_k + g_prob_k
+__global__ void __launch_bounds__(256) motion_mask_bwd(const float* __restrict__ prob, const float* __restrict__ sm,
+                                                       const float* __restrict__ gdef, const float* gprob,
+                                                       float* dlogits, float* dsm, int N, int K1, long V) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * V) return;
+  const long v = i % V;
+  const int n = (int)(i / V);
+  const float g0 = gdef[i * 3], g1 = gdef[i * 3 + 1], g2 = gdef[i * 3 + 2];
+  float ps = 0.f;
+  for (int k = 0; k < K1; ++k) {
+    const long e = ((long)n * K1 + k) * V + v;
+    const float p = prob[e];
+    const float* s = sm + e * 3;
+    const float sk = g0 * s[0] + g1 * s[1] + g2 * s[2] + (gprob ? gprob[e] : 0.f);
+    ps += p * sk;
+    if (dsm) {
+      dsm[e * 3] = p * g0;
+      dsm[e * 3 + 1] = p * g1;
+      dsm[e * 3 + 2] = p * g2;
+    }
+  }
+  if (dlogits) {
+    for (int k = 0; k < K1; ++k) {
+      const long e = ((long)n * K1 + k) * V + v;
+      const float* s = sm + e * 3;
+      const float sk = g0 * s[0] + g1 * s[1] + g2 * s[2] + (gprob ? gprob[e] : 0.f);
+      dlogits[e] = prob[e] * (sk - ps);
+    }
+  }
+}
+
+int lpv_of(int C) {
+  int l = 1;
+  while (l < C && l < 64) l <<= 1;
+  return l;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fv_grid_sample3d_fwd(int dtype, const void* in, const float* grid, int B, int Di, int Hi, int Wi, int Do,
+                         int Ho, int Wo, int C, int group, void* out, void* stream) {
+  FV_REQUIRE(in && grid && out && B > 0 && C > 0 && group > 0 && B % group == 0, "grid_sample3d: bad argument");
+  FV_REQUIRE(dtype == FV_F32 || dtype == FV_BF16, "grid_sample3d: f32 or bf16");
+  hipStream_t s = (hipStream_t)stream;
+  const long nvox = (long)B * Do * Ho * Wo;
+  const int lpv = lpv_of(C);
+  const int nb = fv_cdiv(nvox * lpv, 256);
+#define GS_FWD(T, L)                                                                                              \
+  hipLaunchKernelGGL((grid_sample3d_fwd<T, L>), dim3(nb), dim3(256), 0, s, (const T*)in, grid, (T*)out, B, Di, Hi, \
+                     Wi, Do, Ho, Wo, C, group)
+#define GS_DISPATCH(M, T)               \
+  switch (lpv) {                        \
+    case 1: M(T, 1); break;             \
+    case 2: M(T, 2); break;             \
+    case 4: M(T, 4); break;             \
+    case 8: M(T, 8); break;             \
+    case 16: M(T, 16); break;           \
+    case 32: M(T, 32); break;           \
+    default: M(T, 64); break;           \
+  }
+  if (dtype == FV_BF16) {
+    GS_DISPATCH(GS_FWD, bf16)
+  } else {
+    GS_DISPATCH(GS_FWD, float)
+  }
+  return fv_check_launch("grid_sample3d_fwd");
+}
+
+/* gin: fp32 accumulation buffer in the input's layout, zeroed by the caller (may be NULL);
+ * ggrid: [B][Do][Ho][Wo][3] fp32 (may be NULL) */
+int fv_grid_sample3d_bwd(int dtype, const void* in, const float* grid, const void* gout, int B, int Di, int Hi,
+                         int Wi, int Do, int Ho, int Wo, int C, int group, float* gin, float* ggrid, void* stream) {
+  FV_REQUIRE(in && grid && gout && B > 0 && C > 0 && group > 0 && B % group == 0, "grid_sample3d_bwd: bad argument");
+  FV_REQUIRE(dtype == FV_F32 || dtype == FV_BF16, "grid_sample3d: f32 or bf16");
+  hipStream_t s = (hipStream_t)stream;
+  const long nvox = (long)B * Do * Ho * Wo;
+  const int lpv = lpv_of(C);
+  const int nb = fv_cdiv(nvox * lpv, 256);
+#define GS_BWD(T, L)                                                                                              \
+  hipLaunchKernelGGL((grid_sample3d_bwd<T, L>), dim3(nb), dim3(256), 0, s, (const T*)in, grid, (const T*)gout, gin, \
+                     ggrid, B, Di, Hi, Wi, Do, Ho, Wo, C, group)
+  if (dtype == FV_BF16) {
+    GS_DISPATCH(GS_BWD, bf16)
+  } else {
+    GS_DISPATCH(GS_BWD, float)
+  }
+  return fv_check_launch("grid_sample3d_bwd");
+}
+
+int fv_f32_to(int dtype, const float* a, void* b, long n, void* stream) {
+  FV_REQUIRE(a && b && n >= 0, "f32_to: bad argument");
+  if (n == 0) return FV_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16) hipLaunchKernelGGL(f32_to_kernel<bf16>, dim3(fv_cdiv(n, 256)), dim3(256), 0, s, a, (bf16*)b, n);
+  else hipLaunchKernelGGL(f32_to_kernel<float>, dim3(fv_cdiv(n, 256)), dim3(256), 0, s, a, (float*)b, n);
+  return fv_check_launch("f32_to");
+}
+
+int fv_occlusion_fwd(int dtype, const void* x, const float* occ, long P, int C, void* y, void* stream) {
+  FV_REQUIRE(x && occ && y && P > 0 && C > 0, "occlusion: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(occlusion_fwd<bf16>, dim3(fv_cdiv(P, 4)), dim3(256), 0, s, (const bf16*)x, occ, (bf16*)y, P, C);
+  else
+    hipLaunchKernelGGL(occlusion_fwd<float>, dim3(fv_cdiv(P, 4)), dim3(256), 0, s, (const float*)x, occ, (float*)y, P, C);
+  return fv_check_launch("occlusion_fwd");
+}
+
+int fv_occlusion_bwd(int dtype, const void* g, const void* x, const float* occ, long P, int C, void* dx, float* docc,
+                     void* stream) {
+  FV_REQUIRE(g && x && occ && P > 0 && C > 0, "occlusion_bwd: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(occlusion_bwd<bf16>, dim3(fv_cdiv(P, 4)), dim3(256), 0, s, (const bf16*)g, (const bf16*)x, occ,
+                       (bf16*)dx, docc, P, C);
+  else
+    hipLaunchKernelGGL(occlusion_bwd<float>, dim3(fv_cdiv(P, 4)), dim3(256), 0, s, (const float*)g, (const float*)x,
+                       occ, (float*)dx, docc, P, C);
+  return fv_check_launch("occlusion_bwd");
+}
+
+int fv_sparse_motion_fwd(const float* kp_s, const float* kp_d, const float* J, int N, int K, int D, int H, int W,
+                         float* out, void* stream) {
+  FV_REQUIRE(kp_s && kp_d && J && out && N > 0 && K > 0 && D > 1 && H > 1 && W > 1, "sparse_motion: bad argument");
+  const long n = (long)N * (K + 1) * D * H * W;
+  hipLaunchKernelGGL(sparse_motion_fwd, dim3(fv_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, kp_s, kp_d, J, out,
+                     N, K, D, H, W);
+  return fv_check_launch("sparse_motion_fwd");
+}
+
+/* sums [N][K][12]: (sum_v g, sum_v g c^T) of each keypoint's motion gradient */
+int fv_sparse_motion_bwd(const float* g, const float* kp_d, int N, int K, int D, int H, int W, float* sums,
+                         void* stream) {
+  FV_REQUIRE(g && kp_d && sums && N > 0 && K > 0, "sparse_motion_bwd: bad argument");
+  hipLaunchKernelGGL(sparse_motion_bwd, dim3(N * K), dim3(256), 0, (hipStream_t)stream, g, kp_d, sums, N, K, D, H, W);
+  return fv_check_launch("sparse_motion_bwd");
+}
+
+int fv_heatmap_fwd(const float* kp_s, const float* kp_d, int N, int K, int D, int H, int W, float var, float* out,
+                   void* stream) {
+  FV_REQUIRE(kp_s && kp_d && out && N > 0 && K > 0 && D > 1 && H > 1 && W > 1, "heatmap: bad argument");
+  const long n = (long)N * (K + 1) * D * H * W;
+  hipLaunchKernelGGL(heatmap_fwd, dim3(fv_cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, kp_s, kp_d, out, N, K, D,
+                     H, W, var);
+  return fv_check_launch("heatmap_fwd");
+}
+
+int fv_heatmap_bwd(const float* g, const float* kp_s, const float* kp_d, int N, int K, int D, int H, int W, float var,
+                   float* dkp_s, float* dkp_d, void* stream) {
+  FV_REQUIRE(g && kp_s && kp_d && dkp_s && dkp_d && N > 0 && K > 0, "heatmap_bwd: bad argument");
+  hipLaunchKernelGGL(heatmap_bwd, dim3(N * K), dim3(256), 0, (hipStream_t)stream, g, kp_s, kp_d, dkp_s, dkp_d, N, K,
+                     D, H, W, var);
+  return fv_check_launch("heatmap_bwd");
+}
+
+int fv_motion_mask_fwd(const float* logits, const float* sm, int N, int K1, long V, float* prob, float* def,
+                       void* stream) {
+  FV_REQUIRE(logits && sm && def && N > 0 && K1 > 0 && V > 0, "motion_mask: bad argument");
+  hipLaunchKernelGGL(motion_mask_fwd, dim3(fv_cdiv((long)N * V, 256)), dim3(256), 0, (hipStream_t)stream, logits, sm,
+                     prob, def, N, K1, V);
+  return fv_check_launch("motion_mask_fwd");
+}
+
+int fv_motion_mask_bwd(const float* prob, const float* sm, const float* gdef, const float* gprob, int N, int K1,
+                       long V, float* dlogits, float* dsm, void* stream) {
+  FV_REQUIRE(prob && sm && gdef && N > 0 && K1 > 0 && V > 0, "motion_mask_bwd: bad argument");
+  hipLaunchKernelGGL(motion_mask_bwd, dim3(fv_cdiv((long)N * V, 256)), dim3(256), 0, (hipStream_t)stream, prob, sm,
+                     gdef, gprob, dlogits, dsm, N, K1, V);
+  return fv_check_launch("motion_mask_bwd");
+}
+
+}  // extern "C"

@@ -8,7 +8,7 @@ from torch import nn
 
 from . import config as _config
 from . import ops
-from . import ops3d
+from . import ops3d, warp
 from .modules import Conv2d, ConvBlock2D, DownBlock2D, ResBlock2D, ResBlock3D, UpBlock2D, _Block
 
 
@@ -40,8 +40,11 @@ class AFE(_Block):
 
 
 class Generator(_Block):
-    """Decoder (models.py:1085-1111).  The grid_sample warp (1103) and occlusion multiply
-    (1106) are SURVEY.md §8(f) "next #2": forward() accepts them only as identity (None)."""
+    """Decoder (models.py:1085-1111): grid_sample of the 3-D appearance volume by the motion
+    field (1103, warp.grid_sample_3d), view to [N, C*D, H, W], in_conv (SN, LeakyReLU .2),
+    mid_conv, occlusion multiply (1106, warp.occlusion_multiply), 6 ResBlock2D, 2 UpBlock2D,
+    out_conv 7x7 + sigmoid.  forward(fs, deformation=None, occlusion=None): None skips the warp
+    / the occlusion (identity), which is the FaceVAE composition's 2-D input."""
 
     def __init__(self, use_weight_norm=True, n_res=6, up_seq=(256, 128, 64), D=16, C=32):
         super().__init__()
@@ -53,19 +56,24 @@ class Generator(_Block):
                                   for i in range(len(up_seq) - 1)])
         self.out_conv = Conv2d(up_seq[-1], 3, 7, 1, 3)
 
-    def forward_2d(self, fs):
+    def forward_2d(self, fs, occlusion=None):
         fs = self.in_conv(fs)
         fs = self.mid_conv(fs)
+        if occlusion is not None:
+            fs = warp.occlusion_multiply(fs, occlusion, self.compute_dtype())
         fs = self.res(fs)
         fs = self.up(fs)
         return self.out_conv(fs, sigmoid=True)       # conv + bias + sigmoid, NCHW fp32 out
 
     def forward(self, fs, deformation=None, occlusion=None):
-        if deformation is not None or occlusion is not None:
-            raise NotImplementedError("Generator warp path (grid_sample/occlusion): SURVEY.md §8(f) next #2")
+        mode = self.compute_dtype()
         if fs.dim() == 5:
-            fs = ops3d.depth_merge(fs, self.compute_dtype())   # fs.view(N, -1, H, W), models.py:1103
-        return self.forward_2d(fs)
+            if deformation is not None:
+                fs = warp.grid_sample_3d(fs, deformation, ops.storage(mode))
+            fs = ops3d.depth_merge(fs, mode)          # .view(N, -1, H, W), models.py:1103
+        elif deformation is not None:
+            raise ValueError("Generator: a deformation needs the 5-D feature volume fs [N, C, D, H, W]")
+        return self.forward_2d(fs, occlusion)
 
 
 class FaceVAE(_Block):

@@ -27,6 +27,8 @@
  *   fv_mse_*                 ReconLoss / nn.MSELoss (losses.py:396-403).
  *   fv_l1_*                  PerceptualLoss pixel term nn.L1Loss (losses.py:128,135).
  *   fv_conv3d_*             nn.Conv3d of ResBlock3D (modules.py:52-56,133-135; AFE models.py:935).
+ *   fv_grid_sample3d_*, fv_occlusion_*, fv_sparse_motion_*, fv_heatmap_*, fv_motion_mask_*
+ *                            warp path: models.py:1076-1078,1103,1106; utils.py:123-179.
  *   fv_adam_step             torch.optim.Adam(lr, betas=(0.5,0.999)) (logger.py:60-61).
  *   fv_comm_*                distributed.py:24-31 init_process_group("nccl") + DDP's
  *                            gradient all-reduce (logger.py:55,58) + SyncBN collectives.
@@ -198,6 +200,42 @@ int fv_conv3d_bwd_weight(const fv_conv3d_desc* d, const void* x, const void* dy,
  * (inverse = 1: src NDHWC, dst NHWC) */
 int fv_depth_split(int dtype, const void* src, int n, int hw, int c, int d_count, int inverse, void* dst,
                    void* stream);
+
+/* ------------------------------------------------------- warp path (Generator / MFE) ---- */
+/* F.grid_sample(in, grid, mode="bilinear" (trilinear), padding_mode="zeros",
+ * align_corners=True) for 5-D input (models.py:1103; utils.py:175): in NDHWC [B/group][Di][Hi][Wi][C],
+ * grid [B][Do][Ho][Wo][3] fp32 (x -> W, y -> H, z -> D), out NDHWC [B][Do][Ho][Wo][C]; output
+ * batch b samples input batch b / group (group = K + 1 for create_deformed_source_image's
+ * repeat, utils.py:168-172).  dtype FV_F32 / FV_BF16 for in / out / gout. */
+int fv_grid_sample3d_fwd(int dtype, const void* in, const float* grid, int B, int Di, int Hi, int Wi, int Do,
+                         int Ho, int Wo, int C, int group, void* out, void* stream);
+/* gin (fp32, input layout, zeroed by the caller; float atomics) += dL/din, ggrid = dL/dgrid;
+ * either may be NULL */
+int fv_grid_sample3d_bwd(int dtype, const void* in, const float* grid, const void* gout, int B, int Di, int Hi,
+                         int Wi, int Do, int Ho, int Wo, int C, int group, float* gin, float* ggrid, void* stream);
+int fv_f32_to(int dtype, const float* a, void* b, long n, void* stream);
+/* fs * occlusion (models.py:1106): x [P][C] NHWC, occ [P] fp32; backward dx = g*occ (may be
+ * NULL), docc[p] = sum_c g x (may be NULL) */
+int fv_occlusion_fwd(int dtype, const void* x, const float* occ, long P, int C, void* y, void* stream);
+int fv_occlusion_bwd(int dtype, const void* g, const void* x, const float* occ, long P, int C, void* dx, float* docc,
+                     void* stream);
+/* create_sparse_motions (utils.py:139-152) with J = Rs inv(Rd) [N][3][3]: out [N][K+1][D][H][W][3] */
+int fv_sparse_motion_fwd(const float* kp_s, const float* kp_d, const float* J, int N, int K, int D, int H, int W,
+                         float* out, void* stream);
+/* backward sums [N][K][12] = (sum_v g_k, sum_v g_k (id - kp_d[k])^T) of the motion gradient g */
+int fv_sparse_motion_bwd(const float* g, const float* kp_d, int N, int K, int D, int H, int W, float* sums,
+                         void* stream);
+/* create_heatmap_representations (utils.py:130-137, kp2gaussian_3d 123-129): out [N][K+1][D][H][W] */
+int fv_heatmap_fwd(const float* kp_s, const float* kp_d, int N, int K, int D, int H, int W, float var, float* out,
+                   void* stream);
+int fv_heatmap_bwd(const float* g, const float* kp_s, const float* kp_d, int N, int K, int D, int H, int W, float var,
+                   float* dkp_s, float* dkp_d, void* stream);
+/* MFE mask softmax + deformation (models.py:1076-1078): prob = softmax over K1 of logits
+ * [N][K1][V]; def [N][V][3] = sum_k prob_k sm[N][K1][V][3] */
+int fv_motion_mask_fwd(const float* logits, const float* sm, int N, int K1, long V, float* prob, float* def,
+                       void* stream);
+int fv_motion_mask_bwd(const float* prob, const float* sm, const float* gdef, const float* gprob, int N, int K1,
+                       long V, float* dlogits, float* dsm, void* stream);
 
 /* ------------------------------------------------------------- spectral norm ---- */
 size_t fv_spectral_norm_ws_bytes(int rows, int cols);

@@ -237,6 +237,71 @@ def decode(sd, z, cfg, training=True):
     return torch.sigmoid(conv(sd, "generator.out_conv", g, training))
 
 
+# ----------------------------------------------------------------------------------------
+# warp path
+# ----------------------------------------------------------------------------------------
+
+def coordinate_grid_3d(d, h, w):
+    """make_coordinate_grid_3d (utils.py:91-103) without the .cuda(): [D, H, W, (x, y, z)]."""
+    z = 2 * (torch.arange(d) / (d - 1)) - 1
+    x = 2 * (torch.arange(h) / (h - 1)) - 1
+    y = 2 * (torch.arange(w) / (w - 1)) - 1
+    zz, xx, yy = z.view(-1, 1, 1).repeat(1, h, w), x.view(1, -1, 1).repeat(d, 1, w), y.view(1, 1, -1).repeat(d, h, 1)
+    return torch.cat([yy.unsqueeze(3), xx.unsqueeze(3), zz.unsqueeze(3)], 3)
+
+
+def sparse_motions(fs, kp_s, kp_d, Rs, Rd):
+    """create_sparse_motions (utils.py:139-152)."""
+    N, _, D, H, W = fs.shape
+    K = kp_s.shape[1]
+    ident = coordinate_grid_3d(D, H, W).view(1, 1, D, H, W, 3).repeat(N, 1, 1, 1, 1, 1)
+    cg = ident.repeat(1, K, 1, 1, 1, 1) - kp_d.view(N, K, 1, 1, 1, 3)
+    jac = torch.matmul(Rs, torch.inverse(Rd)).view(N, 1, 1, 1, 1, 3, 3)
+    cg = torch.matmul(jac, cg.unsqueeze(-1)).squeeze(-1) + kp_s.view(N, K, 1, 1, 1, 3)
+    return torch.cat([ident, cg], dim=1)
+
+
+def heatmap_representations(fs, kp_s, kp_d, var=0.01):
+    """create_heatmap_representations (utils.py:130-137, kp2gaussian_3d 123-129)."""
+    N, _, D, H, W = fs.shape
+    grid = coordinate_grid_3d(D, H, W).view(1, 1, D, H, W, 3)
+
+    def gauss(kp):
+        return torch.exp(-0.5 * ((grid - kp.view(N, -1, 1, 1, 1, 3)) ** 2).sum(-1) / var)
+    hm = gauss(kp_d) - gauss(kp_s)
+    return torch.cat([torch.zeros(N, 1, D, H, W), hm], dim=1).unsqueeze(2)
+
+
+def deformed_source(fs, sm):
+    """create_deformed_source_image (utils.py:155-179)."""
+    N, _, D, H, W = fs.shape
+    K1 = sm.shape[1]
+    rep = fs.unsqueeze(1).repeat(1, K1, 1, 1, 1, 1).view(N * K1, -1, D, H, W)
+    out = F.grid_sample(rep, sm.view(N * K1, D, H, W, -1), align_corners=True)
+    return out.view(N, K1, -1, D, H, W)
+
+
+def motion_mask(logits, sm):
+    """MFE.forward tail (models.py:1076-1078) -> (deformation, mask)."""
+    mask = F.softmax(logits, dim=1).unsqueeze(-1)
+    return (sm * mask).sum(dim=1), mask
+
+
+def generator_warp(sd, fs, deformation, occlusion, n_res, n_up, training=True, prefix="generator"):
+    """Generator.forward (models.py:1101-1111) with the warp and the occlusion."""
+    N, _, D, H, W = fs.shape
+    g = F.grid_sample(fs, deformation, align_corners=True).view(N, -1, H, W)
+    g = conv_block(sd, f"{prefix}.in_conv", g, "CNA", training, "leakyrelu")
+    g = conv(sd, f"{prefix}.mid_conv", g, training) * occlusion
+    for i in range(n_res):
+        t = conv_block(sd, f"{prefix}.res.{i}.layers.0", g, "NAC", training)
+        g = g + conv_block(sd, f"{prefix}.res.{i}.layers.1", t, "NAC", training)
+    for i in range(n_up):
+        g = F.interpolate(g, scale_factor=2, mode="nearest")
+        g = conv_block(sd, f"{prefix}.up.{i}.layers.1", g, "CNA", training)
+    return torch.sigmoid(conv(sd, f"{prefix}.out_conv", g, training))
+
+
 def kl_loss(mu, logstd):
     """KLDivergenceLoss (losses.py:392)."""
     return torch.mean(-0.5 - logstd + 0.5 * mu ** 2 + 0.5 * torch.exp(2 * logstd), dim=-1).mean()
