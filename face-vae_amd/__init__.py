@@ -9,14 +9,14 @@ through the C-ABI in include/facevae.h.
 """
 from . import _lib
 from .config import FaceVAEConfig, compute_dtype, set_compute_dtype
-from .losses import KLDivergenceLoss, L1Loss, ReconLoss
+from .losses import KLDivergenceLoss, L1Loss, PerceptualLoss, ReconLoss
 from .models import AFE, FaceVAE, Generator
 from .modules import (Conv2d, ConvBlock2D, ConvBlock3D, ConvTranspose2dELR, DownBlock2D, ResBlock2D, ResBlock3D,
                       SameBlock2D, UpBlock2D)
 from .optim import Adam
 from . import distributed, ops, ops3d, warp
 
-__all__ = ["FaceVAEConfig", "compute_dtype", "set_compute_dtype", "KLDivergenceLoss", "L1Loss", "ReconLoss",
+__all__ = ["FaceVAEConfig", "compute_dtype", "set_compute_dtype", "KLDivergenceLoss", "L1Loss", "PerceptualLoss", "ReconLoss",
            "AFE", "FaceVAE", "Generator", "Conv2d", "ConvBlock2D", "ConvTranspose2dELR", "DownBlock2D", "ResBlock2D", "ResBlock3D", "ConvBlock3D", "SameBlock2D",
            "UpBlock2D", "Adam", "distributed", "ops", "FaceVAETrainer"]
 

@@ -99,6 +99,13 @@ _SIGS = {
     "fv_heatmap_bwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "fv_motion_mask_fwd": (c_int, [P, P, c_int, c_int, c_long, P, P, P]),
     "fv_motion_mask_bwd": (c_int, [P, P, P, P, c_int, c_int, c_long, P, P, P]),
+    "fv_relu_bwd": (c_int, [c_int, P, P, c_long, P, P]),
+    "fv_maxpool2_fwd": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "fv_maxpool2_bwd": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, P, P]),
+    "fv_avgpool2_bwd": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),
+    "fv_l1t_ws_bytes": (c_size_t, []),
+    "fv_l1t_fwd": (c_int, [c_int, P, P, c_long, P, P, P]),
+    "fv_l1t_bwd": (c_int, [c_int, P, P, c_long, P, c_float, P, P]),
     "fv_spectral_norm_ws_bytes": (c_size_t, [c_int, c_int]),
     "fv_spectral_norm_fwd": (c_int, [P, c_int, c_int, P, P, P, c_int, P, P]),
     "fv_spectral_norm_bwd": (c_int, [P, P, c_int, c_int, P, P, P, P, P, P]),

@@ -26,3 +26,6 @@ class L1Loss(nn.Module):
 
     def forward(self, input, target):
         return ops.l1_loss(input, target)
+
+
+from .perceptual import PerceptualLoss  # noqa: E402,F401  (losses.py:123-151)

@@ -237,6 +237,22 @@ int fv_motion_mask_fwd(const float* logits, const float* sm, int N, int K1, long
 int fv_motion_mask_bwd(const float* prob, const float* sm, const float* gdef, const float* gprob, int N, int K1,
                        long V, float* dlogits, float* dsm, void* stream);
 
+/* ------------------------------------------------------------ perceptual loss ---- */
+/* The VGG feature stacks of PerceptualLoss (losses.py:33-151) run their convs on
+ * fv_conv2d_fwd / fv_conv2d_bwd_data and their per-channel normalisations
+ * (apply_imagenet_normalization / apply_vggface_normalization, utils.py:182-193) and the
+ * 0.5x bilinear downscale (== 2x2 average on even sizes, losses.py:148-149) on fv_bn_act_fwd
+ * (slope 1 = identity, scale/shift = the affine, pool = the average).  The rest: */
+int fv_relu_bwd(int dtype, const void* g, const void* y, long n, void* dx, void* stream);
+int fv_maxpool2_fwd(int dtype, const void* x, int n, int h, int w, int c, void* y, void* stream);
+int fv_maxpool2_bwd(int dtype, const void* x, const void* g, int n, int h, int w, int c, void* dx, void* stream);
+int fv_avgpool2_bwd(int dtype, const void* g, int n, int h, int w, int c, void* dx, void* stream);
+/* nn.L1Loss over bf16 / f32 operands (criterion of losses.py:127, 142-151) */
+size_t fv_l1t_ws_bytes(void);
+int fv_l1t_fwd(int dtype, const void* a, const void* b, long n, float* loss, void* ws, void* stream);
+int fv_l1t_bwd(int dtype, const void* a, const void* b, long n, const float* gout, float scale, void* da,
+               void* stream);
+
 /* ------------------------------------------------------------- spectral norm ---- */
 size_t fv_spectral_norm_ws_bytes(int rows, int cols);
 /* one power iteration (u, v updated in place) when power_iter, then sigma = u.(W v) */

@@ -302,6 +302,71 @@ def generator_warp(sd, fs, deformation, occlusion, n_res, n_up, training=True, p
     return torch.sigmoid(conv(sd, f"{prefix}.out_conv", g, training))
 
 
+# ----------------------------------------------------------------------------------------
+# perceptual loss
+# ----------------------------------------------------------------------------------------
+
+VGG19_MAP = {1: "relu_1_1", 3: "relu_1_2", 6: "relu_2_1", 8: "relu_2_2", 11: "relu_3_1", 13: "relu_3_2",
+             15: "relu_3_3", 17: "relu_3_4", 20: "relu_4_1", 22: "relu_4_2", 24: "relu_4_3", 26: "relu_4_4",
+             29: "relu_5_1"}                                    # losses.py:60-74
+VGG16_MAP = {1: "relu_1_1", 3: "relu_1_2", 6: "relu_2_1", 8: "relu_2_2", 11: "relu_3_1", 13: "relu_3_2",
+             15: "relu_3_3", 18: "relu_4_1", 20: "relu_4_2", 22: "relu_4_3", 25: "relu_5_1"}   # losses.py:106-118
+PERCEPTUAL_WEIGHTS = {"relu_1_1": 0.03125, "relu_2_1": 0.0625, "relu_3_1": 0.125, "relu_4_1": 0.25,
+                      "relu_5_1": 1.0}                          # losses.py:124
+
+
+def vgg_features(sd, x, mapping, layers):
+    """_PerceptualNetwork.forward (losses.py:42-49) over a torchvision `features` stack given
+    as {"features.{i}.weight/bias"}: conv 3x3 pad 1 at i, ReLU at i+1, MaxPool2d(2, 2) where no
+    conv sits.  Stops after the last requested layer (later layers cannot change outputs)."""
+    want = {i for i, n in mapping.items() if n in layers}
+    out, i = {}, 0
+    while i <= max(want):
+        if f"features.{i}.weight" in sd:
+            x = F.conv2d(x, sd[f"features.{i}.weight"], sd[f"features.{i}.bias"], 1, 1)
+        elif f"features.{i - 1}.weight" in sd:
+            x = F.relu(x)
+        else:
+            x = F.max_pool2d(x, 2, 2)
+        if mapping.get(i) in layers:
+            out[mapping[i]] = x
+        i += 1
+    return out
+
+
+def imagenet_norm(x):
+    """apply_imagenet_normalization (utils.py:182-186)."""
+    return (x - x.new_tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)) / x.new_tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+
+
+def vggface_norm(x):
+    """apply_vggface_normalization (utils.py:189-193)."""
+    return (x * 255 - x.new_tensor([129.186279296875, 104.76238250732422, 93.59396362304688]).view(1, 3, 1, 1))
+
+
+def perceptual_loss(inp, target, w19, w16, layers_weight=None, n_scale=3):
+    """PerceptualLoss.forward (losses.py:131-151), including the multi-scale loop's reuse of the
+    leaked `layer` / `weight` (the last layers_weight item) at every scale (:145-150)."""
+    layers_weight = layers_weight or PERCEPTUAL_WEIGHTS
+    loss = F.l1_loss(inp, target)
+    fi = vgg_features(w16, vggface_norm(inp), VGG16_MAP, layers_weight)
+    ft = vgg_features(w16, vggface_norm(target), VGG16_MAP, layers_weight)
+    inp, target = imagenet_norm(inp), imagenet_norm(target)
+    gi = vgg_features(w19, inp, VGG19_MAP, layers_weight)
+    gt = vgg_features(w19, target, VGG19_MAP, layers_weight)
+    for layer, weight in layers_weight.items():
+        loss = loss + weight * F.l1_loss(fi[layer], ft[layer].detach()) / 255
+        loss = loss + weight * F.l1_loss(gi[layer], gt[layer].detach())
+    for _ in range(n_scale):
+        inp = F.interpolate(inp, mode="bilinear", scale_factor=0.5, align_corners=False, recompute_scale_factor=True)
+        target = F.interpolate(target, mode="bilinear", scale_factor=0.5, align_corners=False,
+                               recompute_scale_factor=True)
+        gi = vgg_features(w19, inp, VGG19_MAP, layers_weight)
+        gt = vgg_features(w19, target, VGG19_MAP, layers_weight)
+        loss = loss + weight * F.l1_loss(gi[layer], gt[layer].detach())
+    return loss
+
+
 def kl_loss(mu, logstd):
     """KLDivergenceLoss (losses.py:392)."""
     return torch.mean(-0.5 - logstd + 0.5 * mu ** 2 + 0.5 * torch.exp(2 * logstd), dim=-1).mean()
