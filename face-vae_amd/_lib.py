@@ -33,6 +33,11 @@ class Conv3dDesc(ctypes.Structure):
                 ("cin", c_int), ("cout", c_int)]
 
 
+class StoreReduce(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("records", c_void_p), ("bn_input", c_void_p), ("mean", c_void_p),
+                ("invstd", c_void_p), ("gamma", c_void_p), ("beta", c_void_p), ("slope", c_float)]
+
+
 class SnLayer(ctypes.Structure):
     _fields_ = [("w", c_void_p), ("u", c_void_p), ("v", c_void_p), ("sigma", c_void_p), ("usnap", c_void_p),
                 ("vsnap", c_void_p), ("rows", c_int), ("cols", c_int)]
@@ -63,6 +68,10 @@ _SIGS = {
     "fv_conv2d_wgrad_bias_slab_elems": (c_size_t, [D]),
     "fv_conv2d_bwd_weight": (c_int, [D, P, P, P, P, c_int, P, P, P]),
     "fv_conv2d_wgrad_reduce": (c_int, [D, P, P, P, P, P]),
+    "fv_conv2d_sr_records": (c_int, [D, c_int, POINTER(c_int)]),
+    "fv_conv2d_fwd_sr": (c_int, [D, P, P, P, P, P, P, P]),
+    "fv_conv2d_bwd_data_sr": (c_int, [D, P, c_int, P, P, P, P]),
+    "fv_bn_bwd_from_records": (c_int, [P, c_int, c_int, c_long, c_int, c_long, P, P, P, P, P, P]),
     "fv_convt_supported": (c_int, [D]),
     "fv_convt_weight_prep": (c_int, [D, P, c_int, c_float, P, P, P, P]),
     "fv_convt_wgrad_reduce": (c_int, [D, P, P, P, c_int, c_float, P, P, P, P]),

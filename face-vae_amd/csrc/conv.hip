@@ -50,6 +50,15 @@ struct ConvArgs {
   int wphase;     // elements per phase block of the weight buffer (MODE 2)
   const float* dq0;   // fp8 path: per-tensor dequant factors of the two operands (device)
   const float* dq1;
+  // store-pass records (STAGED epilogue, fv_store_reduce): per (m-tile, wave) and output
+  // channel, 1 = (sum, sum of squares) of the stored (bf16, residual-added) output -- the next
+  // BN's statistics; 2 = BN-backward sums (g, g * yhat) of the stored gradient v with
+  // g = v * act'(gamma * yhat + beta), yhat = (res - mean) * invstd (`res` = the BN input,
+  // prefetched like a residual, not added)
+  int spm;
+  float* sprec;
+  const float *bnm, *bni, *bng, *bnb;
+  float bns;
 };
 
 // output pixel of tile-space pixel p (identity unless a sub-pixel phase is set)
@@ -242,6 +251,49 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
       }
     }
     __syncthreads();
+    if (!a.spm) {
+      // the plain store pass (kept free of the record code below: +2-3 us per res conv)
+#pragma unroll
+      for (int it = 0; it < NRES; ++it) {
+        const int idx = tid + it * NT;
+        if (idx >= BM * CPR) break;
+        const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
+        const int tp = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
+        const int co = co0 + ch * 8;
+        if (tp >= a.P || co >= a.Cout || (a.dbg & 256)) continue;   // (bit 8: experiment, no stores)
+        const int pix = out_pix(a, tp);
+        Chunk8<bf16> v;
+        v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+        T* yp = reinterpret_cast<T*>(a.y) + (long)pix * a.ldy + co;
+        if (a.res) {
+          Chunk8<bf16> r;
+          r.raw = rpre[it];
+          float f[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = v.get(j) + r.get(j);
+          v.set8(f);
+        }
+        v.store(reinterpret_cast<bf16*>(yp));
+      }
+      return;
+    }
+    // store-pass records: NT % CPR == 0 keeps every thread on one 8-channel chunk for all its
+    // iterations (the host enables spm only for such tiles, with P % BM == 0)
+    const int sch = tid % CPR;
+    float sacc[8], qacc[8], bm_[8], bi_[8], bg_[8], bb_[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sacc[j] = qacc[j] = 0.f;
+    if (a.spm == 2) {
+      const int c = co0 + sch * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = c + j < a.Cout;
+        bm_[j] = ok ? a.bnm[c + j] : 0.f;
+        bi_[j] = ok ? a.bni[c + j] : 0.f;
+        bg_[j] = ok ? a.bng[c + j] : 0.f;
+        bb_[j] = ok ? a.bnb[c + j] : 0.f;
+      }
+    }
 #pragma unroll
     for (int it = 0; it < NRES; ++it) {
       const int idx = tid + it * NT;
@@ -249,20 +301,57 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
       const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
       const int tp = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
       const int co = co0 + ch * 8;
-      if (tp >= a.P || co >= a.Cout || (a.dbg & 256)) continue;   // (bit 8: experiment, no stores)
+      if (tp >= a.P || co >= a.Cout || (a.dbg & 256)) continue;
       const int pix = out_pix(a, tp);
       Chunk8<bf16> v;
       v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
       T* yp = reinterpret_cast<T*>(a.y) + (long)pix * a.ldy + co;
-      if (a.res) {
-        Chunk8<bf16> r;
-        r.raw = rpre[it];
-        float f[8];
+      Chunk8<bf16> r;
+      r.raw = rpre[it];
+      if (a.spm == 2) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = v.get(j) + r.get(j);
-        v.set8(f);
+        for (int j = 0; j < 8; ++j) {
+          const float yh = (r.get(j) - bm_[j]) * bi_[j];
+          const float gv = v.get(j);
+          const float g = bg_[j] * yh + bb_[j] > 0.f ? gv : gv * a.bns;
+          sacc[j] += g;
+          qacc[j] += g * yh;
+        }
+      } else {
+        if (a.res) {
+          float f[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = v.get(j) + r.get(j);
+          v.set8(f);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float o = v.get(j);
+          sacc[j] += o;
+          qacc[j] += o * o;
+        }
       }
       v.store(reinterpret_cast<bf16*>(yp));
+    }
+    {
+      static_assert(CPR <= 64 && 64 % CPR == 0, "store-pass records: chunks per row must divide a wave");
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sacc[j] += __shfl_xor(sacc[j], o, 64);
+          qacc[j] += __shfl_xor(qacc[j], o, 64);
+        }
+      const int c = co0 + sch * 8;
+      if (lane < CPR && c < a.Cout) {
+        const long rec = (long)tm * (NT / 64) + (tid >> 6);
+        float* r0 = a.sprec + (rec * 2) * a.Cout + c;
+        float* r1 = a.sprec + (rec * 2 + 1) * a.Cout + c;
+        *reinterpret_cast<float4*>(r0) = make_float4(sacc[0], sacc[1], sacc[2], sacc[3]);
+        *reinterpret_cast<float4*>(r0 + 4) = make_float4(sacc[4], sacc[5], sacc[6], sacc[7]);
+        *reinterpret_cast<float4*>(r1) = make_float4(qacc[0], qacc[1], qacc[2], qacc[3]);
+        *reinterpret_cast<float4*>(r1 + 4) = make_float4(qacc[4], qacc[5], qacc[6], qacc[7]);
+      }
     }
     return;
   }
@@ -3398,11 +3487,35 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   return FV_OK;
 }
 
+// store-pass record geometry (fv_store_reduce) of the launch `d` takes: records and pixels per
+// record, 0 when that path has none.  The halo-staged 3x3 kernels only: 256-pixel tiles of 8
+// waves (co tiles of 256 / 128) or 4 waves (co tiles of 64), one record per (tile, wave).
+static int sr_geometry(const fv_conv_desc* d, int* bp) {
+  if (d->dtype != FV_BF16 || use_c7n(d) || halo_tr(d) || use_subpix(d)) return 0;
+  const int bn = halo3_bn(d);
+  const long P = (long)d->n * d->h * d->w;
+  if (!bn || d->cout % bn || P % 256) return 0;
+  const int nw = bn == 64 ? 4 : 8;
+  if (bp) *bp = 256 / nw;
+  return (int)(P / 256 * nw);
+}
+
 static int g_conv_dbg = -1;
 static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
                     const float* psc, const float* psh, const void* res, void* y, float* stats,
-                    hipStream_t s) {
+                    hipStream_t s, const fv_store_reduce* sr = nullptr) {
   ConvArgs a{};
+  if (sr && sr->mode) {
+    FV_REQUIRE(sr_geometry(d, nullptr) > 0, "store-pass records not available for this conv (query fv_conv2d_sr_records)");
+    FV_REQUIRE(sr->records, "store-pass records: null buffer");
+    FV_REQUIRE(sr->mode == 1 || (sr->mode == 2 && sr->bn_input && sr->mean && sr->invstd && sr->gamma && sr->beta && !res),
+               "store-pass records: bad mode / BN arguments");
+    FV_REQUIRE(!stats, "store-pass records and accumulator statistics in one call are not supported");
+    a.spm = sr->mode;
+    a.sprec = sr->records;
+    a.bnm = sr->mean; a.bni = sr->invstd; a.bng = sr->gamma; a.bnb = sr->beta; a.bns = sr->slope;
+    if (sr->mode == 2) res = sr->bn_input;        // prefetched as a residual, not added
+  }
   const FwdTile t = fwd_tile(d->cout);
   a.x = x; a.w = wk; a.bias = bias; a.psc = psc; a.psh = psh; a.slope = d->pro_slope;
   a.res = res; a.y = y; a.stats = stats;
@@ -3532,19 +3645,54 @@ int fv_conv2d_fwd(const fv_conv_desc* d, const void* x, const void* wk, const fl
   return conv_run(d, x, wk, bias, pro_scale, pro_shift, res, y, stats, (hipStream_t)stream);
 }
 
-int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,
-                       void* stream) {
-  int st = check_desc(d);
-  if (st) return st;
+// the forward-conv descriptor the data gradient of `d` runs as (transposed, flipped weights)
+static fv_conv_desc dgrad_desc(const fv_conv_desc* d) {
   fv_conv_desc t{};
   t.dtype = d->dtype;
   t.n = d->n; t.h = d->h; t.w = d->w;
   t.cin = pad_pow2_8(d->cout);
   t.cin_valid = d->cout;
-  FV_REQUIRE(ldy_dy == t.cin, "bwd_data: dy channel stride must be %d (got %d)", t.cin, ldy_dy);
   t.cout = d->cin;   // every (padded) input channel; padded ones come out 0
   t.ldy = d->cin;
   t.ksize = d->ksize;
+  return t;
+}
+
+int fv_conv2d_sr_records(const fv_conv_desc* d, int dgrad, int* record_pixels) {
+  if (check_desc(d) != FV_OK) return 0;
+  if (dgrad) {
+    if (d->upsample) return 0;
+    const fv_conv_desc t = dgrad_desc(d);
+    return sr_geometry(&t, record_pixels);
+  }
+  return sr_geometry(d, record_pixels);
+}
+
+int fv_conv2d_fwd_sr(const fv_conv_desc* d, const void* x, const void* wk, const float* bias, const void* res, void* y,
+                     const fv_store_reduce* sr, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(x && wk && y && sr && sr->mode == 1, "fwd_sr: null pointer or mode != 1");
+  FV_REQUIRE(!d->pro_act && !d->out_nchw_f32 && d->ldy == d->cout, "fwd_sr: plain NHWC output only");
+  return conv_run(d, x, wk, bias, nullptr, nullptr, res, y, nullptr, (hipStream_t)stream, sr);
+}
+
+int fv_conv2d_bwd_data_sr(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,
+                          const fv_store_reduce* sr, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(dy && wt && dx && sr && sr->mode == 2 && !d->upsample, "bwd_data_sr: bad argument");
+  const fv_conv_desc t = dgrad_desc(d);
+  FV_REQUIRE(ldy_dy == t.cin, "bwd_data: dy channel stride must be %d (got %d)", t.cin, ldy_dy);
+  return conv_run(&t, dy, wt, nullptr, nullptr, nullptr, nullptr, dx, nullptr, (hipStream_t)stream, sr);
+}
+
+int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,
+                       void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  const fv_conv_desc t = dgrad_desc(d);
+  FV_REQUIRE(ldy_dy == t.cin, "bwd_data: dy channel stride must be %d (got %d)", t.cin, ldy_dy);
   if (use_dgrad_lowres(d)) {
     FV_REQUIRE(dy && wt && dx, "null pointer");
     ConvArgs a{};

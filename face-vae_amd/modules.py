@@ -140,8 +140,13 @@ class ConvBlock2D(_Block):
         self.pool = False
 
     def forward(self, x):
-        fn = ops.ConvBNActFn if self.pattern == "CNA" else ops.NACFn
-        return fn.apply(x, self.conv.weight_param(), self.conv.bias, self.bn.weight, self.bn.bias, self)
+        if self.pattern == "CNA":
+            z = ops.ConvBNActFn.apply(x, self.conv.weight_param(), self.conv.bias, self.bn.weight, self.bn.bias, self)
+            holder = getattr(self, "_fv_holder", None)
+            if holder is not None and z.requires_grad:
+                z._fv_bnsrc = (holder, z._version)   # read by the consuming conv (ops._claim_bnsrc)
+            return z
+        return ops.NACFn.apply(x, self.conv.weight_param(), self.conv.bias, self.bn.weight, self.bn.bias, self)
 
 
 class DownBlock2D(_Block):
@@ -199,8 +204,13 @@ class ResBlock2D(_Block):
 
     def forward(self, x):
         c1, c2 = self.conv1, self.conv2
-        return ops.ResBlockFn.apply(x, c1.weight_param(), c1.bias, self.bn1.weight, self.bn1.bias,
-                                    c2.weight_param(), c2.bias, self.bn2.weight, self.bn2.bias, self)
+        out = ops.ResBlockFn.apply(x, c1.weight_param(), c1.bias, self.bn1.weight, self.bn1.bias,
+                                   c2.weight_param(), c2.bias, self.bn2.weight, self.bn2.bias, self)
+        rec = getattr(self, "_fv_out_rec", None)
+        if rec is not None:
+            out._fv_bnrec = rec + (out._version,)     # the next ResBlock's bn1 statistics
+            self._fv_out_rec = None
+        return out
 
 
 class _Conv3(nn.Module):

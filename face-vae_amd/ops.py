@@ -15,6 +15,7 @@ Reference semantics restated here (file:line in Luh1124/face-vae):
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -269,8 +270,53 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
     return part
 
 
-def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=True):
-    """-> (dx at the conv input resolution (upsample folded back), dW (param layout), db)."""
+# store-pass reductions (include/facevae.h, fv_store_reduce); FV_DISABLE_SR=1 keeps the
+# separate BN passes (A/B, and the parity tests of both forms)
+_SR_OFF = os.environ.get("FV_DISABLE_SR", "0") == "1"
+_RES_SR = os.environ.get("FV_RES_SR", "0") == "1"
+
+
+def sr_records(d, dgrad):
+    """(records, pixels per record) of the store-pass reduction of a launch, or None."""
+    if _SR_OFF:
+        return None
+    bp = ctypes.c_int(0)
+    nrec = query("fv_conv2d_sr_records", ctypes.byref(d), int(dgrad), ctypes.byref(bp))
+    return (nrec, bp.value) if nrec > 0 else None
+
+
+class BNRecords:
+    """BN-backward sums of a BN output gradient, reduced in the dgrad that produced it."""
+    __slots__ = ("part", "nb", "bp", "dx")
+
+    def __init__(self, part, nb, bp, dx):
+        self.part, self.nb, self.bp, self.dx = part, nb, bp, dx
+
+
+def _dgrad_bnred(cs, dy, dx, bnred):
+    """Data gradient with the BN-backward sums of `bnred` = (bn, BNResult, bn input y, slope)
+    fused into its store pass; -> BNRecords, or None (then dx is not written)."""
+    d = cs.d
+    if bnred is None or cs.fp8 or d.upsample or d.dtype != L.FV_BF16:
+        return None
+    geo = sr_records(d, True)
+    if geo is None:
+        return None
+    bn, r, ybn, slope = bnred
+    if r.count == 0 and r.stats is None:          # eval-mode statistics: no batch sums needed
+        return None
+    nb, bp = geo
+    part = _empty(nb * 2 * d.cin, F32, dy.device)
+    sr = L.StoreReduce(2, ptr(part), ptr(ybn), ptr(r.mean), ptr(r.invstd), ptr(bn.weight), ptr(bn.bias),
+                       float(slope))
+    _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data_sr", ctypes.byref(d), ptr(dy), d.cout, ptr(cs.wt), ptr(dx),
+                                    ctypes.byref(sr), stream()))
+    return BNRecords(part, nb, bp, dx)
+
+
+def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=True, bnred=None, want_recs=False):
+    """-> (dx at the conv input resolution (upsample folded back), dW (param layout), db
+    [, BNRecords or None when want_recs])."""
     d = cs.d
     dev = dy.device
     slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
@@ -293,7 +339,7 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
                                         ptr(cs.wdq), ptr(dx), stream()))
         if CHECK is not None:
             CHECK("dgrad", cs, dy=dy, ldd=ldd, dx=dx, q8=(dy8, dydq))
-        return dx, dw, db
+        return (dx, dw, db, None) if want_recs else (dx, dw, db)
     if need_dx and d.upsample and query("fv_conv2d_dgrad_lowres", ctypes.byref(d)):
         # gradient of the upsample's (low-res) input in one stride-2 pass
         dx = torch.empty((d.n, d.cin, d.h // 2, d.w // 2), dtype=dy.dtype, device=dev, memory_format=CL)
@@ -301,6 +347,11 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
                                         stream()))
     elif need_dx:
         dx = torch.empty((d.n, d.cin, d.h, d.w), dtype=dy.dtype, device=dev, memory_format=CL)
+        recs = _dgrad_bnred(cs, dy, dx, bnred) if ldd == d.cout else None
+        if recs is not None:
+            if CHECK is not None:
+                CHECK("dgrad", cs, dy=dy, ldd=ldd, dx=dx)
+            return dx, dw, db, recs
         _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data", ctypes.byref(d), ptr(dy), ldd, ptr(cs.wt), ptr(dx),
                                         stream()))
         if d.upsample:
@@ -310,7 +361,7 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
             dx = src
     if CHECK is not None and dx is not None:
         CHECK("dgrad", cs, dy=dy, ldd=ldd, dx=dx)
-    return dx, dw, db
+    return (dx, dw, db, None) if want_recs else (dx, dw, db)
 
 
 # ----------------------------------------------------------------------------------------
@@ -413,8 +464,9 @@ def bn_act_forward(y, r: BNResult, slope, pool, bn=None):
     return out
 
 
-def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True):
-    """-> (dx of the BN input, dgamma, dbeta)."""
+def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True, recs=None):
+    """-> (dx of the BN input, dgamma, dbeta).  recs: the BN-backward sums already reduced by
+    the dgrad that produced dout (BNRecords), replacing the reduce pass."""
     N, C, H, W = y.shape
     dev = y.device
     dc = L.dtype_code(y.dtype)
@@ -422,7 +474,19 @@ def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, ne
     dg = torch.empty(C, dtype=F32, device=dev)
     dbt = torch.empty(C, dtype=F32, device=dev)
     k = torch.empty(2 * C, dtype=F32, device=dev)
-    if comm is None:
+    if recs is not None and not pool and recs.dx.data_ptr() == dout.data_ptr():
+        P = N * H * W
+        if comm is None:
+            call("fv_bn_bwd_from_records", ptr(recs.part), recs.nb, recs.bp, P, C, int(r.count), ptr(dg), ptr(dbt),
+                 ptr(k), None, ptr(ws), stream())
+        else:
+            red = torch.empty(2 * C, dtype=F64, device=dev)
+            call("fv_bn_bwd_from_records", ptr(recs.part), recs.nb, recs.bp, P, C, 0, ptr(dg), ptr(dbt), None,
+                 ptr(red), ptr(ws), stream())
+            if need_dx:
+                _sync(red, comm)
+                call("fv_bn_bwd_finalize_dev", ptr(red), C, ptr(r.stats), None, None, ptr(k), stream())
+    elif comm is None:
         # eval mode (running statistics, count 0): the normalisation is a fixed affine map, so
         # the batch-statistics terms k vanish and dx = gamma * invstd * g
         evalm = r.count == 0 and r.stats is None
@@ -486,6 +550,11 @@ class ConvBNActFn(torch.autograd.Function):
         z = bn_act_forward(y, r, blk.slope, blk.pool, bn)
         cs.release()
         ctx.blk, ctx.cs, ctx.r, ctx.comm = blk, cs, r, comm
+        # z = act(BN(y)): a single consumer conv may reduce this BN's backward sums in the store
+        # pass of its data gradient (holder["recs"], read back in backward below)
+        ctx.holder = {"bn": bn, "r": r, "y": y, "slope": blk.slope, "pool": blk.pool, "nuse": 0}
+        blk._fv_holder = ctx.holder if training else None
+        ctx.src = _claim_bnsrc(x, xb)
         ctx.save_for_backward(x, xb, y)
         return z
 
@@ -494,10 +563,29 @@ class ConvBNActFn(torch.autograd.Function):
         x, xb, y = ctx.saved_tensors
         blk, cs, r = ctx.blk, ctx.cs, ctx.r
         dz = grad_in(dz, y.dtype)
-        dy, dg, dbt = bn_act_backward(dz, y, blk.bn, r, blk.slope, blk.pool, ctx.comm)
-        dxb, dw, db = conv_backward(cs, xb, dy, y.shape[1], need_dx=ctx.needs_input_grad[0])
+        recs = ctx.holder.get("recs") if ctx.holder["nuse"] == 1 else None
+        dy, dg, dbt = bn_act_backward(dz, y, blk.bn, r, blk.slope, blk.pool, ctx.comm, recs=recs)
+        dxb, dw, db, recs_in = conv_backward(cs, xb, dy, y.shape[1], need_dx=ctx.needs_input_grad[0],
+                                             bnred=_bnred_of(ctx.src), want_recs=True)
+        if ctx.src is not None:
+            ctx.src["recs"] = recs_in
         dx = from_nhwc(dxb, x) if dxb is not None else None
         return dx, dw, db, dg, dbt, None
+
+
+def _claim_bnsrc(x, xb):
+    """The BN-source holder of x (set by the producing CNA block) when this Function's data
+    gradient will be x's whole gradient in the producer's layout; counts the consumers."""
+    src = getattr(x, "_fv_bnsrc", None)
+    if src is None or src[1] != x._version:
+        return None
+    h = src[0]
+    h["nuse"] += 1
+    return h if (xb is x and not h["pool"]) else None
+
+
+def _bnred_of(src):
+    return None if src is None or src["nuse"] != 1 else (src["bn"], src["r"], src["y"], src["slope"])
 
 
 class ResBlockFn(torch.autograd.Function):
@@ -516,7 +604,12 @@ class ResBlockFn(torch.autograd.Function):
         training = blk.training
         comm = blk.bn_comm()
         c1, c2 = blk.conv1, blk.conv2
-        r1 = bn_from_tensor(blk.bn1, xb, training, comm)
+        rec = getattr(x, "_fv_bnrec", None)
+        if training and rec is not None and rec[3] == x._version and xb is x:
+            # statistics of x reduced in the previous block's conv2 store pass (post-residual)
+            r1 = bn_from_records(blk.bn1, rec[0], rec[1], rec[2], N * H * W, C, True, comm)
+        else:
+            r1 = bn_from_tensor(blk.bn1, xb, training, comm)
         a1 = bn_act_forward(xb, r1, 0.0, False, blk.bn1)
         d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size)
         cs1 = ConvState(c1, d1, dtype, x.device, training, True, fp8=mode == FP8)
@@ -527,7 +620,21 @@ class ResBlockFn(torch.autograd.Function):
         d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size)
         cs2 = ConvState(c2, d2, dtype, x.device, training, True, fp8=mode == FP8)
         out = torch.empty_like(xb)
-        conv_forward(cs2, a2, b2, res=xb, y=out)
+        geo = sr_records(d2, False) if training and not cs2.fp8 else None
+        if geo is not None:
+            # out = x + conv2(.) with its (sum, sum of squares) reduced in the store pass: the
+            # next ResBlock's bn1 statistics without a pass over out (ResBlock2D.forward hands
+            # them on)
+            part = _empty(geo[0] * 2 * C, F32, x.device)
+            sr = L.StoreReduce(1, ptr(part), None, None, None, None, None, 0.0)
+            _timed("fwd", d2, lambda: call("fv_conv2d_fwd_sr", ctypes.byref(d2), ptr(a2), ptr(cs2.wk), ptr(b2),
+                                           ptr(xb), ptr(out), ctypes.byref(sr), stream()))
+            if CHECK is not None:
+                CHECK("fwd", cs2, x=a2, bias=b2, pro=None, res=xb, y=out)
+            blk._fv_out_rec = (part, geo[0], geo[1])
+        else:
+            conv_forward(cs2, a2, b2, res=xb, y=out)
+            blk._fv_out_rec = None
         cs1.release()
         cs2.release()
         ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm = blk, cs1, cs2, r1, r2, comm
@@ -540,10 +647,15 @@ class ResBlockFn(torch.autograd.Function):
         blk, cs1, cs2, r1, r2, comm = ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm
         C = xb.shape[1]
         dout = grad_in(dout, xb.dtype)
-        da2, dw2, db2 = conv_backward(cs2, a2, dout, C)
-        dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm)
-        da1, dw1, db1 = conv_backward(cs1, a1, dt1, C)
-        dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout)
+        # (the BN-backward sums stay a separate pass here: fused into the 256-channel dgrad's
+        # store pass they cost that kernel +29 us per launch against the pass's 27 us,
+        # profiles/r2b_*; FV_RES_SR=1 re-enables it for A/B)
+        br2 = (blk.bn2, r2, t1, 0.0) if _RES_SR else None
+        br1 = (blk.bn1, r1, xb, 0.0) if _RES_SR else None
+        da2, dw2, db2, rec2 = conv_backward(cs2, a2, dout, C, bnred=br2, want_recs=True)
+        dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, recs=rec2)
+        da1, dw1, db1, rec1 = conv_backward(cs1, a1, dt1, C, bnred=br1, want_recs=True)
+        dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout, recs=rec1)
         dx = from_nhwc(dxb, x)
         return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None
 

@@ -117,6 +117,34 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
 int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab,
                            float* dw_param, float* db, void* stream);
 
+/* store-pass reductions of the halo-staged 3x3 kernels (fused into the bf16 store of the
+ * output tile; one record per 256-pixel tile and wave, [records][2][cout] fp32):
+ *   mode 1 (fv_conv2d_fwd_sr): (sum, sum of squares) of the stored output AFTER the residual
+ *          add -- the statistics of the next BatchNorm (ResBlock2D's x + t feeding the next
+ *          block's NAC, modules.py:125 -> 13);
+ *   mode 2 (fv_conv2d_bwd_data_sr): the SyncBatchNorm backward sums (sum g, sum g * yhat) of
+ *          the BN whose output gradient the data gradient produces: g = dx * act'(gamma * yhat
+ *          + beta), yhat = (bn_input - mean) * invstd (replaces fv_bn_act_bwd_reduce's pass).
+ * fv_conv2d_sr_records (dgrad = 1 for the data gradient of d) gives the record count, 0 when
+ * the launch path of d has no store-pass records (then use the separate passes). */
+typedef struct fv_store_reduce {
+  int mode;                /* 1 or 2 */
+  float* records;          /* [records][2][cout] */
+  const void* bn_input;    /* mode 2: the BN input y, NHWC like the output */
+  const float *mean, *invstd, *gamma, *beta;
+  float slope;             /* act slope (0 ReLU, 0.2 LeakyReLU) */
+} fv_store_reduce;
+int fv_conv2d_sr_records(const fv_conv_desc* d, int dgrad, int* record_pixels);
+int fv_conv2d_fwd_sr(const fv_conv_desc* d, const void* x, const void* wk, const float* bias, const void* res, void* y,
+                     const fv_store_reduce* sr, void* stream);
+int fv_conv2d_bwd_data_sr(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,
+                          const fv_store_reduce* sr, void* stream);
+/* BN backward from store-pass records: dgamma / dbeta (either may be NULL) and k [2][c] over
+ * `count` elements (fv_bn_bwd_finalize's outputs); red (optional, [2][c] doubles) receives the
+ * rank-local sums for a SyncBN all-reduce, then k comes from fv_bn_bwd_finalize_dev. */
+int fv_bn_bwd_from_records(const float* records, int nrec, int record_pixels, long pixels, int c, long count,
+                           float* dgamma, float* dbeta, float* k, double* red, void* ws, void* stream);
+
 /* ------------------------------------------- transposed conv (k4, s2, p1) ---- */
 /* ConvTranspose2dELR (models_utils.py:404-516; F.conv_transpose2d at :497-498) with
  * kernel 4, stride 2, padding 1, run as the sub-pixel phases of an upsample descriptor:
