@@ -75,6 +75,16 @@ _SIGS = {
     "fv_convt_supported": (c_int, [D]),
     "fv_convt_weight_prep": (c_int, [D, P, c_int, c_float, P, P, P, P]),
     "fv_convt_wgrad_reduce": (c_int, [D, P, P, P, c_int, c_float, P, P, P, P]),
+    "fv_convt_eff_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
+    "fv_convt_weight_grad": (c_int, [P, c_int, c_int, c_int, c_int, c_float, P, P, P]),
+    "fv_convt_direct_fwd": (c_int, [c_int, P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int,
+                                    c_int, P, P]),
+    "fv_convt_direct_dgrad": (c_int, [c_int, P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int,
+                                      c_int, P, P]),
+    "fv_convt_direct_wgrad": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      c_int, P, P, P]),
+    "fv_chan_scale_fwd": (c_int, [c_int, P, c_int, c_long, c_int, c_int, P, P, P, P]),
+    "fv_chan_scale_bwd": (c_int, [c_int, P, P, c_int, c_long, c_int, c_int, P, P, P, P, P]),
     "fv_fp8_ws_bytes": (c_size_t, []),
     "fv_quantize_fp8": (c_int, [c_int, P, c_long, P, P, P, P]),
     "fv_conv2d_fp8_supported": (c_int, [D]),

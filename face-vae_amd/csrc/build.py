@@ -16,7 +16,7 @@ PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
 OUT = os.path.join(PKG, "libfacevae.so")
 BUILD = os.path.join(HERE, "build")
-SOURCES = ["abi.cpp", "conv.hip", "conv3d.hip", "warp.hip", "vgg.hip", "bn.hip", "misc.hip", "comm.cpp"]
+SOURCES = ["abi.cpp", "conv.hip", "conv3d.hip", "warp.hip", "vgg.hip", "convt.hip", "bn.hip", "misc.hip", "comm.cpp"]
 HEADERS = ["common.h", os.path.join(ROOT, "include", "facevae.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",

@@ -6,10 +6,10 @@ into `train/` and `test/`; with `id_sampling` the training set is the set of ide
 item picks a random video of the identity, then two random frames (sorted indices), returned
 as `(source, driving, source_aug, driving_aug)` float32 CHW arrays in [0, 1]
 (dataset.py:91-129).  Frames are decoded with PIL (skimage is not in this image; for uint8
-PNGs `img_as_float32` is the same division by 255).  The reference's augmentation
-(`AllAugmentationTransform`: rotation / perspective / colour jitter, augmentation.py:384-418)
-feeds only the keypoint / contrastive losses, not the FaceVAE path, and is not rebuilt: the
-`*_aug` items are copies of the un-augmented frames.
+PNGs `img_as_float32` is the same division by 255).  The `*_aug` items go through
+`augmentation.AllAugmentationTransform` with the reference's default parameters (rotation
+30 degrees, perspective (30, 40), colour jitter 0.1, dataset.py:52-57), each frame on its own
+as dataset.py:122-123; they feed the keypoint / contrastive losses, not the FaceVAE path.
 
 `SyntheticFramesDataset` produces VoxCeleb-shaped frames x ~ U[0, 1) deterministically per
 index (the benchmark / test input when no dataset is on disk).
@@ -37,9 +37,16 @@ def _train_test_split(videos: Sequence[str], random_seed: int, test_size: float 
     return train_test_split(list(videos), random_state=random_seed, test_size=test_size)
 
 
+DEFAULT_AUGMENTATION = {
+    "rotation_param": {"degrees": 30},
+    "perspective_param": {"pers_num": 30, "enlarge_num": 40},
+    "jitter_param": {"brightness": 0.1, "contrast": 0.1, "saturation": 0.1, "hue": 0.1},
+}
+
+
 class FramesDataset(Dataset):
     def __init__(self, root_dir: str, frame_shape=(256, 256, 3), id_sampling: bool = True, is_train: bool = True,
-                 random_seed: int = 0, pairs_list: Optional[str] = None, augmentation_params=None):
+                 random_seed: int = 0, pairs_list: Optional[str] = None, augmentation_params=DEFAULT_AUGMENTATION):
         self.root_dir = root_dir
         self.videos = os.listdir(root_dir)
         self.frame_shape = tuple(frame_shape)
@@ -59,6 +66,8 @@ class FramesDataset(Dataset):
             train_videos, test_videos = _train_test_split(self.videos, random_seed)
         self.videos = train_videos if is_train else test_videos
         self.is_train = is_train
+        from .augmentation import AllAugmentationTransform
+        self.transform = AllAugmentationTransform(**(augmentation_params or {})) if is_train else None
 
     def __len__(self):
         return len(self.videos)
@@ -81,7 +90,12 @@ class FramesDataset(Dataset):
             arr = [_read_frame(os.path.join(path, frames[i])) for i in fidx]
             source = np.ascontiguousarray(arr[0].transpose(2, 0, 1))
             driving = np.ascontiguousarray(arr[1].transpose(2, 0, 1))
-            return source, driving, source.copy(), driving.copy()
+            if self.transform is None:
+                return source, driving, None, None
+            s_aug = np.array(self.transform([arr[0].copy()])[0], dtype=np.float32)
+            d_aug = np.array(self.transform([arr[1].copy()])[0], dtype=np.float32)
+            return (source, driving, np.ascontiguousarray(s_aug.transpose(2, 0, 1)),
+                    np.ascontiguousarray(d_aug.transpose(2, 0, 1)))
         video = np.stack([_read_frame(os.path.join(path, f)) for f in frames])
         return np.ascontiguousarray(video.transpose(3, 0, 1, 2))
 

@@ -8,6 +8,7 @@ u/v), so `torch.manual_seed(s)` gives bit-identical initial weights.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -300,16 +301,37 @@ class Conv2d(_Conv):
         return ops.ConvFn.apply(x, self.weight, self.bias, self, self.compute_dtype(), int(sigmoid))
 
 
+class LinearELR(nn.Module):
+    """LinearELR (models_utils.py:134-203) with act=None, norm=None: the style affine of a
+    modulated ConvTranspose2dELR.  Same parameters and init draw; the tiny [B, wsize] x
+    [wsize, outch] product runs as torch.addmm (alpha = weightgain), as the reference."""
+
+    def __init__(self, inch, outch, lrmult=1., norm=None, act=None):
+        super().__init__()
+        if norm is not None or act is not None:
+            raise NotImplementedError("LinearELR: norm=None, act=None only (the ConvTranspose2dELR affine)")
+        self.weight = nn.Parameter(torch.randn(outch, inch) / lrmult)
+        self.weightgain = 1. / math.sqrt(inch) * lrmult
+        self.bias = nn.Parameter(torch.full([outch], 0.))
+
+    def forward(self, x):
+        return torch.addmm(self.bias[None], x, self.weight.t(), alpha=self.weightgain)
+
+
 class ConvTranspose2dELR(nn.Module):
     """Drop-in for `ConvTranspose2dELR` (models_utils.py:404-516): a transposed conv with an
-    equalised-learning-rate gain and optional per-output-channel weight demodulation, same
-    constructor, parameter names (`weight` [inch, outch, k, k], `bias`) and init RNG draw
-    (`blockinit(randn(inch, outch, k//s, k//s), s)`, models_utils.py:283-288, 435-436).
+    equalised-learning-rate gain, optional per-output-channel weight demodulation and optional
+    per-sample affine modulation (wsize > 0, forward(x, w)); same constructor, parameter names
+    (`weight` [inch, outch, k, k], `bias`, `affine.weight/bias`) and init RNG draws
+    (`blockinit(randn(inch, outch, k//s, k//s), s)`, models_utils.py:283-288, 435-446).
 
-    Computed by the HIP sub-pixel kernels for kernel_size 4, stride 2, padding 1 (the
-    upsampling configuration), bf16 operands / fp32 accumulation; other geometries and the
-    per-sample affine modulation (wsize > 0 with a style input) raise.  The untied bias (ub)
-    and the optional activation module are applied after the kernel, as the reference does
+    Kernel size 4 / stride 2 / padding 1 at power-of-two sizes in bf16 runs on the sub-pixel
+    MFMA kernels (ops.ConvTranspose2dFn); every other geometry, and fp32 parity mode, on the
+    direct kernels of convt.hip (ops.ConvTranspose2dDirectFn).  Modulation is moved from the
+    weights onto the activations: conv_t(x, W * s_b[i]) = conv_t(x * s_b, W), and the per-sample
+    demodulation is an output-channel scale gain / ||W * s_b||_(i,r,s) (ops.ChanScaleFn); the
+    [B, inch] / [B, outch] factors are formed with torch ops on those small tensors.  The untied
+    bias (ub) and the activation module are applied after the kernel, as the reference does
     (models_utils.py:507-514)."""
 
     def __init__(self, inch, outch, kernel_size, stride, padding, wsize=0, affinelrmult=1., norm=None, ub=None,
@@ -318,9 +340,6 @@ class ConvTranspose2dELR(nn.Module):
         self.inch, self.outch = inch, outch
         self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
         self.wsize, self.norm, self.ub, self.act = wsize, norm, ub, act
-        if wsize > 0:
-            raise NotImplementedError("ConvTranspose2dELR: per-sample affine modulation (wsize > 0) is not on the "
-                                      "FaceVAE path (SURVEY.md §8a-a15)")
         # models_utils.py:420-433: gain from the activation, then the init gain
         try:
             if isinstance(act, nn.LeakyReLU):
@@ -338,8 +357,16 @@ class ConvTranspose2dELR(nn.Module):
         w = torch.randn(inch, outch, k, k)
         self.weight = nn.Parameter(w.repeat_interleave(stride, dim=2).repeat_interleave(stride, dim=3).contiguous())
         self.bias = nn.Parameter(torch.zeros(outch, ub[0], ub[1]) if ub is not None else torch.zeros(outch))
-        self.affine = None
+        self.affine = LinearELR(wsize, inch, lrmult=affinelrmult) if wsize > 0 else None
         self.fused = False
+        self._dtype = None
+
+    def compute_dtype(self):
+        return ops.storage(self._dtype or config.compute_dtype())
+
+    def set_compute_dtype(self, dtype):
+        self._dtype = dtype
+        return self
 
     def extra_repr(self):
         return (f"inch={self.inch}, outch={self.outch}, kernel_size={self.kernel_size}, stride={self.stride}, "
@@ -347,6 +374,8 @@ class ConvTranspose2dELR(nn.Module):
 
     def fuse(self):
         """Bake gain (and demodulation) into `weight` (models_utils.py:474-478)."""
+        if self.affine is not None:
+            return
         with torch.no_grad():
             w = self.weight
             if self.norm == "demod":
@@ -354,14 +383,32 @@ class ConvTranspose2dELR(nn.Module):
             self.weight.data = (w * self.weightgain).contiguous()
         self.fused = True
 
+    def _core(self, x, bias, demod, gain, dtype):
+        k, s, p = self.kernel_size, self.stride, self.padding
+        if dtype == torch.bfloat16 and (k, s, p) == (4, 2, 1) and x.dim() == 4:
+            N, inch, Hi, Wi = x.shape
+            d = ops.desc(dtype, N, 2 * Hi, 2 * Wi, ops.pad_pow2(inch), inch, self.outch, self.outch, 3, ups=1)
+            if ops.query("fv_convt_supported", ctypes.byref(d)):
+                return ops.ConvTranspose2dFn.apply(x, self.weight, bias, demod, gain)
+        return ops.ConvTranspose2dDirectFn.apply(x, self.weight, bias, k, s, p, demod, gain, dtype)
+
     def forward(self, x, w=None):
-        if (self.kernel_size, self.stride, self.padding) != (4, 2, 1):
-            raise NotImplementedError("ConvTranspose2dELR: only kernel_size=4, stride=2, padding=1 runs on the "
-                                      "HIP kernels")
+        dtype = self.compute_dtype()
         demod = self.norm == "demod" and not self.fused
         gain = 1.0 if self.fused else self.weightgain
         tied = self.bias.dim() == 1
-        out = ops.ConvTranspose2dFn.apply(x, self.weight, self.bias if tied else None, demod, gain)
+        if self.affine is not None and w is not None:
+            sb = self.affine(w) * 0.1 + 1.                          # [B, inch] (models_utils.py:488-489)
+            if demod:                                               # per (b, o) over dims [1, 3, 4]
+                wsq = (self.weight * self.weight).sum(dim=(2, 3))   # [inch, outch]
+                scale = gain / torch.sqrt(torch.matmul(sb * sb, wsq)).clamp_min(1e-12)
+            else:
+                scale = torch.full((x.shape[0], self.outch), gain, device=x.device)
+            xm = ops.ChanScaleFn.apply(x, sb, None, dtype)
+            out = self._core(xm, None, False, 1.0, dtype)
+            out = ops.ChanScaleFn.apply(out, scale, self.bias[None].expand(x.shape[0], -1) if tied else None, dtype)
+        else:
+            out = self._core(x, self.bias if tied else None, demod, gain, dtype)
         if not tied:
             out = out + self.bias[None].to(out.dtype)
         if self.act is not None:

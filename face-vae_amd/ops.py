@@ -913,3 +913,78 @@ class ConvTranspose2dFn(torch.autograd.Function):
             call("fv_conv2d_bwd_data", ctypes.byref(d), ptr(dy), d.cout, ptr(ctx.wt), ptr(dxb), stream())
             dx = from_nhwc(dxb, x)
         return dx, dw, db, None, None
+
+
+class ConvTranspose2dDirectFn(torch.autograd.Function):
+    """F.conv_transpose2d(x, gain * [demod-normalised] W, stride, padding) + bias for any
+    geometry and for fp32 parity mode (ConvTranspose2dELR.getweight/forward,
+    models_utils.py:454-505) on the direct kernels of convt.hip."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, k, stride, pad, demod, gain, dtype):
+        xb, ldx = to_nhwc(x, dtype)
+        N, inch, Hi, Wi = x.shape
+        outch = weight.shape[1]
+        if weight.dtype != F32 or not weight.is_contiguous():
+            raise RuntimeError("conv_transpose2d weights must be contiguous fp32")
+        Ho, Wo = (Hi - 1) * stride - 2 * pad + k, (Wi - 1) * stride - 2 * pad + k
+        dev = x.device
+        inv = torch.empty(outch, dtype=F32, device=dev)
+        we = torch.empty_like(weight)
+        call("fv_convt_eff_weight", ptr(weight), inch, outch, k, int(demod), float(gain), ptr(inv), ptr(we), stream())
+        y = torch.empty((N, outch, Ho, Wo), dtype=dtype, device=dev, memory_format=CL)
+        call("fv_convt_direct_fwd", L.dtype_code(dtype), ptr(xb), N, Hi, Wi, inch, ldx, ptr(we), ptr(bias), outch, outch,
+             k, stride, pad, ptr(y), stream())
+        ctx.geo = (k, stride, pad, int(demod), float(gain), ldx)
+        ctx.dtype, ctx.has_bias = dtype, bias is not None
+        ctx.save_for_backward(x, xb, weight, we, inv)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, xb, weight, we, inv = ctx.saved_tensors
+        k, stride, pad, demod, gain, ldx = ctx.geo
+        N, inch, Hi, Wi = x.shape
+        outch = weight.shape[1]
+        dyb = dy.to(ctx.dtype).contiguous(memory_format=CL)
+        g = torch.empty_like(weight)
+        db = torch.empty(outch, dtype=F32, device=dy.device) if ctx.has_bias else None
+        call("fv_convt_direct_wgrad", L.dtype_code(ctx.dtype), ptr(xb), ptr(dyb), N, Hi, Wi, inch, ldx, outch, outch, k,
+             stride, pad, ptr(g), ptr(db), stream())
+        call("fv_convt_weight_grad", ptr(weight), inch, outch, k, demod, gain, ptr(inv), ptr(g), stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dxb = torch.empty((N, ldx, Hi, Wi), dtype=ctx.dtype, device=dy.device, memory_format=CL)
+            call("fv_convt_direct_dgrad", L.dtype_code(ctx.dtype), ptr(dyb), N, Hi, Wi, inch, ldx, ptr(we), outch, outch,
+                 k, stride, pad, ptr(dxb), stream())
+            dx = from_nhwc(dxb, x)
+        return dx, g, db, None, None, None, None, None, None
+
+
+class ChanScaleFn(torch.autograd.Function):
+    """y[n, c] = x[n, c] * sa[n, c] (+ sb[n, c]) over an NHWC activation (the per-sample
+    modulation / demodulation of ConvTranspose2dELR, models_utils.py:486-495)."""
+
+    @staticmethod
+    def forward(ctx, x, sa, sb, dtype):
+        xb, ld = to_nhwc(x, dtype)
+        N, C, H, W = x.shape
+        sa32 = sa.float().contiguous()
+        sb32 = sb.float().contiguous() if sb is not None else None
+        y = torch.empty((N, ld, H, W), dtype=dtype, device=x.device, memory_format=CL).zero_() if ld != C else torch.empty_like(xb)
+        call("fv_chan_scale_fwd", L.dtype_code(dtype), ptr(xb), N, H * W, C, ld, ptr(sa32), ptr(sb32), ptr(y), stream())
+        ctx.save_for_backward(x, xb, sa32)
+        ctx.dtype, ctx.has_sb = dtype, sb is not None
+        return y if ld == C else from_nhwc(y, x.to(dtype))
+
+    @staticmethod
+    def backward(ctx, g):
+        x, xb, sa32 = ctx.saved_tensors
+        N, C, H, W = x.shape
+        gb, ld = to_nhwc(g, ctx.dtype)
+        dx = torch.zeros_like(xb) if ctx.needs_input_grad[0] else None
+        da = torch.empty((N, C), dtype=F32, device=g.device)
+        db = torch.empty((N, C), dtype=F32, device=g.device) if ctx.has_sb else None
+        call("fv_chan_scale_bwd", L.dtype_code(ctx.dtype), ptr(gb), ptr(xb), N, H * W, C, ld, ptr(sa32), ptr(dx),
+             ptr(da), ptr(db), stream())
+        return (from_nhwc(dx, x) if dx is not None else None), da, db, None

@@ -164,6 +164,28 @@ int fv_convt_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float*
                           const float* w, int demod, float gain, const float* inv, float* dw,
                           float* db, void* stream);
 
+/* any geometry / fp32 (convt.hip, direct kernels; NHWC, x channel stride ldx, out stride ldy):
+ * W_eff = gain * W [/ max(||W[:, o, :, :]||, 1e-12) when demod] -> we [cin][cout][k][k] fp32
+ * (inv [cout] receives the inverse norms); out = conv_transpose2d(x, W_eff, stride, pad) + bias;
+ * the data gradient; g = dL/dW_eff (+ db); fv_convt_weight_grad turns g into dL/dW in place. */
+int fv_convt_eff_weight(const float* w, int cin, int cout, int k, int demod, float gain, float* inv, float* we,
+                        void* stream);
+int fv_convt_weight_grad(const float* w, int cin, int cout, int k, int demod, float gain, const float* inv, float* g,
+                         void* stream);
+int fv_convt_direct_fwd(int dtype, const void* x, int n, int hi, int wi, int cin, int ldx, const float* we,
+                        const float* bias, int cout, int ldy, int k, int stride, int pad, void* y, void* stream);
+int fv_convt_direct_dgrad(int dtype, const void* dy, int n, int hi, int wi, int cin, int ldx, const float* we,
+                          int cout, int ldy, int k, int stride, int pad, void* dx, void* stream);
+int fv_convt_direct_wgrad(int dtype, const void* x, const void* dy, int n, int hi, int wi, int cin, int ldx, int cout,
+                          int ldy, int k, int stride, int pad, float* g, float* db, void* stream);
+/* per-sample channel affine y[n][p][c] = x[n][p][c] * sa[n][c] (+ sb[n][c]) (the weight
+ * modulation x * (affine(w) * 0.1 + 1) and the per-sample demodulation of
+ * models_utils.py:486-495, moved onto the activations) and its backward (dx may be NULL) */
+int fv_chan_scale_fwd(int dtype, const void* x, int n, long hw, int c, int ld, const float* sa, const float* sb,
+                      void* y, void* stream);
+int fv_chan_scale_bwd(int dtype, const void* g, const void* x, int n, long hw, int c, int ld, const float* sa, void* dx,
+                      float* da, float* db, void* stream);
+
 /* ------------------------------------------------- fp8 conv path (config C5) ---- */
 /* OCP e4m3 operands with per-tensor power-of-two scales: a tensor v is stored as
  * fp8(v * s), s = 2^floor(log2(448 / amax|v|)), with dq = 1 / s (a device float) beside it.

@@ -495,3 +495,23 @@ def convt_elr(x, weight, bias, stride, padding, norm, gain, act_slope=None):
     if act_slope is not None:
         out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
     return out
+
+
+def convt_elr_mod(x, wstyle, weight, bias, aff_w, aff_b, aff_gain, stride, padding, norm, gain, act_slope=None):
+    """ConvTranspose2dELR.forward with the per-sample affine modulation (models_utils.py:484-505):
+    s = LinearELR(w) * 0.1 + 1 (addmm with alpha = weightgain, :197-198), weight * s over the input
+    channels, F.normalize over dims [1, 3, 4] when demod, times gain, grouped conv_transpose2d."""
+    b = x.shape[0]
+    aff = torch.addmm(aff_b[None], wstyle, aff_w.t(), alpha=aff_gain)
+    w = weight[None] * (aff[:, :, None, None, None] * 0.1 + 1.)
+    if norm == "demod":
+        w = F.normalize(w, dim=[1, 3, 4])
+    w = w * gain
+    inch, outch, k = weight.shape[0], weight.shape[1], weight.shape[2]
+    out = F.conv_transpose2d(x.reshape(1, b * inch, x.shape[2], x.shape[3]), w.reshape(b * inch, outch, k, k), None,
+                             stride=stride, padding=padding, groups=b)
+    out = out.view(b, outch, out.shape[2], out.shape[3])
+    out = out + (bias[None, :, None, None] if bias.dim() == 1 else bias[None])
+    if act_slope is not None:
+        out = F.leaky_relu(out, act_slope) if act_slope > 0 else F.relu(out)
+    return out

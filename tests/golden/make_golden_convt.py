@@ -21,6 +21,11 @@ CASES = {
     "plain_untied": (4, 8, 4, 2, 1, None, (10, 12), None, (1, 4, 5, 6)),
     "demod_relu_k3s1": (5, 8, 3, 1, 1, "demod", None, 0.0, (2, 5, 6, 6)),
 }
+MOD_CASES = {
+    # name: (inch, outch, k, s, p, norm, wsize, act_slope, x shape)
+    "mod_demod_leaky": (6, 8, 4, 2, 1, "demod", 5, 0.2, (2, 6, 5, 7)),
+    "mod_plain_k3s1": (5, 8, 3, 1, 1, None, 4, None, (3, 5, 6, 6)),
+}
 GPU_SHAPE = (64, 64, 4, 2, 1, "demod")    # tests/test_kernels_gpu.py::test_conv_transpose_elr
 
 
@@ -43,6 +48,24 @@ def main():
         out[name] = {"weight": w0, "bias": b0, "x": x.detach(), "g": g, "y": y.detach(), "dx": x.grad,
                      "dweight": m.weight.grad, "dbias": m.bias.grad,
                      "weightgain": torch.tensor(m.weightgain, dtype=torch.float64)}
+    # per-sample affine modulation (wsize > 0, forward(x, w)): models_utils.py:444-446, 486-495
+    for j, (name, (inch, outch, k, s, p, norm, wsize, slope, xs)) in enumerate(MOD_CASES.items()):
+        act = None if slope is None else nn.LeakyReLU(slope)
+        torch.manual_seed(500 + j)
+        m = MU.ConvTranspose2dELR(inch, outch, k, s, p, wsize=wsize, norm=norm, act=act)
+        with torch.no_grad():
+            m.bias.normal_(generator=torch.Generator().manual_seed(600 + j))
+            m.affine.bias.normal_(generator=torch.Generator().manual_seed(610 + j))
+        init = {kk: v.detach().clone() for kk, v in m.state_dict().items()}
+        x = torch.randn(*xs, generator=torch.Generator().manual_seed(700 + j)).requires_grad_(True)
+        wv = torch.randn(xs[0], wsize, generator=torch.Generator().manual_seed(710 + j)).requires_grad_(True)
+        y = m(x, wv)
+        g = torch.randn(y.shape, generator=torch.Generator().manual_seed(720 + j))
+        y.backward(g)
+        out[name] = {"init": init, "x": x.detach(), "w": wv.detach(), "g": g, "y": y.detach(), "dx": x.grad,
+                     "dw": wv.grad, "grads": {kk: v.grad.clone() for kk, v in m.named_parameters()},
+                     "weightgain": torch.tensor(m.weightgain, dtype=torch.float64),
+                     "affine_gain": torch.tensor(m.affine.weightgain, dtype=torch.float64)}
     inch, outch, k, s, p, norm = GPU_SHAPE
     torch.manual_seed(0)
     m = MU.ConvTranspose2dELR(inch, outch, k, s, p, norm=norm)

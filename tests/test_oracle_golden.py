@@ -188,3 +188,42 @@ def test_convt_elr_module_init_matches_reference():
     m = fv.ConvTranspose2dELR(64, 64, 4, 2, 1, norm="demod")
     assert torch.equal(m.weight.detach()[0, 0], gold["gpu_init"]["weight_00"])
     assert abs(m.weight.double().sum().item() - gold["gpu_init"]["sum"].item()) < 1e-9
+
+
+MOD_CASES = {
+    "mod_demod_leaky": (6, 8, 4, 2, 1, "demod", 5, 0.2),
+    "mod_plain_k3s1": (5, 8, 3, 1, 1, None, 4, None),
+}
+
+
+@pytest.mark.parametrize("name", list(MOD_CASES))
+def test_convt_elr_modulated_oracle_matches_reference(name):
+    """Modulated ConvTranspose2dELR restatement (oracle.convt_elr_mod) vs the reference module."""
+    g = load("convt_elr.pt")[name]
+    inch, outch, k, s, p, norm, wsize, slope = MOD_CASES[name]
+    gain = O.convt_elr_gain(inch, k, s, norm, slope)
+    assert abs(gain - g["weightgain"].item()) < 1e-12
+    assert abs(1.0 / wsize ** 0.5 - g["affine_gain"].item()) < 1e-12
+    prm = {kk: v.clone().requires_grad_(True) for kk, v in g["init"].items()}
+    x, w = g["x"].clone().requires_grad_(True), g["w"].clone().requires_grad_(True)
+    y = O.convt_elr_mod(x, w, prm["weight"], prm["bias"], prm["affine.weight"], prm["affine.bias"],
+                        g["affine_gain"].item(), s, p, norm, gain, slope)
+    y.backward(g["g"])
+    assert rel(y.detach(), g["y"]) < 1e-6
+    assert rel(x.grad, g["dx"]) < 1e-5 and rel(w.grad, g["dw"]) < 1e-5
+    for kk, v in g["grads"].items():
+        assert rel(prm[kk].grad, v) < 1e-5, kk
+
+
+def test_convt_elr_modulated_module_init_matches_reference():
+    import fvamd  # noqa: F401
+    import facevae_amd as fv
+    for j, (name, (inch, outch, k, s, p, norm, wsize, slope)) in enumerate(MOD_CASES.items()):
+        g = load("convt_elr.pt")[name]
+        act = None if slope is None else torch.nn.LeakyReLU(slope)
+        torch.manual_seed(500 + j)
+        m = fv.ConvTranspose2dELR(inch, outch, k, s, p, wsize=wsize, norm=norm, act=act)
+        sd = m.state_dict()
+        assert set(sd) == set(g["init"])
+        for kk in ("weight", "affine.weight"):
+            assert torch.equal(sd[kk], g["init"][kk]), (name, kk)
