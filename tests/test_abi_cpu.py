@@ -87,3 +87,17 @@ def test_product_never_imports_oracle():
         if f.endswith(".py"):
             assert "oracle" not in re.sub(r"#.*", "", open(os.path.join(pkg, f)).read()).replace(
                 "oracle/", ""), f
+
+
+def test_full_size_afe_generator_state_dicts_match_reference():
+    """The reference's default AFE() (with its 3-D ResBlock3D trunk) and Generator() state-dict
+    keys, order and shapes (tests/golden/module_keys.json, from the reference classes): a
+    reference checkpoint's 'afe' / 'generator' entries load into the product modules."""
+    import json
+    import os
+    import fvamd  # noqa: F401
+    import facevae_amd as fv
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "module_keys.json")))
+    for name, mod in (("afe", fv.AFE()), ("generator", fv.Generator())):
+        got = [[k, list(v.shape)] for k, v in mod.state_dict().items()]
+        assert got == gold[name], name
