@@ -118,3 +118,55 @@ def test_generator_warp_bf16_vs_reference():
     # (16-32 channel, 512-pixel BN) trunk is stored in bf16, and the input gradients pass back
     # through 6 convs and 4 BN layers (measured: image 1.8e-3, input gradients 0.09-0.13)
     assert e["out"] < 2e-2 and max(e["d_fs"], e["d_occlusion"], e["d_deformation"]) < 2.5e-1
+
+
+def test_reference_size_afe_to_warped_generator_vs_oracle():
+    """The reference's full-size decoder input path (trainer.py:268, 296-297 without the keypoint
+    nets): fs = AFE()(x) [1, 32, 16, 64, 64] with its ResBlock3D trunk, then
+    Generator()(fs, deformation, occlusion) at 256x256 in fp32 parity mode, against the CPU
+    oracle on the same weights run in float64.  Forward: 1e-3 (north_star).  Weight gradients:
+    at this depth the reference's own fp32 arithmetic (the oracle in float32) is already up to
+    ~1e-2 away from float64 (BatchNorm-backward cancellation, compounding through 18 BN layers),
+    so each parameter's error is gated at 2x the fp32 reference's own error + 1e-4: the product
+    is as accurate as the reference computed in fp32."""
+    from oracle import facevae_cpu as O
+    torch.manual_seed(3)
+    afe, gen = fv.AFE(), fv.Generator()
+    base = {**{f"afe.{k}": v for k, v in afe.state_dict().items()},
+            **{f"generator.{k}": v for k, v in gen.state_dict().items()}}
+    g = torch.Generator().manual_seed(4)
+    x = torch.rand(1, 3, 256, 256, generator=g)
+    ident = warp.make_coordinate_grid_3d((16, 64, 64))[None]
+    deform = ident + 0.05 * torch.randn(1, 16, 64, 64, 3, generator=g)
+    occ = torch.sigmoid(torch.randn(1, 1, 64, 64, generator=g))
+    gy = torch.randn(1, 3, 256, 256, generator=g)
+    afe = afe.cuda().train().set_compute_dtype(torch.float32)
+    gen = gen.cuda().train().set_compute_dtype(torch.float32)
+    fs = afe(x.cuda())
+    y = gen(fs, deform.cuda(), occ.cuda())
+    (y * gy.cuda()).sum().backward()
+    torch.cuda.synchronize()
+    ref = {}
+    for dt in (torch.float64, torch.float32):
+        sd = O.prepare_state(base)
+        sd = {k: (v.detach().to(dt).requires_grad_(v.requires_grad) if v.is_floating_point() else v.clone())
+              for k, v in sd.items()}
+        fso = O.encode_afe(sd, x.to(dt), [64, 128, 256], 32, 16, 6, True)
+        yo = O.generator_warp(sd, fso, deform.to(dt), occ.to(dt), n_res=6, n_up=2, training=True)
+        (yo * gy.to(dt)).sum().backward()
+        ref[dt] = (fso.detach(), yo.detach(), {k: v.grad for k, v in sd.items() if v.grad is not None})
+    f64, f32 = ref[torch.float64], ref[torch.float32]
+    fwd = {"fs": rel(fs, f64[0]), "image": rel(y, f64[1])}
+    prm = {**{f"generator.{k}": p for k, p in gen.named_parameters()}, **{f"afe.{k}": p for k, p in afe.named_parameters()}}
+    worst = []
+    for k, p in prm.items():
+        if k.endswith("bias"):
+            continue
+        e_prod, e_ref = rel(p.grad, f64[2][k]), rel(f32[2][k], f64[2][k])
+        worst.append((e_prod / (2 * e_ref + 1e-4), k, e_prod, e_ref))
+    worst.sort(reverse=True)
+    print("\nfull-size AFE -> warped Generator, fp32 vs float64 oracle: "
+          + " ".join(f"{k} {v:.2e}" for k, v in fwd.items()) + " | weight grads (product, fp32 reference): "
+          + " ".join(f"{k} {a:.1e}/{b:.1e}" for _, k, a, b in worst[:4]))
+    assert max(fwd.values()) < 1e-3, fwd
+    assert worst[0][0] < 1.0, worst[:4]
