@@ -2900,6 +2900,9 @@ int halo3_bn(const fv_conv_desc* d) {
   // the res convs; FV_H3_256=0 keeps conv_fwd_v2 for A/B)
   static const bool h3_256 = !getenv("FV_H3_256") || atoi(getenv("FV_H3_256")) != 0;
   if (d->cout % 256 == 0) return h3_256 ? 256 : 0;
+  // AFE.down1's forward (64 -> 128 channels, K = 576): conv_fwd_v2's 128 x 256 tile measured
+  // 500 us against 543 (pipelined halo) / 579 (single-tap halo) at 256x256, B=32
+  if (d->cin == 64 && d->cout == 128 && !getenv("FV_H3_DOWN1")) return 0;
   return d->cout % 128 == 0 ? 128 : d->cout % 64 == 0 ? 64 : 0;
 }
 
@@ -3590,10 +3593,11 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.ntn = d->cout / bn;
     const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
-    // 256: pipelined (1 block/CU either way); 128 / 64: the 2-blocks-per-CU single-tap loop
-    // wins (FV_H3_PIPE=0/1 forces one for A/B)
+    // pipelined pair-of-taps kernel for every co tile (r2 convbench, 256x256 B=32: down2 dgrad
+    // 369 -> 324 us, down1 dgrad 433 -> 414 us against the single-tap loop; FV_H3_PIPE=0/1
+    // forces one for A/B)
     static const int pipe_env = getenv("FV_H3_PIPE") ? atoi(getenv("FV_H3_PIPE")) : -1;
-    const int pipe = pipe_env >= 0 ? pipe_env : bn == 256;
+    const int pipe = pipe_env >= 0 ? pipe_env : 1;
     if (bn == 256) {
       static const int nsb = getenv("FV_H3_NSB") ? atoi(getenv("FV_H3_NSB")) : 2;   // 3: deeper ring (A/B: 2.5 % slower)
       if (pipe && nsb == 2) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
