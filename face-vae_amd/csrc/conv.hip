@@ -3005,16 +3005,18 @@ bool use_subpix(const fv_conv_desc* d) {
 }
 
 // sub-pixel phases through the halo-staged kernel: co tile (128 / 64), 0 when not eligible
-static int g_disable_h3sub = -1;
+// Off by default: an alternating A/B on one box (r2, 4 reps each) put up1's forward at
+// 214.9 us through this path against 193.7 us through conv_fwd_v2 MODE 2, and up2 (64-channel
+// co tiles) was already 5 % faster on v2.  FV_H3SUB=1 turns it back on for A/B runs.
+static int g_h3sub = -1;
 int subpix_halo_bn(const fv_conv_desc* d) {
-  if (g_disable_h3sub < 0) {
-    const char* e = getenv("FV_DISABLE_H3SUB");
-    g_disable_h3sub = (e && e[0] == '1') ? 1 : 0;
+  if (g_h3sub < 0) {
+    const char* e = getenv("FV_H3SUB");
+    g_h3sub = (e && e[0] == '1') ? 1 : 0;
   }
-  if (g_disable_h3sub || !use_subpix(d)) return 0;
+  if (!g_h3sub || !use_subpix(d)) return 0;
   const int hl = d->h / 2, wl = d->w / 2;
   if (wl % 64 || hl % 4 || d->cin % 32) return 0;
-  // co tiles of 128 only: up1 -17 %; with 64 (up2) conv_fwd_v2 MODE 2 stays 5 % faster
   return d->cout % 128 == 0 ? 128 : 0;
 }
 
