@@ -1121,6 +1121,161 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
 }
 
+// Linear-halo variant of conv3_halo_fwd2: every LDS fragment address is a per-lane base
+// register plus an immediate.  In fwd2 the XOR swizzle of a 64-B halo pixel moves with the tap
+// shift, so each of the 16 fragment reads of a step costs ~5 VALU (88 non-MFMA VALU per 64
+// MFMAs): with two waves per SIMD that fills most of the vector issue slots the MFMAs leave.
+// Here a halo pixel takes 96 B (64 B of channels + 32 B zero-filled by out-of-range DMA
+// slots): 16 consecutive pixels read by ds_read_b128 from ANY start are conflict-free, and the
+// address of pixel hp shifted by a tap is linear: a tap adds one wave-uniform offset to a
+// per-lane base and the fragments of the step are immediate offsets from it (measured in the
+// asm: 4 non-MFMA VALU per 64-MFMA step against 88).  LDS: [NSB weight stages][2 halo buffers].
+template <int WN, int WM, int RN, int RM, int NSB>
+__global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
+conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
+  constexpr int NW = WN * WM;
+  constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
+  static_assert(RM % 4 == 0, "a wave's pixels start on an image-row boundary of the tile");
+  constexpr int PXB = 96;                                  // LDS bytes per halo pixel
+  constexpr int HP = (TR + 2) * 66, HSL = HP * (PXB / 16), HQ = (HSL + 63) / 64, JH = (HQ + NW - 1) / NW;
+  constexpr int HALO = HQ * 1024;
+  constexpr int QB = BN / 16, JB = QB / NW;
+  static_assert(QB % NW == 0, "weight pieces per wave");
+  constexpr int BST = BN * 64, STG = 2 * BST, WOFF = NSB * STG;
+  constexpr int MAIN = WOFF + 2 * HALO, EPI = BM * BN * 2;
+  static_assert(MAIN <= 163840, "LDS");
+  static_assert(STG * (NSB - 1) + BST + (BN - 16) * 64 < 65536, "weight fragment immediates");
+  __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % WN, wm = wave / WN;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tn = lid % a.ntn, tm = lid / a.ntn;
+  const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
+  const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
+  const int co0 = tn * BN;
+  const int p0 = (n * a.H + th * TR) * a.W + tw * 64;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+  const int lrow = lane >> 2, lchk = lane & 3;
+
+  // halo slots of this wave: slot k = 16-B chunk k % 6 of halo pixel k / 6 (chunks 4, 5 pad)
+  unsigned hoff[JH];
+#pragma unroll
+  for (int j = 0; j < JH; ++j) {
+    const int k = (wave + j * NW) * 64 + lane;
+    const int hp = k / 6, ch = k - (k / 6) * 6;
+    const int hr = hp / 66, hc = hp - (hp / 66) * 66;
+    const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
+    const bool ok = hp < HP && ch < 4 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+    hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
+  }
+  // weight rows of piece jb are row0 + jb * NW * 16 (same chunk swizzle): one base register,
+  // the piece step goes into the scalar offset
+  const unsigned wbase = (unsigned)(((co0 + wave * 16 + lrow) * a.Kpad + ((lchk ^ rswz<bf16>(lrow)) << 3)) * 2);
+  const unsigned wstep = (unsigned)(NW * 16 * a.Kpad * 2);
+  const int nch = a.Cin >> 5, nsteps = 9 * nch / 2;
+  auto issue_b = [&](int j, int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = 2 * j + h;
+      const int c = u / 9, t = u - c * 9;
+      const unsigned Bs = sbase + buf * STG + h * BST;
+      const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
+#pragma unroll
+      for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, k0 * 2 + jb * wstep);
+    }
+  };
+  // one weight DMA piece q (0 .. 2 JB - 1) of stage j: tap half q / JB, row piece q % JB
+  auto issue_halo = [&](int c) {
+    const unsigned Hs = sbase + WOFF + (c & 1) * HALO;
+#pragma unroll
+    for (int j = 0; j < JH; ++j)
+      if (j < JH - 1 || wave + j * NW < HQ) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], (unsigned)(c * 64));
+  };
+
+  const int lr = lane & 15, lh = lane >> 4;
+  // per-lane bases: weight row wn*RN*16 + lr (chunk swizzle is a function of lr only), halo
+  // pixel of tile pixel wm*RM*16 + lr (RM*16 is a multiple of the 64-pixel tile row).  A tap
+  // adds one wave-uniform offset to each (2 VALU per tap); the fragments are immediates.
+  const int va = (wn * RN * 16 + lr) * 64 + ((lh ^ rswz<bf16>(lr)) << 4);
+  const int vb = WOFF + ((wm * RM / 4) * 66 + lr) * PXB + lh * 16;
+  auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], int u, int buf) {
+    const int c = u / 9, t = u - c * 9, r = t / 3, s3 = t - (t / 3) * 3;
+    const int pa = va + (buf * STG + (u & 1) * BST);
+    const int pb = vb + ((c & 1) * HALO + (r * 66 + s3) * PXB);
+#pragma unroll
+    for (int i = 0; i < RN; ++i) fa[i].lds(smem + pa + i * 1024);
+#pragma unroll
+    for (int m = 0; m < RM; ++m) fb[m].lds(smem + pb + (((m * 16) >> 6) * 66 + ((m * 16) & 63)) * PXB);
+  };
+  f32x4 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // the ring and halo schedule of conv3_halo_fwd2 (nch even: no odd last tap)
+  Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
+  auto bcnt = [&](int j) { return j < nsteps ? 2 * JB : 0; };
+  issue_b(0, 0);
+  issue_halo(0);
+  issue_halo(1);
+  for (int i = 1; i < NSB - 1; ++i)
+    if (i < nsteps) issue_b(i, i);
+  wait_vm<0>();
+  __syncthreads();
+  int pend = 0;
+  if (NSB - 1 < nsteps) {
+    issue_b(NSB - 1, NSB - 1);
+    pend = bcnt(NSB - 1);
+  }
+  load_frags(fa0, fb0, 0, 0);
+  int hn = 2, hstep = (9 * 2 - 10) / 2;
+  int bj = 0;
+  for (int j = 0; j < nsteps; ++j) {
+    load_frags(fa1, fb1, 2 * j + 1, bj);
+    mfma_all(fa0, fb0);
+    const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
+    if (j + 1 < nsteps) {
+      if constexpr (NSB == 2) wait_vm<0>();
+      else if (pend == 2 * JB) wait_vm<2 * JB>();
+      else wait_vm_dyn(pend);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (hn < nch && j == hstep) {
+        issue_halo(hn);
+        ++hn;
+        hstep = (9 * hn - 10) / 2;
+      }
+      pend = 0;
+      if (j + NSB < nsteps) {
+        issue_b(j + NSB, bj);
+        pend = bcnt(j + NSB);
+      }
+      load_frags(fa0, fb0, 2 * j + 2, bn1);
+    }
+    mfma_all(fa1, fb1);
+    bj = bn1;
+  }
+  __syncthreads();
+  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+}
+
 // ----------------------------------------------------------------------------------------
 // Halo-tiled 7x7 forward for a small channel side (bf16): AFE.in_conv 3->64 forward,
 // Generator.out_conv 64->3 forward and its 3->64 backward-data.  The block's TR x 64 output
@@ -3600,7 +3755,13 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // forces one for A/B)
     static const int pipe_env = getenv("FV_H3_PIPE") ? atoi(getenv("FV_H3_PIPE")) : -1;
     const int pipe = pipe_env >= 0 ? pipe_env : 1;
-    if (bn == 256) {
+    // linear-halo kernel (conv3_halo_fwd3); FV_H3_V3=0 falls back to fwd2 for A/B
+    static const int v3 = getenv("FV_H3_V3") ? atoi(getenv("FV_H3_V3")) : 1;
+    // (64-channel co tiles stay on fwd2: 448 -> 667 us for AFE.down1's data gradient)
+    if (pipe && v3 && bn >= 128 && a.Cin % 64 == 0) {
+      if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+      else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
+    } else if (bn == 256) {
       static const int nsb = getenv("FV_H3_NSB") ? atoi(getenv("FV_H3_NSB")) : 2;   // 3: deeper ring (A/B: 2.5 % slower)
       if (pipe && nsb == 2) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
       else if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
