@@ -1822,6 +1822,7 @@ struct Wg2Args {
   // the block's phase (pa, pb) pairs low-res pixel (n, i, j) with dy pixel (n, 2i+pa, 2j+pb)
   // of the Ho x Wo image; phase slabs follow each other ([4][nsplit][CW][KW])
   int Ho, Wo, nsplit;
+  int il;      // row-aligned stages: spread the next stage's DMA pieces between MFMAs
 };
 
 // 32-B-block XOR of a [row][NCOL] bf16 image: the 8 rows {0-3, 8-11} (and {4-7, 12-15}) one
@@ -1955,37 +1956,53 @@ conv_wgrad_v2(Wg2Args a) {
   for (int j = 0; j < JB; ++j) cB[j] = bok[j] ? (unsigned)(brow[j] * (SUB ? 2 : 1) * a.ldd + bco[j]) * 2u : 0x80000000u;
   const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
 
-  auto issue_rowal = [&](int st, int buf) {
+  // row-aligned stage: wave-uniform state once per stage, then one DMA piece at a time, so
+  // the pieces can be spread between MFMAs (a piece costs ~60 cycles among MFMAs, 100-185
+  // back to back; issued as a block, both waves of a SIMD stall on them together)
+  struct RowSt {
+    unsigned As, Bs, dpo;
+    int S, h, w0;
+    bool sok, odd;
+  };
+  auto rowal_state = [&](int st, int buf) {
+    RowSt r;
     const int pbase = (s_begin + st) * PX;
-    const unsigned As = sbase + buf * STAGE;
-    const unsigned Bs = As + SA;
+    r.As = sbase + buf * STAGE;
+    r.Bs = r.As + SA;
     const int hrow = (int)fdiv((uint32_t)pbase, a.fw);
-    const int w0 = pbase - hrow * a.W;
+    r.w0 = pbase - hrow * a.W;
     const int n = (int)fdiv((uint32_t)hrow, a.fh);
-    const int h = hrow - n * a.H;
-    const bool sok = pbase < a.P;
-    const int S = UPS ? ((((n * a.Hin + (h >> 1)) * a.Win + (w0 >> 1)) << a.lgCin) * 2)
-                      : ((((n * a.Hin + h) * a.Win + w0) << a.lgCin) * 2);
-    const bool odd = UPS && (h & 1);
-#pragma unroll
-    for (int j = 0; j < JA; ++j) {
-      const int q = wave + j * 8;
-      if (QA % 8 == 0 || q < QA) {
-        const bool ok = sok && (unsigned)(h + adh[j]) < (unsigned)a.H && (unsigned)(w0 + cwA[j]) < (unsigned)a.W;
-        const int c = odd ? cA1[j] : cA0[j];
-        dma16s(xr, As + q * 1024, ok ? (unsigned)(S + c) : 0x80000000u, 0u);
+    r.h = hrow - n * a.H;
+    r.sok = pbase < a.P;
+    r.S = UPS ? ((((n * a.Hin + (r.h >> 1)) * a.Win + (r.w0 >> 1)) << a.lgCin) * 2)
+              : ((((n * a.Hin + r.h) * a.Win + r.w0) << a.lgCin) * 2);
+    r.odd = UPS && (r.h & 1);
+    // dy pixel of the stage's first pixel: itself, or (n, 2h+pa, 2*w0+pb) for a phase
+    const unsigned dp = SUB ? (unsigned)((n * a.Ho + 2 * r.h + pa) * a.Wo + 2 * r.w0 + pb) : (unsigned)pbase;
+    r.dpo = dp * (unsigned)a.ldd * 2u;
+    return r;
+  };
+  // piece q in [0, JA + JB): x pieces first, then dy (compile-time q after unrolling)
+  auto rowal_piece = [&](const RowSt& r, int q) {
+    if (q < JA) {
+      const int j = q, qq = wave + j * 8;
+      if (QA % 8 == 0 || qq < QA) {
+        const bool ok = r.sok && (unsigned)(r.h + adh[j]) < (unsigned)a.H && (unsigned)(r.w0 + cwA[j]) < (unsigned)a.W;
+        const int c = r.odd ? cA1[j] : cA0[j];
+        dma16s(xr, r.As + qq * 1024, ok ? (unsigned)(r.S + c) : 0x80000000u, 0u);
+      }
+    } else {
+      const int j = q - JA, qq = wave + j * 8;
+      if (QB % 8 == 0 || qq < QB) {
+        if (r.sok) dma16s(dr, r.Bs + qq * 1024, cB[j], r.dpo);
+        else dma16s(dr, r.Bs + qq * 1024, 0x80000000u, 0u);
       }
     }
+  };
+  auto issue_rowal = [&](int st, int buf) {
+    const RowSt r = rowal_state(st, buf);
 #pragma unroll
-    for (int j = 0; j < JB; ++j) {
-      const int q = wave + j * 8;
-      if (QB % 8 == 0 || q < QB) {
-        // dy pixel of the stage's first pixel: itself, or (n, 2h+pa, 2*w0+pb) for a phase
-        const unsigned dp = SUB ? (unsigned)((n * a.Ho + 2 * h + pa) * a.Wo + 2 * w0 + pb) : (unsigned)pbase;
-        if (sok) dma16s(dr, Bs + q * 1024, cB[j], dp * (unsigned)a.ldd * 2u);
-        else dma16s(dr, Bs + q * 1024, 0x80000000u, 0u);
-      }
-    }
+    for (int q = 0; q < JA + JB; ++q) rowal_piece(r, q);
   };
 
   auto issue = [&](int st, int buf) {
@@ -2040,7 +2057,9 @@ conv_wgrad_v2(Wg2Args a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
 
-  auto compute = [&](int buf) {
+  // hook(i): called after MFMA row i of the first 32-pixel slice (the DMA pieces of the
+  // next stage go there)
+  auto compute_h = [&](int buf, auto&& hook) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + SA;
 #pragma unroll
@@ -2051,9 +2070,11 @@ conv_wgrad_v2(Wg2Args a) {
 #pragma unroll
       for (int i = 0; i < RK; ++i) af[i] = tfrag<BKT>(As, kk * 32, wk * RK * 16 + i * 16, lane);
 #pragma unroll
-      for (int i = 0; i < RK; ++i)
+      for (int i = 0; i < RK; ++i) {
 #pragma unroll
         for (int j = 0; j < RC; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if (kk == 0) hook(i);
+      }
       if (do_bias) {
 #pragma unroll
         for (int j = 0; j < RC; ++j) accb[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[j], accb[j], 0, 0, 0);
@@ -2066,13 +2087,31 @@ conv_wgrad_v2(Wg2Args a) {
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
     if (i < nst) issue(i, i);
-  for (int it = 0; it < nst; ++it) {
-    const int ahead = min(NS - 2, nst - 1 - it);   // younger stages allowed in flight
-    wait_ahead<NS, PW>(ahead);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (it + NS - 1 < nst) issue(it + NS - 1, (it + NS - 1) % NS);
-    compute(it % NS);
+  if ((SUB || a.rowal) && a.il) {
+    // the next stage's pieces spread over the first slice's MFMA rows (all issued within the
+    // iteration, in piece order: the counted waits are unchanged)
+    for (int it = 0; it < nst; ++it) {
+      const int ahead = min(NS - 2, nst - 1 - it);
+      wait_ahead<NS, PW>(ahead);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const bool more = it + NS - 1 < nst;
+      const RowSt r = rowal_state(it + NS - 1, (it + NS - 1) % NS);
+      compute_h(it % NS, [&](int i) {
+#pragma unroll
+        for (int q = i * (JA + JB) / RK; q < (i + 1) * (JA + JB) / RK; ++q)
+          if (more) rowal_piece(r, q);
+      });
+    }
+  } else {
+    for (int it = 0; it < nst; ++it) {
+      const int ahead = min(NS - 2, nst - 1 - it);   // younger stages allowed in flight
+      wait_ahead<NS, PW>(ahead);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (it + NS - 1 < nst) issue(it + NS - 1, (it + NS - 1) % NS);
+      compute_h(it % NS, [](int) {});
+    }
   }
 
   // D[k][co]: lane holds k = kb + 4*(lane>>4) + i for co = cb + (lane & 15)
@@ -3061,6 +3100,13 @@ int halo3_bn(const fv_conv_desc* d) {
   return d->cout % 128 == 0 ? 128 : d->cout % 64 == 0 ? 64 : 0;
 }
 
+// wgrad v2: next-stage DMA pieces spread between MFMA rows (FV_WG_IL=0 issues them as a
+// block after the barrier, for A/B)
+static int wg_interleave() {
+  static const int v = getenv("FV_WG_IL") ? atoi(getenv("FV_WG_IL")) : 1;
+  return v;
+}
+
 // v2 tile configs: id -> (co per block, pixels per block); waves/layout in launch_v2_ks
 struct V2Cfg { int bn, bm; };
 constexpr V2Cfg kV2Cfg[] = {
@@ -3979,6 +4025,7 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.fw = make_fastdiv((uint32_t)Win);
     a.fh = make_fastdiv((uint32_t)Hin);
     a.rowal = 1;
+    a.il = wg_interleave();
     a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
     const int nblk = 4 * t.ntk * t.ntc * t.nsplit;
@@ -4002,6 +4049,7 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.fw = make_fastdiv((uint32_t)d->w);
     a.fh = make_fastdiv((uint32_t)d->h);
     a.rowal = (d->w % t.px) == 0;
+    a.il = wg_interleave();
     a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
     const int nblk = t.ntk * t.ntc * t.nsplit;
