@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-syncbn", action="store_true", help="per-rank BN statistics (labelled)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="1: replay the step as one captured HIP graph (StepGraph), 0: eager launches; "
+                         "default: graph at one process, eager with collectives")
     return ap.parse_args()
 
 
@@ -166,22 +169,38 @@ def main():
     timer = ops.KernelTimer(is_res)
     ops.TIMER = timer
 
-    for _ in range(args.warmup):
-        step()
+    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
+    run = step
+    if use_graph:
+        # W eager warm-up steps, then one step captured into a HIP graph; two untimed replays
+        sg = fv.StepGraph(step, [opt], warmup=max(1, args.warmup)).capture()
+        run = sg.replay
+        for _ in range(2):
+            run()
+    else:
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.enabled = True
+    timer.enabled = not use_graph
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     t_host = time.perf_counter() - t0      # host time to issue K steps (launches are async)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
     timer.enabled = False
+    if use_graph:
+        # the roofline kernel's launch durations: HIP events around its launches over K eager
+        # steps right after the graph-timed region (ROCm refuses event nodes inside a capture)
+        timer.enabled = True
+        for _ in range(args.steps):
+            step()
+        timer.enabled = False
     if world > 1:
         tt = torch.tensor([t], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -195,7 +214,12 @@ def main():
     P = B * cfg.latent_hw * cfg.latent_hw
     f_launch = 2.0 * P * res_c * res_c * 9
     fam = {k: sum(v) / len(v) for k, v in ev.items() if v}
-    dom = max(fam, key=lambda k: fam[k] * len(ev[k])) if fam else None
+    # the roofline kernel: the res conv's forward launches.  conv3_halo_fwd3 (forward and data
+    # gradient, 27 launches) is the step's largest kernel by time; its forward launches run
+    # alone, while the data-gradient and weight-gradient launches share the CUs with each other
+    # and the BN passes (weight gradients on the side stream, ops.wgrad_stream_for), so their
+    # event-bracketed durations are co-scheduled times, reported in families_avg_ms only
+    dom = "fwd" if "fwd" in fam else (max(fam, key=lambda k: fam[k] * len(ev[k])) if fam else None)
     peak = {torch.bfloat16: PEAK_BF16_TFLOPS, torch.float32: PEAK_F32_TFLOPS,
             torch.float8_e4m3fn: PEAK_FP8_TFLOPS}[dtype]
     roof = None
@@ -204,7 +228,9 @@ def main():
         roof = {"bound": "mfma", "kernel": f"conv3x3 {res_c}->{res_c} {dom} @{cfg.latent_hw}x{cfg.latent_hw} B={B}",
                 "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "avg_ms": round(fam[dom], 4), "flop_per_launch": f_launch, "traffic": None,
-                "families_avg_ms": {k: round(v, 4) for k, v in fam.items()}}
+                "families_avg_ms": {k: round(v, 4) for k, v in fam.items()},
+                "timing": ("HIP events on the launch stream, K eager steps after the graph-timed region"
+                           if use_graph else "HIP events on the launch stream over the timed region")}
         roof.update(pmc_counters(cfg, B, dtype, dom, fam[dom]))
     from oracle.facevae_cpu import OracleConfig, flops_per_image
     _, f_img = flops_per_image(OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent,
@@ -220,6 +246,7 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "resolution": cfg.H,
                    "parallelism": f"dp{world}" + ("" if world == 1 else (" syncbn" if not args.no_syncbn else " local-bn"))},
         "host_issue_ms_per_step": round(t_host / args.steps * 1e3, 3),
+        "launch": "hip graph (one captured step replayed)" if use_graph else "eager",
         "mfma_util_step": round(step_util, 4),
         "step_flop_per_image": f_img,
         "roofline": roof,

@@ -167,6 +167,9 @@ _SIGS = {
     "fv_l1_bwd": (c_int, [P, P, c_long, P, P, P, P]),
     "fv_adam_step": (c_int, [P, P, c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                              c_long, P]),
+    "fv_adam_step_dev": (c_int, [P, P, c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                 P, P, P]),
+    "fv_copy_h2d_async": (c_int, [P, P, c_size_t, P]),
     "fv_comm_unique_id": (c_int, [P]),
     "fv_comm_init": (c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
     "fv_comm_allreduce": (c_int, [c_void_p, P, c_size_t, c_int, c_int, P]),
@@ -238,3 +241,52 @@ def dtype_code(dt: torch.dtype) -> int:
     if dt == torch.float64:
         return FV_F64
     raise TypeError(f"unsupported dtype {dt}")
+
+
+class _Staging:
+    """Host -> device copies of the descriptor tables the batched launches read (spectral-norm
+    layers, Adam tensors).  Eager: a fresh pinned buffer per copy, copied with torch's
+    non_blocking copy (torch's pinned allocator keeps it until the copy has run).  Under HIP-
+    graph capture (graph.StepGraph): persistent pinned buffers, one per copy in issue order,
+    reserved from the sizes recorded during the last eager step before the capture; the
+    captured memcpy nodes re-read them on every replay, so they live as long as the graph."""
+
+    def __init__(self):
+        self.mode = "eager"          # "eager" | "record" | "capture"
+        self.sizes = []
+        self.bufs = []
+        self.i = 0
+
+    def begin_record(self):
+        self.mode, self.sizes = "record", []
+
+    def begin_capture(self):
+        if self.mode != "record":
+            raise RuntimeError("staging: capture without a recorded eager step")
+        self.bufs = [torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True) for n in self.sizes]
+        self.mode, self.i = "capture", 0
+        return self.bufs
+
+    def end(self):
+        self.mode = "eager"
+
+
+staging = _Staging()
+
+
+def h2d_table(data: bytes, device):
+    """-> (device uint8 tensor holding `data`, host buffer to keep alive until consumed)."""
+    n = len(data)
+    if staging.mode == "capture":
+        if staging.i >= len(staging.bufs) or staging.bufs[staging.i].numel() < n:
+            raise RuntimeError("staging: the captured step issues other table copies than the recorded one")
+        hb = staging.bufs[staging.i]
+        staging.i += 1
+        hb[:n].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+        dev = torch.empty(n, dtype=torch.uint8, device=device)
+        call("fv_copy_h2d_async", dev.data_ptr(), hb.data_ptr(), n, stream())
+        return dev, hb
+    if staging.mode == "record":
+        staging.sizes.append(n)
+    hb = torch.frombuffer(bytearray(data), dtype=torch.uint8).pin_memory()
+    return hb.to(device, non_blocking=True), hb

@@ -1550,6 +1550,138 @@ conv7_n3_fwd(ConvArgs a, unsigned x_bytes) {
   }
 }
 
+// ----------------------------------------------------------------------------------------
+// conv7_n3_fwd2: the same "column taps in N" out_conv forward, sliding down a band of rows.
+// conv7_n3_fwd stages a 10-row halo for every 4 output rows (2.5x input re-read, 598 MB of
+// HBM per launch for a 268 MB input) and waits for it with one block per CU.  Here a block
+// owns (image, 64-column strip, band of C7B_BAND output rows) and keeps a ring of 14 input
+// rows in LDS (72 pixels x 128 B = 9 pieces of 1 KB per row, so a row is whole DMA pieces):
+// while the 8 waves compute output rows 4j..4j+3 from ring rows 4j-3..4j+6, the DMA of rows
+// 4j+7..4j+10 (the next group's) is in flight.  Input bytes per launch ~1.05x the tensor.
+// The weights sit in registers as MFMA B fragments (14 k-steps x 2 n-tiles, 112 VGPRs).
+// Per group: D[row][w'][n] (fp32, the 21 used columns) through LDS, then the 7-tap column
+// sums + bias (+ sigmoid, + BN records) as in conv7_n3_fwd.
+// ----------------------------------------------------------------------------------------
+constexpr int C7B_SLOTS = 14, C7B_ROWPX = 72, C7B_ROWB = C7B_ROWPX * 128;   // 9216 B
+constexpr int C7B_DLD = 22;                                                // D row stride (floats)
+__global__ void __launch_bounds__(512, 1)
+conv7_n3_fwd2(ConvArgs a, unsigned x_bytes, int band) {
+  constexpr int RING = C7B_SLOTS * C7B_ROWB;                // 129024
+  constexpr int DB = C7_TR * 70 * C7B_DLD * 4;               // 24640
+  __shared__ __attribute__((aligned(1024))) char smem[RING + DB];
+  float* Dl = reinterpret_cast<float*>(smem + RING);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_w = a.W / 64, bands = a.H / band;
+  const int blk = blockIdx.x;
+  const int n = blk / (bands * tiles_w);
+  const int rem = blk - n * bands * tiles_w;
+  const int hb = (rem / tiles_w) * band, w0 = (rem % tiles_w) * 64;
+  const int li = lane & 15, g = lane >> 4;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+
+  // ring row `rel` (input row hb - 3 + rel) -> slot rel % 14; 9 pieces per row
+  auto issue_rows = [&](int rel0, int nrows) {
+    for (int q = wave; q < nrows * 9; q += 8) {
+      const int rr = q / 9, pc = q - rr * 9;
+      const int rel = rel0 + rr;
+      const int hh = hb - 3 + rel;
+      const int L = pc * 64 + lane;                 // chunk within the row
+      const int px = L >> 3, ch = L & 7;
+      const int ww = w0 - 3 + px;
+      const bool ok = px < 70 && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+      const unsigned off = ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * 64 + ((ch ^ (px & 7)) << 3)) * 2)
+                              : 0x80000000u;
+      dma16(xr, smem + (rel % C7B_SLOTS) * C7B_ROWB + pc * 1024, off);
+    }
+  };
+  issue_rows(0, 10);
+
+  // weights wn [32][448] bf16 -> B fragments in registers
+  const bf16* __restrict__ wn = reinterpret_cast<const bf16*>(a.w);
+  bf16x8 bw[14][2];
+#pragma unroll
+  for (int ks = 0; ks < 14; ++ks)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) bw[ks][t] = *reinterpret_cast<const bf16x8*>(wn + (t * 16 + li) * 448 + (ks * 4 + g) * 8);
+
+  const int row = wave >> 1, half = wave & 1;
+  const int mb = half ? 2 : 0;
+  int apix[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) apix[t] = min((mb + t) * 16 + li, C7B_ROWPX - 1);
+  const int pm[5] = {half ? 2 : 0, half ? 3 : 0, half ? 3 : 1, half ? 4 : 1, half ? 4 : 2};
+  const int pn[5] = {half ? 1 : 0, half ? 0 : 1, half ? 1 : 0, half ? 0 : 1, half ? 1 : 0};
+  const int HWo = a.H * a.W;
+  const int ngroups = band / C7_TR;
+
+  for (int j = 0; j < ngroups; ++j) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                           // group j's rows landed; group j-1's D reads done
+    if (j + 1 < ngroups) issue_rows(4 * j + 10, 4);
+    f32x4 acc[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      const char* slot = smem + ((4 * j + row + r) % C7B_SLOTS) * C7B_ROWB;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int ks = r * 2 + kh, c = kh * 4 + g;
+        bf16x8 afr[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          afr[t] = *reinterpret_cast<const bf16x8*>(slot + (apix[t] * 8 + (c ^ (apix[t] & 7))) * 16);
+        if (half == 0) {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bw[ks][0], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bw[ks][1], acc[1], 0, 0, 0);
+          acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bw[ks][0], acc[2], 0, 0, 0);
+          acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bw[ks][1], acc[3], 0, 0, 0);
+          acc[4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bw[ks][0], acc[4], 0, 0, 0);
+        } else {
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bw[ks][1], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bw[ks][0], acc[1], 0, 0, 0);
+          acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bw[ks][1], acc[2], 0, 0, 0);
+          acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bw[ks][0], acc[3], 0, 0, 0);
+          acc[4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bw[ks][1], acc[4], 0, 0, 0);
+        }
+      }
+    }
+    // D[row][w'][n]: pixel w' = m*16 + 4g + i (MFMA row), column n = nt*16 + li; keep n < 21, w' < 70
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int nn = pn[i] * 16 + li;
+      if (nn < 21) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int wp = pm[i] * 16 + g * 4 + q;
+          if (wp < 70) Dl[(row * 70 + wp) * C7B_DLD + nn] = acc[i][q];
+        }
+      }
+    }
+    __syncthreads();
+    const int h0 = hb + 4 * j;
+    for (int o = tid; o < C7_TR * 64 * a.Cout; o += 512) {
+      const int co = o / (C7_TR * 64), rr = (o / 64) % C7_TR, w = o % 64;
+      float v = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+      for (int s7 = 0; s7 < 7; ++s7) v += Dl[(rr * 70 + w + s7) * C7B_DLD + co * 7 + s7];
+      if (a.stats) {
+        const float sv = wave_sum(v), qv = wave_sum(v * v);
+        const int rec = ((n * a.H + h0 + rr) * a.W + w0) >> 6;
+        if (lane == 0) {
+          a.stats[(long)(rec * 2) * a.Cout + co] = sv;
+          a.stats[(long)(rec * 2 + 1) * a.Cout + co] = qv;
+        }
+      }
+      if (a.sigmoid) v = 1.f / (1.f + expf(-v));
+      const int pix = (h0 + rr) * a.W + w0 + w;
+      if (a.nchw) reinterpret_cast<float*>(a.y)[((long)(n * a.Cout + co)) * HWo + pix] = v;
+      else reinterpret_cast<bf16*>(a.y)[((long)n * HWo + pix) * a.ldy + co] = (bf16)v;
+    }
+  }
+}
+
 // wn [32][448]: n = co * 7 + s (co < cout, s < 7), k = r * 64 + ci
 __global__ void weight_prep_c7n_kernel(const float* __restrict__ wp, const float* sigma, bf16* wn, int cout) {
   const float inv = sigma ? 1.f / sigma[0] : 1.f;
@@ -3244,6 +3376,26 @@ bool use_c7n(const fv_conv_desc* d) {
          (long)d->n * d->h * d->w * 64 * 2 < (1L << 31);
 }
 
+// band of output rows per block of the sliding out_conv forward (conv7_n3_fwd2): the largest
+// of 128/64/32/16/8/4 dividing H that still gives >= 256 blocks (else the smallest dividing);
+// 0 = the per-tile conv7_n3_fwd (FV_C7_V1=1 forces it, for A/B).  FV_C7_BAND=b forces a band
+// (tests: multi-group rings on small images); read per call.
+static const int g_c7_v1 = getenv("FV_C7_V1") && atoi(getenv("FV_C7_V1")) != 0;
+static int c7n_band(const fv_conv_desc* d) {
+  if (g_c7_v1) return 0;
+  if (const char* e = getenv("FV_C7_BAND")) {
+    const int b = atoi(e);
+    if (b >= 4 && b % 4 == 0 && d->h % b == 0) return b;
+  }
+  int pick = 0;
+  for (int band : {128, 64, 32, 16, 8, 4}) {
+    if (d->h % band) continue;
+    pick = band;
+    if ((long)d->n * (d->w / 64) * (d->h / band) >= 256) return band;
+  }
+  return pick;
+}
+
 // 3x3 weight gradient with the halo-staged input: conv3_halo_wgrad2 (sliding rows, default)
 // or conv3_halo_wgrad (FV_H3W_V1=1, for A/B)
 static const int g_h3w_v1 = getenv("FV_H3W_V1") && atoi(getenv("FV_H3W_V1")) != 0;
@@ -3742,8 +3894,13 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   int st;
   if (use_c7n(d)) {
     FV_REQUIRE(!res, "out_conv kernel: no residual");
-    const int nblk = d->n * (d->h / C7_TR) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
+    if (const int band = c7n_band(d)) {
+      const int nblk = d->n * (d->h / band) * (d->w / 64);
+      hipLaunchKernelGGL(conv7_n3_fwd2, dim3(nblk), dim3(512), 0, s, a, xb, band);
+      return fv_check_launch("conv2d_fwd_c7n2");
+    }
+    const int nblk = d->n * (d->h / C7_TR) * (d->w / 64);
     hipLaunchKernelGGL(conv7_n3_fwd, dim3(nblk), dim3(512), 0, s, a, xb);
     return fv_check_launch("conv2d_fwd_c7n");
   }

@@ -594,6 +594,37 @@ __global__ void adam_kernel(const fv_adam_tensor* __restrict__ ts, const int* __
   }
 }
 
+// device-step variant: one lane advances the step and writes the coefficients (fp64 math,
+// as fv_adam_step computes them on the host), then adam_dev_kernel reads them
+__global__ void adam_coef_kernel(double* step, float* coef, double lr, double beta1, double beta2) {
+  if (threadIdx.x != 0) return;
+  const double t = step[0] + 1.0;
+  step[0] = t;
+  const double bc1 = 1.0 - pow(beta1, t);
+  const double bc2 = 1.0 - pow(beta2, t);
+  coef[0] = (float)(lr / bc1);
+  coef[1] = (float)sqrt(bc2);
+}
+
+__global__ void adam_dev_kernel(const fv_adam_tensor* __restrict__ ts, const int* __restrict__ blocks, float omb1,
+                                float b2, float omb2, float eps, const float* __restrict__ coef) {
+  const float step_size = coef[0], bc2_sqrt = coef[1];
+  const int t = blocks[2 * blockIdx.x], ch = blocks[2 * blockIdx.x + 1];
+  const fv_adam_tensor d = ts[t];
+  const long base = (long)ch * FV_ADAM_CHUNK;
+  const long end = min(d.numel, base + FV_ADAM_CHUNK);
+  for (long i = base + threadIdx.x; i < end; i += NTH) {
+    const float g = d.grad[i];
+    float m = d.exp_avg[i], v = d.exp_avg_sq[i];
+    m = m + omb1 * (g - m);
+    v = v * b2 + omb2 * g * g;
+    d.exp_avg[i] = m;
+    d.exp_avg_sq[i] = v;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    d.param[i] = d.param[i] - step_size * (m / denom);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -909,6 +940,28 @@ int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, 
                      (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, (float)(lr / bc1),
                      (float)sqrt(bc2));
   return fv_check_launch("adam");
+}
+
+int fv_adam_step_dev(const fv_adam_tensor* tensors, const int* blocks, int nblocks, double lr, double beta1,
+                     double beta2, double eps, double* step_dev, float* coef_ws, void* stream) {
+  FV_REQUIRE(tensors && blocks && nblocks > 0 && step_dev && coef_ws, "adam_dev: bad args");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_coef_kernel, dim3(1), dim3(64), 0, s, step_dev, coef_ws, lr, beta1, beta2);
+  int st = fv_check_launch("adam_coef");
+  if (st) return st;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(nblocks), dim3(NTH), 0, s, tensors, blocks, (float)(1.0 - beta1),
+                     (float)beta2, (float)(1.0 - beta2), (float)eps, coef_ws);
+  return fv_check_launch("adam_dev");
+}
+
+int fv_copy_h2d_async(void* dst, const void* src_pinned, size_t bytes, void* stream) {
+  FV_REQUIRE(dst && src_pinned, "copy_h2d: bad args");
+  hipError_t e = hipMemcpyAsync(dst, src_pinned, bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    fv_set_error("copy_h2d: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return FV_OK;
 }
 
 }  // extern "C"

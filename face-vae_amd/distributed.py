@@ -30,6 +30,7 @@ averaging / SyncBN plumbing is testable on CPU with world_size 2.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import random
@@ -38,6 +39,8 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 import torch.distributed as dist
+
+from . import ops as _ops
 
 _COMM = None          # installed communicator (RcclComm / TorchComm)
 _SYNCBN = True
@@ -301,15 +304,22 @@ class DataParallel(torch.nn.Module):
 
     def _on_grad(self, p):
         bi, off = self._where[id(p)]
-        flat = self._flat_buf(bi, p.grad)
-        flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
-        if not self._armed:
-            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
-            self._armed = True
-        self._pending[bi] -= 1
-        if self._pending[bi] == 0:
-            self.launch_order.append(bi)
-            self.comm.allreduce_(self._flat[bi], op="avg", wait_back=False)
+        # conv weight gradients may come from the ops' side stream (ops.wgrad_stream_for): the
+        # bucket copy and the all-reduce launch are then issued there, after everything the
+        # compute stream has issued so far (BN / bias gradients), without stalling it
+        side = _ops.active_side_stream(p.grad.device) if p.grad.is_cuda else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(p.grad.device))
+        with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
+            flat = self._flat_buf(bi, p.grad)
+            flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
+            if not self._armed:
+                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+                self._armed = True
+            self._pending[bi] -= 1
+            if self._pending[bi] == 0:
+                self.launch_order.append(bi)
+                self.comm.allreduce_(self._flat[bi], op="avg", wait_back=False)
 
     def _finish(self):
         for bi, n in enumerate(self._pending):     # params that got no grad this step

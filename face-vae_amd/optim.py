@@ -34,13 +34,37 @@ class Adam(torch.optim.Optimizer):
             self._blocks[key] = t
         return t
 
+    # ------------------------------------------------------------------ HIP-graph replay
+    def prepare_graph(self):
+        """Before a graph capture (graph.StepGraph): the step count moves to the device (one fp64
+        counter per group, advanced by the captured launch, as torch.optim.Adam(capturable=True)),
+        and the group's host "step" tensors are shared so graph_step_done() is one fill."""
+        self._graph = {}
+        for gi, group in enumerate(self.param_groups):
+            ps = [p for p in group["params"] if len(self.state[p]) > 0]
+            if not ps:
+                continue
+            n = int(self.state[ps[0]]["step"].item())
+            host = torch.tensor(float(n))
+            for p in ps:
+                self.state[p]["step"] = host
+            dev = ps[0].device
+            self._graph[gi] = (torch.full((1,), float(n), dtype=torch.float64, device=dev),
+                               torch.empty(2, dtype=torch.float32, device=dev), host)
+
+    def graph_step_done(self):
+        """After a replay: the host step count follows the device counter (no sync)."""
+        for _, _, host in getattr(self, "_graph", {}).values():
+            host.add_(1.0)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             items = []
             for p in group["params"]:
@@ -50,6 +74,8 @@ class Adam(torch.optim.Optimizer):
                     raise RuntimeError("facevae_amd Adam: contiguous fp32 CUDA params only")
                 st = self.state[p]
                 if len(st) == 0:
+                    if capturing:
+                        raise RuntimeError("facevae_amd Adam: run an eager step before capturing a graph")
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
@@ -65,17 +91,26 @@ class Adam(torch.optim.Optimizer):
             if len(steps) != 1:
                 raise RuntimeError("facevae_amd Adam: params of a group must share the step count")
             step = steps.pop() + 1
-            for _, _, st in items:
-                st["step"].fill_(float(step))
             dev = items[0][0].device
             descs = (L.AdamTensor * len(items))()
             for i, (p, g, st) in enumerate(items):
                 descs[i] = L.AdamTensor(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
                                         st["exp_avg_sq"].data_ptr(), p.numel())
-            host = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8)
-            dtab = host.pin_memory().to(dev, non_blocking=True) if torch.cuda.is_available() else host
             blocks = self._block_table([p.numel() for p, _, _ in items], dev)
-            call("fv_adam_step", dtab.data_ptr(), blocks.data_ptr(), blocks.numel() // 2, float(group["lr"]),
-                 float(b1), float(b2), float(group["eps"]), step, stream())
+            dtab, host = L.h2d_table(bytes(descs), dev)
+            if capturing:
+                gs = getattr(self, "_graph", {}).get(gi)
+                if gs is None:
+                    raise RuntimeError("facevae_amd Adam: prepare_graph() before capturing")
+                call("fv_adam_step_dev", dtab.data_ptr(), blocks.data_ptr(), blocks.numel() // 2, float(group["lr"]),
+                     float(b1), float(b2), float(group["eps"]), gs[0].data_ptr(), gs[1].data_ptr(), stream())
+            else:
+                for _, _, st in items:
+                    st["step"].fill_(float(step))
+                gs = getattr(self, "_graph", {}).get(gi)
+                if gs is not None:          # an eager step after a capture keeps the device count in step
+                    gs[0].fill_(float(step))
+                call("fv_adam_step", dtab.data_ptr(), blocks.data_ptr(), blocks.numel() // 2, float(group["lr"]),
+                     float(b1), float(b2), float(group["eps"]), step, stream())
             self._keep = (dtab, host)   # keep the staging buffers alive until the launch is consumed
         return loss

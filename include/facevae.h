@@ -441,6 +441,18 @@ typedef struct fv_adam_tensor {
  * one per FV_ADAM_CHUNK elements of each tensor; `step` is the step count after increment. */
 int fv_adam_step(const fv_adam_tensor* tensors, const int* blocks, int nblocks, double lr,
                  double beta1, double beta2, double eps, long step, void* stream);
+/* The same update with the step count kept on the DEVICE (graph-replayable, as
+ * torch.optim.Adam(capturable=True)): one launch increments *step_dev (fp64) and writes the
+ * bias-correction coefficients (lr / (1 - beta1^t), sqrt(1 - beta2^t), computed in fp64 as
+ * the host path does) to coef_ws (2 floats), the update kernel reads them. */
+int fv_adam_step_dev(const fv_adam_tensor* tensors, const int* blocks, int nblocks, double lr,
+                     double beta1, double beta2, double eps, double* step_dev, float* coef_ws,
+                     void* stream);
+
+/* ------------------------------------------------------------------ staging ---- */
+/* stream-ordered host -> device copy of `bytes` from PINNED host memory (descriptor tables of
+ * the batched spectral norm / Adam launches); captured into a HIP graph as a memcpy node. */
+int fv_copy_h2d_async(void* dst, const void* src_pinned, size_t bytes, void* stream);
 
 /* ------------------------------------------------------------ communication ---- */
 typedef void* fv_comm_t;

@@ -60,6 +60,7 @@ CONV_CASES = [
     (7, 3, 64, 16, 64, False, False),
     (7, 64, 3, 8, 128, False, False),
     (7, 64, 3, 20, 64, False, False),   # out_conv wgrad: 3 ragged row segments
+    (7, 64, 3, 64, 128, False, False),  # out_conv forward: a 64-row band per block (ring wraps 4x), below
     # halo-staged 3x3 (bf16, W % 64 == 0, H % 4 == 0): co tiles of 128 / 256 / 64, 2 column tiles
     (3, 64, 128, 8, 64, False, False),
     (3, 256, 256, 4, 64, False, False),
@@ -78,8 +79,10 @@ CONV_CASES = [
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd(case, dtype):
+def test_conv_fwd(case, dtype, monkeypatch):
     k, cin, cout, H, W, ups, pro = case
+    if (k, cin, cout, H) == (7, 64, 3, 64):
+        monkeypatch.setenv("FV_C7_BAND", "64")     # conv7_n3_fwd2: 16 row groups per block
     g = gen(100 + k + cin)
     x = torch.randn(2, cin, H, W, generator=g)
     w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
