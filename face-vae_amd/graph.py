@@ -36,6 +36,7 @@ class StepGraph:
         self.warmup = warmup
         self.graph = None
         self.out = None
+        self.warm_out = None
         self._bufs = None
 
     def capture(self, before_capture: Callable = None):
@@ -51,7 +52,7 @@ class StepGraph:
             for i in range(self.warmup):
                 if i == self.warmup - 1:
                     L.staging.begin_record()
-                self.step_fn()
+                self.warm_out = self.step_fn()     # the last warm-up step's outputs (it trained)
         cur.wait_stream(side)
         torch.cuda.synchronize()
         for o in self.optimizers:

@@ -27,7 +27,7 @@ from .optim import Adam
 class FaceVAETrainer:
     def __init__(self, ckp_dir, vis_dir, dataloader, lr, checkpoint_freq=1, visualizer_params=None, zfill_num=8,
                  log_file_name="log_facevae.txt", cfg: Optional[_config.FaceVAEConfig] = None,
-                 compute_dtype: Optional[torch.dtype] = None, seed: Optional[int] = None):
+                 compute_dtype: Optional[torch.dtype] = None, seed: Optional[int] = None, graph: bool = False):
         self.cfg = cfg or _config.FaceVAEConfig(lr=lr)
         self.ckp_dir, self.vis_dir = ckp_dir, vis_dir
         self.dataloader = dataloader
@@ -61,9 +61,35 @@ class FaceVAETrainer:
         self.kl, self.recon = KLDivergenceLoss(), ReconLoss()
         self.weights = {"R": self.cfg.w_R, "K": self.cfg.w_K}
         self._eps_gen = None
+        # graph=True (single process): train_step replays one captured HIP graph per batch shape
+        # (graph.StepGraph); the batch is copied into static input buffers first.  A batch of
+        # another shape (e.g. the last, smaller one) runs eagerly.
+        self.graph = bool(graph) and self.ddp is None
+        self._sg = None
 
     # ---------------------------------------------------------------- one iteration
     def train_step(self, x: torch.Tensor, eps: torch.Tensor) -> Dict[str, torch.Tensor]:
+        if self.graph:
+            return self._graph_step(x, eps)
+        return self._eager_step(x, eps)
+
+    def _graph_step(self, x, eps):
+        from .graph import StepGraph
+        key = (tuple(x.shape), x.dtype, tuple(eps.shape))
+        if self._sg is None or self._sg[0] != key:
+            if self._sg is not None:
+                return self._eager_step(x, eps)          # one graph, for the first batch shape
+            xs, es = x.detach().clone(), eps.detach().clone()
+            sg = StepGraph(lambda: self._eager_step(xs, es), list(self.g_optimizers.values()), warmup=1)
+            sg.capture()                                  # the warm-up step trains on this batch
+            self._sg = (key, xs, es, sg)
+            return sg.warm_out
+        _, xs, es, sg = self._sg
+        xs.copy_(x)
+        es.copy_(eps)
+        return {k: v.clone() for k, v in sg.replay().items()}
+
+    def _eager_step(self, x: torch.Tensor, eps: torch.Tensor) -> Dict[str, torch.Tensor]:
         for opt in self.g_optimizers.values():
             opt.zero_grad(set_to_none=True)
         y, mu, logstd = self.net(x, eps)
@@ -135,3 +161,4 @@ class FaceVAETrainer:
         for k, o in self.g_optimizers.items():
             o.load_state_dict(ckp["optimizer_" + k])
         self.epoch = ckp["epoch"] + 1
+        self._sg = None            # new optimizer state tensors: the next graph step recaptures

@@ -136,3 +136,29 @@ def test_side_stream_wgrad_bit_identical(monkeypatch):
     assert torch.equal(out[0][0], out[1][0])
     for k in out[0][1]:
         assert torch.equal(out[0][1][k], out[1][1][k]), k
+
+
+def test_trainer_graph_mode_matches_eager():
+    """FaceVAETrainer(graph=True): the first batch captures, later batches replay; a batch of
+    another shape runs eagerly.  Same parameters and losses as the eager trainer."""
+    g = torch.load(os.path.join(GOLD, "toy_step.pt"), weights_only=True)
+    cfg = fv.FaceVAEConfig.toy()
+    res = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = fv.FaceVAETrainer(None, None, [], cfg.lr, cfg=cfg, compute_dtype=torch.float32, graph=graph)
+        tr.model.load_state_dict(g["init"])
+        gen = torch.Generator().manual_seed(7)
+        losses = []
+        for i in range(4):
+            B = 2 if i < 3 else 1
+            x = torch.rand(B, 3, 64, 64, generator=gen).cuda()
+            eps = torch.randn(B, cfg.latent, cfg.latent_hw, cfg.latent_hw, generator=gen).cuda()
+            out = tr.train_step(x, eps)
+            losses.append((out["R"].item(), out["K"].item()))
+        torch.cuda.synchronize()
+        res.append((losses, {k: p.detach().clone() for k, p in tr.model.named_parameters()}))
+    for (ra, ka), (rb, kb) in zip(res[0][0], res[1][0]):
+        assert abs(ra - rb) <= 1e-6 * abs(ra) and abs(ka - kb) <= 1e-6 * abs(ka)
+    for k in res[0][1]:
+        assert rel(res[1][1][k], res[0][1][k]) < 1e-6, k

@@ -24,8 +24,8 @@ import re
 # bench family -> (kernel-name pattern, total grid size in work-items) of the 256->256 res conv
 # at 64x64, B=32 (bench.py's dominant kernel)
 DOMS = {
-    "fwd": (re.compile(r"conv3_halo_fwd2<4, 2, 4, 8, 2>"), 512 * 512),
-    "dgrad": (re.compile(r"conv3_halo_fwd2<4, 2, 4, 8, 2>"), 512 * 512),
+    "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2>"), 512 * 512),
+    "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2>"), 512 * 512),
     "wgrad": (re.compile(r"conv_wgrad_v2<3, 256, 256, 2, 4, 64, 2, false, false>"), 252 * 512),
 }
 RES_FLOP = 2.0 * 32 * 64 * 64 * 256 * 256 * 9     # one res-conv launch, B=32 (154.6 GFLOP)
