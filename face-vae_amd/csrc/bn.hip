@@ -348,6 +348,112 @@ __global__ void act_bwd_reduce_kernel(const T* __restrict__ dout, const T* __res
   }
 }
 
+// Pooled layers (DownBlock2D: conv -> BN -> act -> AvgPool2d(2)): one thread per (2x2 quad,
+// 8-channel chunk), so the pooled output gradient is loaded once for its four pixels (the
+// per-pixel kernels above load it four times and divide every pixel index by W): 5 loads in
+// flight per iteration, not 8.  Quad q = (n*Ho + ho)*Wo + wo covers pixels (2ho + i, 2wo + j).
+template <typename T>
+__device__ __forceinline__ void quad_g(const T* dout, const T* y, int q, FastDiv fwo, int W, int C, int c,
+                                       const BnChunk& bp, float slope, float (&g)[4][8], float (&yh)[4][8],
+                                       int (&pix)[4]) {
+  const int hr = (int)fdiv((uint32_t)q, fwo);           // n*Ho + ho
+  const int wo = q - hr * (W >> 1);
+  pix[0] = (2 * hr) * W + 2 * wo;
+  pix[1] = pix[0] + 1;
+  pix[2] = pix[0] + W;
+  pix[3] = pix[2] + 1;
+  float d[8], v[4][8];
+  ld8<T>(dout + (size_t)q * C + c, d);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ld8<T>(y + (size_t)pix[t] * C + c, v[t]);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      yh[t][u] = (v[t][u] - bp.mean[u]) * bp.inv[u];
+      const float z = bp.gam[u] * yh[t][u] + bp.bet[u];
+      const float dq = 0.25f * d[u];
+      g[t][u] = z > 0.f ? dq : dq * slope;
+    }
+}
+
+template <typename T>
+__global__ void act_bwd_reduce_pool_kernel(const T* __restrict__ dout, const T* __restrict__ y, int Pq, FastDiv fwo,
+                                           int W, int C, const float* mean, const float* invstd,
+                                           const float* gamma, const float* beta, float slope, double* ws) {
+  const int tpp = C / 8;
+  const int rows = NTH / tpp;
+  const int cg = threadIdx.x % tpp, row = threadIdx.x / tpp;
+  BnChunk bp;
+  bp.load(mean, invstd, gamma, beta, cg * 8);
+  float s[8], q2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q2[j] = 0.f;
+  for (int q = blockIdx.x * rows + row; q < Pq; q += gridDim.x * rows) {
+    float g[4][8], yh[4][8];
+    int pix[4];
+    quad_g<T>(dout, y, q, fwo, W, C, cg * 8, bp, slope, g, yh, pix);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += (g[0][j] + g[1][j]) + (g[2][j] + g[3][j]);
+      q2[j] += (g[0][j] * yh[0][j] + g[1][j] * yh[1][j]) + (g[2][j] * yh[2][j] + g[3][j] * yh[3][j]);
+    }
+  }
+  __shared__ float ss[2][NTH * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ss[0][row * C + cg * 8 + j] = s[j];
+    ss[1][row * C + cg * 8 + j] = q2[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += NTH) {
+    double a = 0, b = 0;
+    for (int r = 0; r < rows; ++r) {
+      a += ss[0][r * C + c];
+      b += ss[1][r * C + c];
+    }
+    ws[((long)blockIdx.x * 2 + 0) * C + c] = a;
+    ws[((long)blockIdx.x * 2 + 1) * C + c] = b;
+  }
+}
+
+template <typename T>
+__global__ void act_bwd_apply_pool_kernel(const T* __restrict__ dout, const T* __restrict__ y, int Pq, FastDiv fwo,
+                                          int W, int C, int lgcpc, const float* mean, const float* invstd,
+                                          const float* gamma, const float* beta, float slope,
+                                          const float* __restrict__ k, const T* __restrict__ addend,
+                                          T* __restrict__ dx) {
+  const int total = Pq << lgcpc;
+  const int e0 = blockIdx.x * NTH + threadIdx.x;
+  const int c = (e0 & ((1 << lgcpc) - 1)) * 8;
+  BnChunk bp;
+  bp.load(mean, invstd, gamma, beta, c);
+  float k0[8], k1[8], gi[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    k0[u] = k[c + u];
+    k1[u] = k[C + c + u];
+    gi[u] = bp.gam[u] * bp.inv[u];
+  }
+  for (int e = e0; e < total; e += gridDim.x * NTH) {
+    const int q = e >> lgcpc;
+    float g[4][8], yh[4][8];
+    int pix[4];
+    quad_g<T>(dout, y, q, fwo, W, C, c, bp, slope, g, yh, pix);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float o[8], ad[8];
+      if (addend) ld8<T>(addend + (size_t)pix[t] * C + c, ad);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        o[u] = gi[u] * (g[t][u] - k0[u] - yh[t][u] * k1[u]);
+        if (addend) o[u] += ad[u];
+      }
+      st8<T>(dx + (size_t)pix[t] * C + c, o);
+    }
+  }
+}
+
 // cnt (optional): per-channel element count on the device (row 0 of the all-reduced [3][C]
 // statistics record: the global count even with uneven per-rank batches); k may be NULL
 // (dgamma / dbeta only)
@@ -447,6 +553,13 @@ __global__ void bwd_from_stats_kernel(const double* st, int C, double count, flo
     red[c] = sg;
     red[C + c] = sgy;
   }
+}
+
+// 2x2-quad kernels for the pooled BN backward (FV_POOL_QUADS=0 keeps the per-pixel ones, A/B);
+// the quads need even H and W, which AvgPool2d(2) over the layer already requires
+static int fv_pool_quads() {
+  static const int v = getenv("FV_POOL_QUADS") ? atoi(getenv("FV_POOL_QUADS")) : 1;
+  return v;
 }
 
 int grid_for(long work, int cap = 8192) {
@@ -607,12 +720,24 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
   const int nb = stream_blocks((long)n * h * w, c);
   const int P = n * h * w;
   const FastDiv fw = make_fastdiv((uint32_t)w);
-  if (dtype == FV_BF16)
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
-                       (const bf16*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
-  else
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
-                       (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+  if (pool && fv_pool_quads()) {
+    FV_REQUIRE(h % 2 == 0 && w % 2 == 0, "pooled bwd needs even h, w");
+    const int Pq = P / 4;
+    const FastDiv fwo = make_fastdiv((uint32_t)(w / 2));
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(act_bwd_reduce_pool_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
+                         (const bf16*)y, Pq, fwo, w, c, mean, invstd, gamma, beta, slope, (double*)ws);
+    else
+      hipLaunchKernelGGL(act_bwd_reduce_pool_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
+                         (const float*)y, Pq, fwo, w, c, mean, invstd, gamma, beta, slope, (double*)ws);
+  } else {
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
+                         (const bf16*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+    else
+      hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
+                         (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+  }
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
   hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, 2, c,
                      red);
@@ -632,12 +757,24 @@ int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, in
   const int nb = stream_blocks((long)n * h * w, c);
   const int P = n * h * w;
   const FastDiv fw = make_fastdiv((uint32_t)w);
-  if (dtype == FV_BF16)
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
-                       (const bf16*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
-  else
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
-                       (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+  if (pool && fv_pool_quads()) {
+    FV_REQUIRE(h % 2 == 0 && w % 2 == 0, "pooled bwd needs even h, w");
+    const int Pq = P / 4;
+    const FastDiv fwo = make_fastdiv((uint32_t)(w / 2));
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(act_bwd_reduce_pool_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
+                         (const bf16*)y, Pq, fwo, w, c, mean, invstd, gamma, beta, slope, (double*)ws);
+    else
+      hipLaunchKernelGGL(act_bwd_reduce_pool_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
+                         (const float*)y, Pq, fwo, w, c, mean, invstd, gamma, beta, slope, (double*)ws);
+  } else {
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(act_bwd_reduce_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout,
+                         (const bf16*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+    else
+      hipLaunchKernelGGL(act_bwd_reduce_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
+                         (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
+  }
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
   hipLaunchKernelGGL(bwd_sum_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, (const double*)ws, nb, c,
                      (double)count, dgamma, dbeta, k);
@@ -671,6 +808,21 @@ int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h
   const int P = n * h * w, lgcpc = fv_ilog2(c / 8);
   const FastDiv fw = make_fastdiv((uint32_t)w);
   hipStream_t s = (hipStream_t)stream;
+  if (pool && fv_pool_quads()) {
+    FV_REQUIRE(h % 2 == 0 && w % 2 == 0, "pooled bwd needs even h, w");
+    const int Pq = P / 4;
+    const FastDiv fwo = make_fastdiv((uint32_t)(w / 2));
+    const long qwork = (long)Pq * (c / 8);
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(act_bwd_apply_pool_kernel<bf16>, dim3(grid_for(qwork, 16384)), dim3(NTH), 0, s,
+                         (const bf16*)dout, (const bf16*)y, Pq, fwo, w, c, lgcpc, mean, invstd, gamma, beta, slope, k,
+                         (const bf16*)addend, (bf16*)dx);
+    else
+      hipLaunchKernelGGL(act_bwd_apply_pool_kernel<float>, dim3(grid_for(qwork, 16384)), dim3(NTH), 0, s,
+                         (const float*)dout, (const float*)y, Pq, fwo, w, c, lgcpc, mean, invstd, gamma, beta, slope,
+                         k, (const float*)addend, (float*)dx);
+    return fv_check_launch("bn_bwd_apply_pool");
+  }
   if (dtype == FV_BF16)
     hipLaunchKernelGGL(act_bwd_apply_kernel<bf16>, dim3(grid_for(work, 16384)), dim3(NTH), 0, s, (const bf16*)dout,
                        (const bf16*)y, P, fw, w, c, ldc, lgcpc, mean, invstd, gamma, beta, slope, pool, k,

@@ -376,3 +376,51 @@ def test_conv_transpose_elr_modulated_matches_reference(name, mode):
     assert rel(x.grad, g["dx"]) < tol and rel(w.grad, g["dw"]) < tol
     for kk, prm in m.named_parameters():
         assert rel(prm.grad, g["grads"][kk]) < tol * 3, kk
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 16, 32), (3, 128, 8, 8)])
+def test_bn_act_bwd_pooled(shape, dtype):
+    """DownBlock2D's BN backward (BN -> ReLU -> AvgPool2d(2)): the 2x2-quad reduce + apply
+    kernels against torch autograd of batch_norm(training) -> relu -> avg_pool2d on the same
+    (rounded) operands; dgamma, dbeta and dx."""
+    N, C, H, W = shape
+    g = gen(7 + C)
+    y = torch.randn(N, C, H, W, generator=g) * 2 + 0.3
+    gam = torch.rand(C, generator=g) + 0.5
+    bet = torch.randn(C, generator=g) * 0.2
+    dout = torch.randn(N, C, H // 2, W // 2, generator=g)
+    y = y.to(dtype).float()
+    dout = dout.to(dtype).float()
+    yr = y.double().requires_grad_(True)
+    gr, br = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    z = F.avg_pool2d(F.relu(F.batch_norm(yr, None, None, gr, br, training=True, eps=1e-5)), 2)
+    z.backward(dout.double())
+    mean = y.double().mean(dim=(0, 2, 3))
+    var = y.double().var(dim=(0, 2, 3), unbiased=False)
+    inv = (var + 1e-5).rsqrt()
+    yd = y.to(dtype).cuda().contiguous(memory_format=CL)
+    dd = dout.to(dtype).cuda().contiguous(memory_format=CL)
+    dev = lambda t: t.float().cuda().contiguous()
+    dg = torch.empty(C, device="cuda")
+    db = torch.empty(C, device="cuda")
+    k = torch.empty(2 * C, device="cuda")
+    ws = torch.empty(L.query("fv_bn_ws_bytes", C) // 8, dtype=torch.float64, device="cuda")
+    m_, i_, g_, b_ = dev(mean), dev(inv), dev(gam), dev(bet)
+    L.call("fv_bn_act_bwd_reduce_finalize", L.dtype_code(dtype), dd.data_ptr(), yd.data_ptr(), N, H, W, C, C,
+           m_.data_ptr(), i_.data_ptr(), g_.data_ptr(), b_.data_ptr(), 0.0, 1, N * H * W, dg.data_ptr(),
+           db.data_ptr(), k.data_ptr(), ws.data_ptr(), L.stream())
+    dx = torch.empty((N, C, H, W), dtype=dtype, device="cuda", memory_format=CL)
+    L.call("fv_bn_act_bwd_apply", L.dtype_code(dtype), dd.data_ptr(), yd.data_ptr(), N, H, W, C, C,
+           m_.data_ptr(), i_.data_ptr(), g_.data_ptr(), b_.data_ptr(), 0.0, 1, k.data_ptr(), None, dx.data_ptr(),
+           L.stream())
+    torch.cuda.synchronize()
+    tol = 1e-4 if dtype == torch.float32 else 1e-2
+    assert rel(dg, gr.grad) < tol and rel(db, br.grad) < tol
+    assert rel(dx.float(), yr.grad) < tol * 2
+    # the comm-path reduce (sums only, all-reduced elsewhere) gives the same sums
+    red = torch.empty(2 * C, dtype=torch.float64, device="cuda")
+    L.call("fv_bn_act_bwd_reduce", L.dtype_code(dtype), dd.data_ptr(), yd.data_ptr(), N, H, W, C, C, m_.data_ptr(),
+           i_.data_ptr(), g_.data_ptr(), b_.data_ptr(), 0.0, 1, red.data_ptr(), ws.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert rel(red[:C], br.grad) < tol and rel(red[C:], gr.grad) < tol
