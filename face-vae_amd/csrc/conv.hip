@@ -59,7 +59,6 @@ struct ConvArgs {
   float* sprec;
   const float *bnm, *bni, *bng, *bnb;
   float bns;
-  int il;         // conv3_halo_fwd3: next-stage weight DMA pieces spread over the MFMA rows
 };
 
 // output pixel of tile-space pixel p (identity unless a sub-pixel phase is set)
@@ -1064,30 +1063,6 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
       for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
     if (prio) __builtin_amdgcn_s_setprio(0);
   };
-  // weight DMA piece q (0 .. 2 JB - 1) of stage j: tap half q / JB, row piece q % JB
-  auto issue_b_piece = [&](int j, int buf, int q) {
-    const int h = q / JB, jb = q - (q / JB) * JB;
-    const int u = 2 * j + h;
-    if (u < ntap) {
-      const int c = u / 9, t = u - c * 9;
-      const unsigned Bs = sbase + 2 * HALO + buf * STG + h * BST;
-      const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
-      dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase[jb], k0 * 2);
-    }
-  };
-  // the second tap's MFMA rows with the next stage's pieces between them (a.il)
-  auto mfma_all_il = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM], bool more, int jn, int buf) {
-    if (prio) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < RN; ++i) {
-#pragma unroll
-      for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
-#pragma unroll
-      for (int q = i * (2 * JB) / RN; q < (i + 1) * (2 * JB) / RN; ++q)
-        if (more) issue_b_piece(jn, buf, q);
-    }
-    if (prio) __builtin_amdgcn_s_setprio(0);
-  };
 
   Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
   const int nh = (HQ - wave + NW - 1) / NW;   // halo pieces this wave issues
@@ -1134,15 +1109,12 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
       }
       pend = 0;
       if (j + NSB < nsteps) {
-        if (!(a.il && two)) issue_b(j + NSB, bj);
+        issue_b(j + NSB, bj);
         pend = bcnt(j + NSB);
       }
       load_frags(fa0, fb0, 2 * j + 2, bn1);
     }
-    if (two) {
-      if (a.il) mfma_all_il(fa1, fb1, j + 1 < nsteps && j + NSB < nsteps, j + NSB, bj);
-      else mfma_all(fa1, fb1);
-    }
+    if (two) mfma_all(fa1, fb1);
     bj = bn1;
   }
   __syncthreads();
@@ -1255,28 +1227,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
     __builtin_amdgcn_s_setprio(0);
   };
-  // one weight DMA piece q (0 .. 2 JB - 1) of stage j into buffer buf: tap half q / JB, row piece q % JB
-  auto issue_b_piece = [&](int j, int buf, int q) {
-    const int h = q / JB, jb = q - (q / JB) * JB;
-    const int u = 2 * j + h;
-    const int c = u / 9, t = u - c * 9;
-    const unsigned Bs = sbase + buf * STG + h * BST;
-    const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
-    dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, k0 * 2 + jb * wstep);
-  };
-  // MFMA rows with the next stage's pieces issued between them (conv_wgrad_v2's interleave)
-  auto mfma_all_il = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM], bool more, int jn, int buf) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < RN; ++i) {
-#pragma unroll
-      for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
-#pragma unroll
-      for (int q = i * (2 * JB) / RN; q < (i + 1) * (2 * JB) / RN; ++q)
-        if (more) issue_b_piece(jn, buf, q);
-    }
-    __builtin_amdgcn_s_setprio(0);
-  };
 
   // the ring and halo schedule of conv3_halo_fwd2 (nch even: no odd last tap)
   Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
@@ -1296,31 +1246,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   load_frags(fa0, fb0, 0, 0);
   int hn = 2, hstep = (9 * 2 - 10) / 2;
   int bj = 0;
-  if (a.il && NSB == 2) {
-    // the next stage's weight pieces go out between the second tap's MFMA rows (issued within
-    // the iteration, so the vmcnt(0) of the next barrier is unchanged)
-    for (int j = 0; j < nsteps; ++j) {
-      load_frags(fa1, fb1, 2 * j + 1, bj);
-      mfma_all(fa0, fb0);
-      const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
-      bool more = false;
-      if (j + 1 < nsteps) {
-        wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        if (hn < nch && j == hstep) {
-          issue_halo(hn);
-          ++hn;
-          hstep = (9 * hn - 10) / 2;
-        }
-        more = j + NSB < nsteps;
-        load_frags(fa0, fb0, 2 * j + 2, bn1);
-      }
-      mfma_all_il(fa1, fb1, more, j + NSB, bj);
-      bj = bn1;
-    }
-  } else {
   for (int j = 0; j < nsteps; ++j) {
     load_frags(fa1, fb1, 2 * j + 1, bj);
     mfma_all(fa0, fb0);
@@ -1346,7 +1271,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     }
     mfma_all(fa1, fb1);
     bj = bn1;
-  }
   }
   __syncthreads();
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
@@ -4170,9 +4094,6 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     const int pipe = pipe_env >= 0 ? pipe_env : 1;
     // linear-halo kernel (conv3_halo_fwd3); FV_H3_V3=0 falls back to fwd2 for A/B
     static const int v3 = getenv("FV_H3_V3") ? atoi(getenv("FV_H3_V3")) : 1;
-    // fwd3: weight DMA pieces interleaved with the MFMA rows (FV_H3_IL=0 issues them as a block)
-    static const int h3il = getenv("FV_H3_IL") ? atoi(getenv("FV_H3_IL")) : 1;
-    a.il = h3il;
     // (64-channel co tiles stay on fwd2: 448 -> 667 us for AFE.down1's data gradient)
     if (pipe && v3 && bn >= 128 && a.Cin % 64 == 0) {
       if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
@@ -4186,8 +4107,9 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
       if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else {
-      // (8-row tiles, conv3_halo_fwd2<1, 8, 4, 4, 3>, measured 418 -> 420 us for AFE.down1's
-      // data gradient in a convbench A/B: no gain, not kept)
+      // (measured and not kept: 8-row tiles, conv3_halo_fwd2<1, 8, 4, 4, 3>, AFE.down1's data
+      // gradient 418 -> 420 us; weight-DMA pieces spread between the MFMA rows as conv_wgrad_v2
+      // does, in fwd2 / fwd3: res conv forward 134 -> 160 us)
       if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4, 3>), dim3(nblk), dim3(256), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
     }
