@@ -2947,14 +2947,16 @@ conv_halo_wgrad(HaloWgArgs a) {
   constexpr int HB = HQ * 1024, DB = DQ * 1024, BUF = HB + DB;
   constexpr int KT = KS * KS * CIN;                 // valid k
   constexpr int MTT = (KT + 15) / 16;               // m-tiles (16 k rows)
-  constexpr int WPN = 8 / NT;                       // waves per n-tile
-  constexpr int RMW = (MTT + WPN - 1) / WPN;        // m-tiles per wave (max)
+  // every wave owns m-tiles {wave, wave + 8, ...} and ALL NT n-tiles: the A fragment of an
+  // m-tile (two transposed 8-B halo reads) feeds NT MFMAs.  (One n-tile per wave, as before,
+  // paid two LDS reads per MFMA: LDS-bound at 21 % MFMA busy on AFE.in_conv, NT = 4.)
+  constexpr int RMW = (MTT + 7) / 8;                // m-tiles per wave (max)
   constexpr int NKG = TR * TW / 32;                 // 32-pixel k-groups per tile
   __shared__ __attribute__((aligned(1024))) char smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nt = wave % NT, mw = wave / NT;
+  const int mw = wave;
   const int li = lane & 15, g = lane >> 4, q4 = li >> 2, pp = li & 3;
   const int tiles_w = a.W / TW, tiles_h = a.H / TR;
 
@@ -2994,7 +2996,7 @@ conv_halo_wgrad(HaloWgArgs a) {
   bool aok[RMW];
 #pragma unroll
   for (int j = 0; j < RMW; ++j) {
-    const int mt = mw + j * WPN;
+    const int mt = mw + j * 8;
     const int k = mt * 16 + 4 * pp;                 // first of this lane's 4 k (same tap, same chunk)
     const int tap = k / CIN, ci = k - (k / CIN) * CIN;
     const int r = tap / KS, s = tap - (tap / KS) * KS;
@@ -3002,11 +3004,15 @@ conv_halo_wgrad(HaloWgArgs a) {
     aoff[j] = k < KT ? r * HW + s : 0;              // k >= K rows: finite junk, never stored
     akx[j] = k < KT ? ci : 0;
   }
-  f32x4 acc[RMW];
+  f32x4 acc[RMW][NT];
 #pragma unroll
-  for (int j = 0; j < RMW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool do_bias = a.bslab && wave < NT;
+  for (int j = 0; j < RMW; ++j)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[j][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) accb[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bslab && wave == 7;        // a wave with the fewest m-tiles
   bf16x8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
@@ -3016,8 +3022,10 @@ conv_halo_wgrad(HaloWgArgs a) {
     const char* dys = halo + HB;
     FV_LDS char* hl = (FV_LDS char*)(halo);
     for (int kg = 0; kg < NKG; ++kg) {
-      // B: dy[32 px][16 co] of n-tile nt
-      const bf16x8 bfr = tfrag<LDD>(dys, kg * 32, nt * 16, lane);   // co >= LDD lanes: ignored
+      // B: dy[32 px][16 co] of every n-tile
+      bf16x8 bfr[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bfr[n] = tfrag<LDD>(dys, kg * 32, n * 16, lane);   // co >= LDD lanes: ignored
       // pixel rows 8g+q4 and 8g+4+q4 of this k-group -> halo pixel at tap (0,0)
       const int p0 = kg * 32 + 8 * g + q4, p1 = p0 + 4;
       const int hb0 = (p0 / TW) * HW + (p0 % TW), hb1 = (p1 / TW) * HW + (p1 % TW);
@@ -3034,9 +3042,13 @@ conv_halo_wgrad(HaloWgArgs a) {
           const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
           af = __builtin_bit_cast(bf16x8, v);
         }
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[j], 0, 0, 0);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[n], acc[j][n], 0, 0, 0);
       }
-      if (do_bias) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr, accb, 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[n], accb[n], 0, 0, 0);
+      }
     }
   };
 
@@ -3052,16 +3064,19 @@ conv_halo_wgrad(HaloWgArgs a) {
 
   // D[k][co]: lane holds k = mt*16 + 4*(lane>>4) + i for co = nt*16 + (lane & 15)
   float* slab = a.slab + (long)blockIdx.x * a.CW * a.KW;
-  const int co = nt * 16 + li;
-  if (co < a.cout) {
 #pragma unroll
-    for (int j = 0; j < RMW; ++j) {
-      const int mt = mw + j * WPN;
-      if (mt < MTT)
-        *reinterpret_cast<float4*>(slab + (long)co * a.KW + mt * 16 + g * 4) =
-            make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+  for (int n = 0; n < NT; ++n) {
+    const int co = n * 16 + li;
+    if (co < a.cout) {
+#pragma unroll
+      for (int j = 0; j < RMW; ++j) {
+        const int mt = mw + j * 8;
+        if (mt < MTT)
+          *reinterpret_cast<float4*>(slab + (long)co * a.KW + mt * 16 + g * 4) =
+              make_float4(acc[j][n][0], acc[j][n][1], acc[j][n][2], acc[j][n][3]);
+      }
+      if (do_bias && g == 0) a.bslab[(long)blockIdx.x * a.CW + co] = accb[n][0];
     }
-    if (do_bias && g == 0) a.bslab[(long)blockIdx.x * a.CW + co] = accb[0];
   }
 }
 
