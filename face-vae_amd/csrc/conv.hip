@@ -1429,113 +1429,6 @@ conv_halo_fwd(ConvArgs a, unsigned x_bytes) {
 }
 
 // ----------------------------------------------------------------------------------------
-// conv7_c8_band: the 7x7, 8-channel-input (3 padded to 8), 64-output-channel conv of
-// AFE.in_conv's forward and Generator.out_conv's data gradient, as a persistent band.
-// conv_halo_fwd<7, 8, 4, 4, ...> re-stages the 54 KB weight image (64 rows x 53 padded
-// chunks) by DMA for every 4x64-pixel tile (8192 tiles: 440 MB of L2 -> LDS traffic) and
-// waits for its halo before any MFMA.  Here a block owns (image, 64-column strip, band of
-// rows): the weights are staged once, the input rows (70 pixels x 16 B) live in a 14-slot
-// LDS ring, and the 4 rows the next group adds are loaded into registers while the 8 waves
-// compute the current 4 output rows, then written to the ring slots the current group does
-// not read (one barrier per group).  Same wave / tile / BN-record layout as
-// conv_halo_fwd (records keyed by the 4x64 tile index), same epilogue.  70 KB of LDS: two
-// blocks per CU.
-// ----------------------------------------------------------------------------------------
-constexpr int C8B_SLOTS = 14, C8B_ROWPX = 70;
-__global__ void __launch_bounds__(512, 2)
-conv7_c8_band(ConvArgs a, int band) {
-  constexpr int KS = 7, CIN = 8, RN = 4, TR = 4, TW = 64, RM = 2;
-  constexpr int KPAD = ((KS * KS * CIN + 31) / 32) * 32;          // 416
-  constexpr int NKS = KPAD / 32;                                  // 13
-  constexpr int WROW = KPAD / 8 + 1;                              // 53 chunks (padded row)
-  constexpr int WCH = RN * 16 * WROW, WQ = (WCH + 63) / 64;       // 3392 chunks, 53 pieces
-  constexpr int WB = WQ * 1024;
-  constexpr int RB = C8B_SLOTS * C8B_ROWPX * 16;                  // 15680
-  constexpr int GCH = TR * C8B_ROWPX;                             // 280 chunks per group
-  __shared__ __attribute__((aligned(1024))) char smem[WB + RB];
-  char* wlds = smem;
-  char* ring = smem + WB;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_w = a.W / TW, bands = a.H / band;
-  const int blk = blockIdx.x;
-  const int n = blk / (bands * tiles_w);
-  const int rem = blk - n * bands * tiles_w;
-  const int bi = rem / tiles_w, strip = rem - (rem / tiles_w) * tiles_w;
-  const int hb = bi * band, w0 = strip * TW;
-  const int li = lane & 15, g = lane >> 4;
-  const uint4* __restrict__ xg = reinterpret_cast<const uint4*>(a.x);
-
-  {
-    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
-    for (int q = wave; q < WQ; q += 8) {
-      const int L = q * 64 + lane;
-      const int row = L / WROW, ch = L - (L / WROW) * WROW;
-      const bool ok = L < WCH && ch < KPAD / 8;
-      const unsigned off = ok ? (unsigned)((row * a.Kpad + ch * 8) * 2) : 0x80000000u;
-      dma16(wr, wlds + q * 1024, off);
-    }
-  }
-  // ring row rel (input row hb - 3 + rel) -> slot rel % 14; chunk = one pixel (8 channels)
-  auto load_chunk = [&](int rel, int px) -> uint4 {
-    const int hh = hb - 3 + rel, ww = w0 - 3 + px;
-    if (hh < 0 || hh >= a.H || ww < 0 || ww >= a.W) return make_uint4(0, 0, 0, 0);
-    return xg[(long)(n * a.H + hh) * a.W + ww];
-  };
-  auto put_chunk = [&](int rel, int px, uint4 v) {
-    *reinterpret_cast<uint4*>(ring + ((rel % C8B_SLOTS) * C8B_ROWPX + px) * 16) = v;
-  };
-  for (int c = tid; c < 10 * C8B_ROWPX; c += 512) {
-    const int rr = c / C8B_ROWPX, px = c - rr * C8B_ROWPX;
-    put_chunk(rr, px, load_chunk(rr, px));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int rr = wave >> 1;                        // this wave's output row within a group
-  const int col0 = (wave & 1) * 32;                // its first column (2 m-tiles of 16)
-  const int ngroups = band / TR;
-  const int pre_px = tid % C8B_ROWPX, pre_r = tid / C8B_ROWPX;   // prefetch chunk (tid < 280)
-  for (int j = 0; j < ngroups; ++j) {
-    uint4 pre = make_uint4(0, 0, 0, 0);
-    const bool has_pre = j + 1 < ngroups && tid < GCH;
-    if (has_pre) pre = load_chunk(4 * j + 10 + pre_r, pre_px);
-    f32x4 acc[RN][RM];
-#pragma unroll
-    for (int i = 0; i < RN; ++i)
-#pragma unroll
-      for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int base = (4 * j + rr) % C8B_SLOTS;     // ring slot of tap row 0
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const int tap = ks * 4 + g;
-      const int r = tap / KS, s = tap - (tap / KS) * KS;
-      int slot = base + r;
-      slot = slot >= C8B_SLOTS ? slot - C8B_SLOTS : slot;
-      bf16x8 bfr[RN], afr[RM];
-#pragma unroll
-      for (int nn = 0; nn < RN; ++nn)
-        bfr[nn] = *reinterpret_cast<const bf16x8*>(wlds + ((nn * 16 + li) * WROW + ks * 4 + g) * 16);
-#pragma unroll
-      for (int m = 0; m < RM; ++m) {
-        bf16x8 v = *reinterpret_cast<const bf16x8*>(ring + (slot * C8B_ROWPX + col0 + m * 16 + li + s) * 16);
-        if (tap >= KS * KS) v = bf16x8{};
-        afr[m] = v;
-      }
-#pragma unroll
-      for (int nn = 0; nn < RN; ++nn)
-#pragma unroll
-        for (int m = 0; m < RM; ++m) acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nn], afr[m], acc[nn][m], 0, 0, 0);
-    }
-    const int h0 = hb + 4 * j;
-    const int tile = (n * (a.H / TR) + h0 / TR) * tiles_w + strip;
-    conv_epilogue<bf16, 1, 8, RN, RM>(a, acc, nullptr, 0, (n * a.H + h0) * a.W + w0, tile, 0, wave, lane, tid);
-    if (has_pre) put_chunk(4 * j + 10 + pre_r, pre_px, pre);   // slots of rows 4j-4..4j-1: unused by group j
-    __syncthreads();
-  }
-}
-
-// ----------------------------------------------------------------------------------------
 // 7x7 conv with a 64-channel input and <= 4 output channels (Generator.out_conv 64 -> 3,
 // models.py:1099 + sigmoid 1110), "column taps in N": for every input pixel w' of a row the
 // block computes D[h][w'][(co, s)] = sum_{r, ci} x[h + r - 3][w'][ci] * W[co][ci][r][s]
@@ -3518,30 +3411,6 @@ static int c7n_band(const fv_conv_desc* d) {
   return pick;
 }
 
-// band of output rows per block of conv7_c8_band (in_conv forward, out_conv data gradient):
-// the largest of 64/32/16/8/4 dividing H that still gives >= 512 blocks (two per CU), else
-// the smallest dividing; FV_C8_BAND=b forces a band.  OFF by default (FV_C8=1 enables it):
-// at 256x256, B=32 it measured slower than the per-tile conv_halo_fwd (in_conv forward 162
-// -> 175-207 us, out_conv data gradient 132 -> 145 us; step 13.30 -> 13.37 ms): the per-group
-// barrier serialises each group's scattered epilogue stores behind its MFMAs, where the
-// 8192-block grid overlapped them across blocks.
-static const int g_c8_on = getenv("FV_C8") && atoi(getenv("FV_C8")) != 0;
-static int c8_band(const fv_conv_desc* d) {
-  if (d->cin != 8 || d->cout != 64 || d->ksize != 7 || d->w % 64) return 0;
-  if (const char* e = getenv("FV_C8_BAND")) {
-    const int b = atoi(e);
-    if (b >= 4 && b % 4 == 0 && d->h % b == 0) return b;
-  }
-  if (!g_c8_on) return 0;
-  int pick = 0;
-  for (int band : {64, 32, 16, 8, 4}) {
-    if (d->h % band) continue;
-    pick = band;
-    if ((long)d->n * (d->w / 64) * (d->h / band) >= 512) return band;
-  }
-  return pick;
-}
-
 // 3x3 weight gradient with the halo-staged input: conv3_halo_wgrad2 (sliding rows, default)
 // or conv3_halo_wgrad (FV_H3W_V1=1, for A/B)
 static const int g_h3w_v1 = getenv("FV_H3W_V1") && atoi(getenv("FV_H3W_V1")) != 0;
@@ -3880,6 +3749,8 @@ static int halo_tr(const fv_conv_desc* d) {
   }
   if (g_disable_halo || d->dtype != FV_BF16 || d->ksize != 7 || d->pro_act || d->upsample || d->w % 64) return 0;
   int tr = 0;
+  // (8-row tiles for the 8-channel side, 16 MFMAs per 8 LDS reads per wave, measured 13.28 ->
+  // 13.33 ms/step in an A/B: not kept)
   if (d->cin == 8 && d->cout == 64) tr = 4;
   else if (d->cin == 64 && d->cout <= 16) tr = 2;
   if (!tr || d->h % tr) return 0;
@@ -4054,10 +3925,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.lgtw = 6;
     const int nblk = d->n * (d->h / tr) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
-    if (d->cin == 8 && c8_band(d)) {
-      const int band = c8_band(d);
-      hipLaunchKernelGGL(conv7_c8_band, dim3(d->n * (d->h / band) * (d->w / 64)), dim3(512), 0, s, a, band);
-    } else if (d->cin == 8)
+    if (d->cin == 8)
       hipLaunchKernelGGL((conv_halo_fwd<7, 8, 4, 4, true, false>), dim3(nblk), dim3(512), 0, s, a, xb);
     else
       hipLaunchKernelGGL((conv_halo_fwd<7, 64, 1, 2, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
