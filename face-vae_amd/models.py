@@ -102,7 +102,12 @@ class FaceVAE(_Block):
     def forward(self, x, eps):
         if x.is_cuda:
             self._sn_batch().run(self.training)   # all 15 power iterations in 4 launches
-        h = self.afe.forward_2d(x)
-        mu, logstd, z = ops.reparameterise(h, eps, self.compute_dtype())
-        y = self.generator.forward_2d(z)
+            ops.begin_forward(x.device)             # weight re-layouts may start from here (aux stream)
+        try:
+            h = self.afe.forward_2d(x)
+            mu, logstd, z = ops.reparameterise(h, eps, self.compute_dtype())
+            y = self.generator.forward_2d(z)
+        finally:
+            if x.is_cuda:
+                ops.end_forward(x.device)
         return y, mu, logstd

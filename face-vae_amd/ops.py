@@ -205,6 +205,36 @@ class SNBatch:
             c._sn_pre = (sigma[i:i + 1], snaps[i][0], snaps[i][1])
 
 
+# Auxiliary stream (FV_AUX_STREAM=1 / 2; off by default): the short kernels off the critical path
+# run on the side stream, as parallel branches of the step -- the weight re-layouts of every
+# conv (they depend only on the weights and the spectral-norm pass at the start of the forward:
+# begin_forward() records that point) and, in backward, the split-K slab reduction and the
+# spectral-norm term of each weight gradient (after the wgrad kernel, which stays in line).
+# The compute stream waits for a conv's prepared weights just before its launch, and for the
+# side stream at the end of backward.  Bit-identical (tests/test_graph_gpu.py), but slower in an
+# alternating on-box A/B of the graph-replayed 256x256, B=32 step: 13.00 ms/step in line, 13.71
+# with the weight preps on the aux stream, 13.44 with the post-processing too (the data
+# gradients overlapped by slab reductions stretch 128 -> 149 us; every conv's cross-stream wait
+# is a cross-queue dependency of the graph).
+_AUX_MODE = int(os.environ.get("FV_AUX_STREAM", "0"))   # 0 off, 1 weight preps, 2 + wgrad post-processing
+_AUX = _AUX_MODE >= 1
+_AUX_BWD = _AUX_MODE >= 2
+_FWD_EVENT = {}
+
+
+def begin_forward(dev):
+    """Mark the compute-stream point the weight preparations of this forward may start from
+    (after the model's spectral-norm pass); FaceVAE.forward calls it, end_forward() clears it."""
+    if _AUX and dev.type == "cuda":
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        _FWD_EVENT[dev.index] = ev
+
+
+def end_forward(dev):
+    _FWD_EVENT.pop(dev.index, None)
+
+
 class ConvState:
     """Per-forward state of one conv: descriptor, prepared weights, SN snapshot.  With fp8
     (and a descriptor the fp8 kernels support) the prepared weights are e4m3 with one
@@ -227,6 +257,7 @@ class ConvState:
                 self.sigma = spectral_norm_fwd(w, conv.weight_u, conv.weight_v, training)
                 self.u = conv.weight_u.clone()
                 self.v = conv.weight_v.clone()
+        self.ready = None
         self.fp8 = bool(fp8) and bool(query("fv_conv2d_fp8_supported", ctypes.byref(d)))
         if self.fp8:
             self.wk = _empty(query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), torch.uint8, device)
@@ -235,6 +266,26 @@ class ConvState:
             ws = _empty(query("fv_fp8_ws_bytes") // 4, F32, device)
             call("fv_conv_weight_prep_fp8", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
                  ptr(self.wdq), ptr(ws), stream())
+            return
+        self.ready = None
+        ev = _FWD_EVENT.get(device.index) if _AUX else None
+        if ev is not None:
+            # on the side stream from the start of the forward; the launch waits for `ready`
+            main = torch.cuda.current_stream(device)
+            side = _side_stream(device)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self.wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
+                self.wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if need_wt else None
+                call("fv_conv_weight_prep", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
+                     stream())
+                self.ready = torch.cuda.Event()
+                self.ready.record(side)
+            for t in (self.wk, self.wt):
+                if t is not None:
+                    t.record_stream(main)
+            if self.sigma is not None:
+                self.sigma.record_stream(side)
             return
         self.wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
         self.wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if need_wt else None
@@ -253,8 +304,16 @@ def stats_geometry(cs: ConvState):
     return query("fv_conv2d_stats_blocks", d), query("fv_conv2d_stats_block_pixels", d)
 
 
+def wait_weights(cs: ConvState):
+    """Compute stream waits for the conv's weight preparation (aux stream)."""
+    if cs.ready is not None:
+        torch.cuda.current_stream().wait_event(cs.ready)
+        cs.ready = None
+
+
 def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False):
     d = cs.d
+    wait_weights(cs)
     part = None
     if stats:
         nb, _ = stats_geometry(cs)
@@ -369,9 +428,20 @@ def _arm_join(main, side):
         _join_side()
 
 
+def aux_stream_for(cs: ConvState, dev):
+    """The aux stream for the weight-gradient post-processing of cs, or None (in line)."""
+    if not _AUX_BWD:
+        return None
+    b = cs.conv.bias
+    if cs.w.grad is not None or (b is not None and b.grad is not None):
+        return None
+    return _side_stream(dev)
+
+
 def active_side_stream(dev):
-    """The weight-gradient side stream of a device when side-stream wgrads are on, else None."""
-    return _side_stream(dev) if _WG_SIDE else None
+    """The side stream of a device when gradients may come from it (side-stream wgrads or the
+    aux stream), else None."""
+    return _side_stream(dev) if (_WG_SIDE or _AUX_BWD) else None
 
 
 def side_stream_join(device=None):
@@ -381,7 +451,7 @@ def side_stream_join(device=None):
         torch.cuda.current_stream(device).wait_stream(s)
 
 
-def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db):
+def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db, aux=None):
     d = cs.d
     dev = dy.device
     slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
@@ -389,6 +459,26 @@ def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db):
     psc, psh = (pro if pro is not None else (None, None))
     _timed("wgrad", d, lambda: call("fv_conv2d_bwd_weight", ctypes.byref(d), ptr(x), ptr(psc), ptr(psh), ptr(dy),
                                     ldd, ptr(slab), ptr(bslab), stream()))
+    if aux is not None:
+        # slab reduce + spectral-norm term on the aux stream, after the wgrad kernel
+        main = torch.cuda.current_stream(dev)
+        aux.wait_stream(main)
+        with torch.cuda.stream(aux):
+            dw, db = _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab)
+        for t in (slab, bslab, cs.sigma, getattr(cs, "u", None), getattr(cs, "v", None)):
+            if t is not None:
+                t.record_stream(aux)
+        for t in (dw, db):
+            if t is not None:
+                t.record_stream(main)
+        _arm_join(main, aux)
+        return dw, db
+    return _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab)
+
+
+def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab):
+    d = cs.d
+    dev = dy.device
     dw = torch.empty_like(cs.w)
     db = torch.empty(d.cout, dtype=F32, device=dev) if need_db else None
     call("fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(dw), ptr(db), stream())
@@ -423,7 +513,7 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
     dev = dy.device
     side = wgrad_stream_for(cs, dev)
     if side is None:
-        dw, db = _wgrad(cs, x, dy, ldd, pro, need_db)
+        dw, db = _wgrad(cs, x, dy, ldd, pro, need_db, aux=aux_stream_for(cs, dev))
     dx, recs = _dgrad(cs, dy, ldd, need_dx, bnred)
     if side is not None:
         # issued after the data gradient, so that kernel reaches the CUs first
@@ -732,6 +822,7 @@ class ResBlockFn(torch.autograd.Function):
             # them on)
             part = _empty(geo[0] * 2 * C, F32, x.device)
             sr = L.StoreReduce(1, ptr(part), None, None, None, None, None, 0.0)
+            wait_weights(cs2)
             _timed("fwd", d2, lambda: call("fv_conv2d_fwd_sr", ctypes.byref(d2), ptr(a2), ptr(cs2.wk), ptr(b2),
                                            ptr(xb), ptr(out), ctypes.byref(sr), stream()))
             if CHECK is not None:

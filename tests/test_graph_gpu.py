@@ -162,3 +162,29 @@ def test_trainer_graph_mode_matches_eager():
         assert abs(ra - rb) <= 1e-6 * abs(ra) and abs(ka - kb) <= 1e-6 * abs(ka)
     for k in res[0][1]:
         assert rel(res[1][1][k], res[0][1][k]) < 1e-6, k
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_aux_stream_bit_identical(monkeypatch, graph):
+    """Weight re-layouts and weight-gradient post-processing on the aux stream (ops._AUX) give
+    bit-identical steps, eager and graph-replayed."""
+    g = torch.load(os.path.join(GOLD, "toy_step.pt"), weights_only=True)
+    x, eps = g["x"].cuda(), g["eps"].cuda()
+    out = []
+    for aux in (False, True):
+        monkeypatch.setattr(ops, "_AUX", aux)
+        monkeypatch.setattr(ops, "_AUX_BWD", aux)
+        cfg, m, opt = _setup(torch.bfloat16, g["init"])
+        s = _step_fn(m, opt, x, eps, cfg)
+        if graph:
+            sg = fv.StepGraph(s, [opt], warmup=1).capture()
+            for _ in range(2):
+                y, R, K = sg.replay()
+        else:
+            for _ in range(3):
+                y, R, K = s()
+        torch.cuda.synchronize()
+        out.append((y.clone(), {k: p.detach().clone() for k, p in m.named_parameters()}))
+    assert torch.equal(out[0][0], out[1][0])
+    for k in out[0][1]:
+        assert torch.equal(out[0][1][k], out[1][1][k]), k
