@@ -3017,6 +3017,28 @@ __global__ void weight_prep2_kernel(const float* __restrict__ wp, const float* s
                       second ? blockIdx.x - j0.nb : blockIdx.x, j.nb);
 }
 
+// one launch for the generic weight layouts of many convs (fv_conv_weight_prep_multi): job j
+// owns blocks [blk0, blk0 + nb); at most 2 * FV_WPREP_MAX jobs, passed by value
+struct WPrepMJob {
+  const float* w;
+  const float* sigma;
+  void* out;
+  int rows, Kpad, lgCin, K, transposed, nb, cout, cin_valid, KS, blk0;
+};
+struct WPrepMulti {
+  int n;
+  WPrepMJob j[2 * FV_WPREP_MAX];
+};
+template <typename T>
+__global__ void weight_prep_multi_kernel(WPrepMulti m) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < m.n && b >= m.j[k + 1].blk0) ++k;
+  const WPrepMJob& j = m.j[k];
+  weight_prep_body<T>(j.w, j.sigma, (T*)j.out, j.rows, j.Kpad, j.cout, j.cin_valid, j.lgCin, j.KS, j.K, j.transposed,
+                      b - j.blk0, j.nb);
+}
+
 // sub-pixel phase weights of an upsample + 3x3 conv: for phase (pa, pb) the 2x2 tap (r', s')
 // sums the 3x3 taps that land on the same low-res input pixel (rows r in [lo, hi] with
 // lo = r' ? 1 + pa : 0, hi = r' ? 2 : pa; columns alike).  wk [4][rows][Kpad], k = (r'*2+s')*cin + ci.
@@ -3860,6 +3882,51 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     if ((st = fv_check_launch("weight_prep_t"))) return st;
   }
   return FV_OK;
+}
+
+int fv_conv_weight_prep_batchable(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  return !use_c7n(d) && !use_subpix(d) && !use_dgrad_lowres(d);
+}
+
+int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* const* w_params,
+                              const float* const* sigmas, void* const* wks, void* const* wts, void* stream) {
+  FV_REQUIRE(n >= 1 && n <= FV_WPREP_MAX && descs && w_params && sigmas && wks && wts, "weight_prep_multi: bad args");
+  WPrepMulti m{};
+  int nb_total = 0;
+  const int dtype = descs[0].dtype;
+  for (int i = 0; i < n; ++i) {
+    const fv_conv_desc* d = &descs[i];
+    int st = check_desc(d);
+    if (st) return st;
+    FV_REQUIRE(d->dtype == dtype, "weight_prep_multi: one dtype per call");
+    FV_REQUIRE(fv_conv_weight_prep_batchable(d), "weight_prep_multi: conv %d needs a special layout", i);
+    FV_REQUIRE(w_params[i] && wks[i], "weight_prep_multi: null pointer (conv %d)", i);
+    const int ks = d->ksize;
+    const FwdTile tk = fwd_tile(d->cout);
+    WPrepMJob j0{w_params[i], sigmas[i], wks[i], fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin),
+                 ks * ks * d->cin, 0, 0, d->cout, d->cin_valid, ks, 0};
+    j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 4096);
+    j0.blk0 = nb_total;
+    nb_total += j0.nb;
+    m.j[m.n++] = j0;
+    if (wts[i]) {
+      const FwdTile tt = fwd_tile(d->cin);
+      const int cin_t = pad_pow2_8(d->cout);
+      WPrepMJob j1{w_params[i], sigmas[i], wts[i], fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t),
+                   ks * ks * cin_t, 1, 0, d->cout, d->cin_valid, ks, 0};
+      j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 4096);
+      j1.blk0 = nb_total;
+      nb_total += j1.nb;
+      m.j[m.n++] = j1;
+    }
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(weight_prep_multi_kernel<bf16>, dim3(nb_total), dim3(256), 0, s, m);
+  else
+    hipLaunchKernelGGL(weight_prep_multi_kernel<float>, dim3(nb_total), dim3(256), 0, s, m);
+  return fv_check_launch("weight_prep_multi");
 }
 
 // store-pass record geometry (fv_store_reduce) of the launch `d` takes: records and pixels per

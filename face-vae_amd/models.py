@@ -99,9 +99,18 @@ class FaceVAE(_Block):
             object.__setattr__(self, "_snb", sb)
         return sb
 
+    def _wprep_batch(self):
+        wb = getattr(self, "_wpb", None)
+        if wb is None:
+            from .modules import _Conv
+            wb = ops.WPrepBatch([c for c in self.modules() if isinstance(c, _Conv)])
+            object.__setattr__(self, "_wpb", wb)
+        return wb
+
     def forward(self, x, eps):
         if x.is_cuda:
             self._sn_batch().run(self.training)   # all 15 power iterations in 4 launches
+            self._wprep_batch().run(x.device)       # the generic weight layouts in one launch
             ops.begin_forward(x.device)             # weight re-layouts may start from here (aux stream)
         try:
             h = self.afe.forward_2d(x)

@@ -235,6 +235,58 @@ def end_forward(dev):
     _FWD_EVENT.pop(dev.index, None)
 
 
+_WPREP_BATCH = os.environ.get("FV_WPREP_BATCH", "1") != "0"
+WPREP_MAX = 24
+
+
+class WPrepBatch:
+    """One launch (fv_conv_weight_prep_multi) for the weight re-layouts of every conv of a model
+    whose last forward used a generic layout, run right after the model's SNBatch (the 1/sigma
+    scales are its snapshots); each conv's ConvState then takes its prepared buffers instead of
+    launching fv_conv_weight_prep (17 launches of ~7.5 us per FaceVAE step).  A conv whose
+    descriptor changed since its last forward (other input shape) re-prepares itself."""
+
+    def __init__(self, convs):
+        self.convs = list(convs)
+
+    def run(self, device):
+        if not _WPREP_BATCH:
+            return
+        groups = {}
+        for c in self.convs:
+            key = getattr(c, "_fv_desc", None)
+            if key is None:
+                continue
+            d = L.ConvDesc.from_buffer_copy(key[0])
+            if not query("fv_conv_weight_prep_batchable", ctypes.byref(d)):
+                continue
+            sigma = None
+            if c.sn:
+                pre = getattr(c, "_sn_pre", None)
+                if pre is None:
+                    continue
+                sigma = pre[0]
+            groups.setdefault(d.dtype, []).append((c, d, key, sigma))
+        for dt, items in groups.items():
+            dtype = {L.FV_BF16: torch.bfloat16, L.FV_F32: torch.float32}[dt]
+            for i0 in range(0, len(items), WPREP_MAX):
+                chunk = items[i0:i0 + WPREP_MAX]
+                n = len(chunk)
+                descs = (L.ConvDesc * n)(*[d for _, d, _, _ in chunk])
+                wp, sg, wk, wt = ((ctypes.c_void_p * n)() for _ in range(4))
+                bufs = []
+                for i, (c, d, key, sigma) in enumerate(chunk):
+                    k = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
+                    t = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if key[1] else None
+                    w = c.weight_param()
+                    wp[i], sg[i], wk[i], wt[i] = w.data_ptr(), ptr(sigma), k.data_ptr(), ptr(t)
+                    bufs.append((c, key, k, t))
+                call("fv_conv_weight_prep_multi", n, ctypes.addressof(descs), ctypes.addressof(wp),
+                     ctypes.addressof(sg), ctypes.addressof(wk), ctypes.addressof(wt), stream())
+                for c, key, k, t in bufs:
+                    c._fv_prep = (key[0], k, t)
+
+
 class ConvState:
     """Per-forward state of one conv: descriptor, prepared weights, SN snapshot.  With fp8
     (and a descriptor the fp8 kernels support) the prepared weights are e4m3 with one
@@ -260,6 +312,7 @@ class ConvState:
         self.ready = None
         self.fp8 = bool(fp8) and bool(query("fv_conv2d_fp8_supported", ctypes.byref(d)))
         if self.fp8:
+            conv._fv_desc = conv._fv_prep = None
             self.wk = _empty(query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), torch.uint8, device)
             self.wt = _empty(query("fv_conv_fp8_wt_bytes", ctypes.byref(d)), torch.uint8, device) if need_wt else None
             self.wdq = _empty(1, F32, device)
@@ -267,7 +320,13 @@ class ConvState:
             call("fv_conv_weight_prep_fp8", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
                  ptr(self.wdq), ptr(ws), stream())
             return
-        self.ready = None
+        key = (bytes(d), bool(need_wt))
+        pre = getattr(conv, "_fv_prep", None)
+        conv._fv_prep = None
+        conv._fv_desc = key                # what the next forward's WPrepBatch prepares
+        if pre is not None and pre[0] == key[0] and (pre[2] is not None or not need_wt):
+            self.wk, self.wt = pre[1], (pre[2] if need_wt else None)
+            return
         ev = _FWD_EVENT.get(device.index) if _AUX else None
         if ev is not None:
             # on the side stream from the start of the forward; the launch waits for `ready`

@@ -85,6 +85,13 @@ int fv_conv2d_stats_block_pixels(const fv_conv_desc* d);
  * NULL), both scaled by 1/sigma[0] when sigma != NULL (spectral norm), dtype d->dtype. */
 int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma,
                         void* wk, void* wt, void* stream);
+/* The same for n convs in ONE launch (the generic layouts only: fv_conv_weight_prep_batchable(d)
+ * != 0; all descriptors of one dtype, n <= FV_WPREP_MAX): descs is an array of n descriptors,
+ * w_params / sigmas / wks / wts arrays of n pointers (sigma, wt entries may be NULL). */
+#define FV_WPREP_MAX 24
+int fv_conv_weight_prep_batchable(const fv_conv_desc* d);
+int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* const* w_params,
+                              const float* const* sigmas, void* const* wks, void* const* wts, void* stream);
 
 /* y = epi(conv(pro(x), wk) + bias [+ res]); stats (optional) receives per-record
  * (sum, sum of squares) of the pre-sigmoid output per channel. */
