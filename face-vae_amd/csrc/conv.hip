@@ -3029,14 +3029,14 @@ struct WPrepMulti {
   int n;
   WPrepMJob j[2 * FV_WPREP_MAX];
 };
+// grid (max nb, jobs): blockIdx.y selects the job directly (a per-block search over the job
+// list in kernel-argument memory cost more than the launches it replaced)
 template <typename T>
 __global__ void weight_prep_multi_kernel(WPrepMulti m) {
-  const int b = blockIdx.x;
-  int k = 0;
-  while (k + 1 < m.n && b >= m.j[k + 1].blk0) ++k;
-  const WPrepMJob& j = m.j[k];
+  const WPrepMJob& j = m.j[blockIdx.y];
+  if ((int)blockIdx.x >= j.nb) return;
   weight_prep_body<T>(j.w, j.sigma, (T*)j.out, j.rows, j.Kpad, j.cout, j.cin_valid, j.lgCin, j.KS, j.K, j.transposed,
-                      b - j.blk0, j.nb);
+                      blockIdx.x, j.nb);
 }
 
 // sub-pixel phase weights of an upsample + 3x3 conv: for phase (pa, pb) the 2x2 tap (r', s')
@@ -3906,26 +3906,24 @@ int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* con
     const FwdTile tk = fwd_tile(d->cout);
     WPrepMJob j0{w_params[i], sigmas[i], wks[i], fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin),
                  ks * ks * d->cin, 0, 0, d->cout, d->cin_valid, ks, 0};
-    j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 4096);
-    j0.blk0 = nb_total;
-    nb_total += j0.nb;
+    j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 256);
+    nb_total = std::max(nb_total, j0.nb);
     m.j[m.n++] = j0;
     if (wts[i]) {
       const FwdTile tt = fwd_tile(d->cin);
       const int cin_t = pad_pow2_8(d->cout);
       WPrepMJob j1{w_params[i], sigmas[i], wts[i], fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t),
                    ks * ks * cin_t, 1, 0, d->cout, d->cin_valid, ks, 0};
-      j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 4096);
-      j1.blk0 = nb_total;
-      nb_total += j1.nb;
+      j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 256);
+      nb_total = std::max(nb_total, j1.nb);
       m.j[m.n++] = j1;
     }
   }
   hipStream_t s = (hipStream_t)stream;
   if (dtype == FV_BF16)
-    hipLaunchKernelGGL(weight_prep_multi_kernel<bf16>, dim3(nb_total), dim3(256), 0, s, m);
+    hipLaunchKernelGGL(weight_prep_multi_kernel<bf16>, dim3(nb_total, m.n), dim3(256), 0, s, m);
   else
-    hipLaunchKernelGGL(weight_prep_multi_kernel<float>, dim3(nb_total), dim3(256), 0, s, m);
+    hipLaunchKernelGGL(weight_prep_multi_kernel<float>, dim3(nb_total, m.n), dim3(256), 0, s, m);
   return fv_check_launch("weight_prep_multi");
 }
 
