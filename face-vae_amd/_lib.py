@@ -171,6 +171,7 @@ _SIGS = {
                                  P, P, P]),
     "fv_copy_h2d_async": (c_int, [P, P, c_size_t, P]),
     "fv_conv_weight_prep_batchable": (c_int, [D]),
+    "fv_spectral_norm_bwd_multi": (c_int, [c_int, P, P, P]),
     "fv_conv_weight_prep_multi": (c_int, [c_int, P, P, P, P, P, P]),
     "fv_comm_unique_id": (c_int, [P]),
     "fv_comm_init": (c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
@@ -181,6 +182,11 @@ _SIGS = {
 }
 
 _lib = None
+
+
+class SnBwdLayer(ctypes.Structure):
+    _fields_ = [("w", c_void_p), ("g", c_void_p), ("u", c_void_p), ("v", c_void_p), ("sigma", c_void_p),
+                ("rows", c_int), ("cols", c_int)]
 
 
 class FaceVAELibError(RuntimeError):

@@ -9,6 +9,8 @@
 //   Adam    : torch.optim.Adam (logger.py:60)
 #include <math.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -452,6 +454,52 @@ __global__ void sn_bwd_apply_kernel(const float* __restrict__ g, int rows, int c
   }
 }
 
+// batched spectral-norm backward: grid (256, layers) partial dots, then grid (blocks, layers)
+// apply; per layer the same partial count and order as fv_spectral_norm_bwd (bit-identical)
+struct SnBwdMulti {
+  int n;
+  fv_sn_bwd_layer l[FV_SNB_MAX];
+};
+__global__ void sn_dot_multi_kernel(SnBwdMulti m, float* part) {
+  const fv_sn_bwd_layer& L = m.l[blockIdx.y];
+  const long n = (long)L.rows * L.cols;
+  const int nb = (int)min((n + NTH - 1) / NTH, 256L);
+  if ((int)blockIdx.x >= nb) return;
+  float acc = 0.f;
+  for (long i = blockIdx.x * (long)NTH + threadIdx.x; i < n; i += (long)nb * NTH) acc += L.g[i] * L.w[i];
+  acc = wave_sum(acc);
+  __shared__ float sh[NTH / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.y * 256 + blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void sn_bwd_apply_multi_kernel(SnBwdMulti m, const float* part) {
+  const fv_sn_bwd_layer& L = m.l[blockIdx.y];
+  const long n = (long)L.rows * L.cols;
+  const int nparts = (int)min((n + NTH - 1) / NTH, 256L);
+  const float* pp = part + blockIdx.y * 256;
+  __shared__ float red[NTH / 64];
+  __shared__ float dot_s;
+  float d = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += NTH) d += pp[i];
+  d = wave_sum(d);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < NTH / 64; ++i) t += red[i];
+    dot_s = t;
+  }
+  __syncthreads();
+  const float sg = L.sigma[0];
+  const float c1 = 1.f / sg, c2 = dot_s / (sg * sg);
+  for (long e = blockIdx.x * (long)NTH + threadIdx.x; e < n; e += (long)gridDim.x * NTH) {
+    const int i = (int)(e / L.cols), j = (int)(e - (long)i * L.cols);
+    L.g[e] = L.g[e] * c1 - c2 * L.u[i] * L.v[j];
+  }
+}
+
 // ---------------------------------------------------- batched spectral norm (all layers)
 // One power iteration + sigma for every spectral-normed conv of the model in 4 launches
 // (torch/nn/utils/spectral_norm.py:62-113 per layer): K1 partial W^T u over 64-row slices,
@@ -871,6 +919,25 @@ int fv_spectral_norm_bwd(const float* w, const float* g_sn, int rows, int cols, 
   hipLaunchKernelGGL(sn_bwd_apply_kernel, dim3(grid_for(n, 2048)), dim3(NTH), 0, s, g_sn, rows, cols, u, v, sigma,
                      part, nb, g_orig);
   return fv_check_launch("sn_bwd");
+}
+
+int fv_spectral_norm_bwd_multi(int n, const fv_sn_bwd_layer* layers, float* ws, void* stream) {
+  FV_REQUIRE(n >= 1 && n <= FV_SNB_MAX && layers && ws, "spectral norm bwd multi: bad args");
+  SnBwdMulti m{};
+  m.n = n;
+  long maxn = 0;
+  for (int i = 0; i < n; ++i) {
+    const fv_sn_bwd_layer& L = layers[i];
+    FV_REQUIRE(L.w && L.g && L.u && L.v && L.sigma && L.rows > 0 && L.cols > 0, "spectral norm bwd multi: layer %d", i);
+    m.l[i] = L;
+    maxn = std::max(maxn, (long)L.rows * L.cols);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sn_dot_multi_kernel, dim3(256, n), dim3(NTH), 0, s, m, ws);
+  int st = fv_check_launch("sn_dot_multi");
+  if (st) return st;
+  hipLaunchKernelGGL(sn_bwd_apply_multi_kernel, dim3(grid_for(maxn, 2048), n), dim3(NTH), 0, s, m, (const float*)ws);
+  return fv_check_launch("sn_bwd_multi");
 }
 
 size_t fv_spectral_norm_batch_ws_floats(const fv_sn_layer* layers, int nlayers) {

@@ -510,7 +510,7 @@ def side_stream_join(device=None):
         torch.cuda.current_stream(device).wait_stream(s)
 
 
-def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db, aux=None):
+def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db, aux=None, main=None):
     d = cs.d
     dev = dy.device
     slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
@@ -523,7 +523,7 @@ def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db, aux=None):
         main = torch.cuda.current_stream(dev)
         aux.wait_stream(main)
         with torch.cuda.stream(aux):
-            dw, db = _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab)
+            dw, db = _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab, main=main)
         for t in (slab, bslab, cs.sigma, getattr(cs, "u", None), getattr(cs, "v", None)):
             if t is not None:
                 t.record_stream(aux)
@@ -532,10 +532,10 @@ def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db, aux=None):
                 t.record_stream(main)
         _arm_join(main, aux)
         return dw, db
-    return _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab)
+    return _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab, main=main)
 
 
-def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab):
+def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab, main=None):
     d = cs.d
     dev = dy.device
     dw = torch.empty_like(cs.w)
@@ -543,9 +543,68 @@ def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab):
     call("fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(dw), ptr(db), stream())
     if CHECK is not None:
         CHECK("wgrad", cs, x=x, dy=dy, ldd=ldd, dw=dw, db=db, pro=pro)
-    if cs.conv.sn:
+    if cs.conv.sn and not (_sn_defer_ok(cs) and _sn_defer(cs, main)):
         spectral_norm_bwd(cs.w, dw, cs.u, cs.v, cs.sigma)
     return dw, db
+
+
+# Spectral-norm backward terms batched at the end of backward (FV_SN_BWD_BATCH, default on):
+# instead of two launches per SN conv (<g, w> partials, then the rank-1 update), one
+# fv_spectral_norm_bwd_multi pair for every SN conv of the backward pass, applied in place to
+# the parameters' .grad from an autograd final callback.  Only in a single process (data-parallel
+# hooks all-reduce each gradient as it is accumulated, so the term must be in it by then) and
+# only for parameters whose .grad was None (AccumulateGrad then holds exactly this gradient).
+_SN_BATCH = os.environ.get("FV_SN_BWD_BATCH", "1") != "0"
+_SN_DEFER = {"items": [], "armed": False, "stream": None}
+
+
+def _sn_defer_ok(cs: ConvState) -> bool:
+    if not _SN_BATCH or cs.w.grad is not None:
+        return False
+    if torch.distributed.is_available() and torch.distributed.is_initialized() \
+            and torch.distributed.get_world_size() > 1:
+        return False
+    return True
+
+
+def _sn_flush():
+    items, st = _SN_DEFER["items"], _SN_DEFER["stream"]
+    _SN_DEFER.update(items=[], armed=False, stream=None)
+    layers = [(w, u, v, sig) for w, u, v, sig in items if w.grad is not None]
+    if not layers:
+        return
+    with torch.cuda.stream(st):
+        for side in _SIDE.values():       # gradients finished on a side stream (aux / wgrad options)
+            st.wait_stream(side)
+        for i0 in range(0, len(layers), 24):
+            chunk = layers[i0:i0 + 24]
+            arr = (L.SnBwdLayer * len(chunk))()
+            for i, (w, u, v, sig) in enumerate(chunk):
+                g = w.grad
+                if g.dtype != F32 or not g.is_contiguous():
+                    raise RuntimeError("spectral-norm backward: fp32 contiguous gradient expected")
+                arr[i] = L.SnBwdLayer(w.data_ptr(), g.data_ptr(), u.data_ptr(), v.data_ptr(), sig.data_ptr(),
+                                      w.shape[0], w.numel() // w.shape[0])
+            ws = _empty(256 * len(chunk), F32, chunk[0][0].device)
+            call("fv_spectral_norm_bwd_multi", len(chunk), ctypes.addressof(arr), ptr(ws), stream())
+
+
+def _sn_defer(cs: ConvState, main=None) -> bool:
+    """Queue cs's spectral-norm term for the end of this backward pass (applied on the compute
+    stream `main`, default the current one); False (caller applies it now) outside a backward
+    pass."""
+    if any(w is cs.w for w, _, _, _ in _SN_DEFER["items"]):
+        raise RuntimeError("spectral-norm backward batching: a conv used twice in one backward pass "
+                           "(set FV_SN_BWD_BATCH=0)")
+    if not _SN_DEFER["armed"]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_sn_flush)
+        except RuntimeError:         # not inside a backward pass
+            return False
+        _SN_DEFER["armed"] = True
+        _SN_DEFER["stream"] = main if main is not None else torch.cuda.current_stream(cs.w.device)
+    _SN_DEFER["items"].append((cs.w, cs.u, cs.v, cs.sigma))
+    return True
 
 
 def _wgrad_side(side, cs: ConvState, x, dy, ldd, pro, need_db):
@@ -554,7 +613,7 @@ def _wgrad_side(side, cs: ConvState, x, dy, ldd, pro, need_db):
     main = torch.cuda.current_stream(dy.device)
     side.wait_stream(main)
     with torch.cuda.stream(side):
-        dw, db = _wgrad(cs, x, dy, ldd, pro, need_db)
+        dw, db = _wgrad(cs, x, dy, ldd, pro, need_db, main=main)
     for t in (x, dy, cs.sigma, getattr(cs, "u", None), getattr(cs, "v", None)) + tuple(pro or ()):
         if t is not None:
             t.record_stream(side)

@@ -456,6 +456,20 @@ int fv_adam_step_dev(const fv_adam_tensor* tensors, const int* blocks, int nbloc
                      double beta1, double beta2, double eps, double* step_dev, float* coef_ws,
                      void* stream);
 
+/* ------------------------------------------------- batched spectral-norm backward ---- */
+/* g <- g / sigma - (<g, w> / sigma^2) u v^T in place for n layers in two launches (the
+ * per-layer fv_spectral_norm_bwd is two launches each); ws >= 256 * n floats. */
+#define FV_SNB_MAX 24
+typedef struct fv_sn_bwd_layer {
+  const float* w;
+  float* g;
+  const float* u;
+  const float* v;
+  const float* sigma;
+  int rows, cols;
+} fv_sn_bwd_layer;
+int fv_spectral_norm_bwd_multi(int n, const fv_sn_bwd_layer* layers, float* ws, void* stream);
+
 /* ------------------------------------------------------------------ staging ---- */
 /* stream-ordered host -> device copy of `bytes` from PINNED host memory (descriptor tables of
  * the batched spectral norm / Adam launches); captured into a HIP graph as a memcpy node. */

@@ -188,3 +188,21 @@ def test_aux_stream_bit_identical(monkeypatch, graph):
     assert torch.equal(out[0][0], out[1][0])
     for k in out[0][1]:
         assert torch.equal(out[0][1][k], out[1][1][k]), k
+
+
+def test_sn_bwd_batch_bit_identical(monkeypatch):
+    """Spectral-norm backward terms batched at the end of backward (ops._SN_BATCH) against the
+    per-conv launches: the same partial sums in the same order, bit-identical parameters."""
+    g = torch.load(os.path.join(GOLD, "toy_step.pt"), weights_only=True)
+    x, eps = g["x"].cuda(), g["eps"].cuda()
+    out = []
+    for batch in (False, True):
+        monkeypatch.setattr(ops, "_SN_BATCH", batch)
+        cfg, m, opt = _setup(torch.float32, g["init"])
+        s = _step_fn(m, opt, x, eps, cfg)
+        for _ in range(2):
+            s()
+        torch.cuda.synchronize()
+        out.append({k: p.detach().clone() for k, p in m.named_parameters()})
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
