@@ -53,7 +53,7 @@ def main(proc, args):
     trainloader = data.DataLoader(trainset, batch_size=args.batch_size, num_workers=args.num_workers,
                                   pin_memory=True, sampler=trainsampler)
     logger = fv.FaceVAETrainer(args.ckp_dir, args.vis_dir, trainloader, args.lr, log_file_name=args.log_file,
-                               cfg=cfg)
+                               cfg=cfg, graph=args.graph and world_size == 1)
     if args.ckp > 0:
         logger.load_cpk(args.ckp)
     for _ in range(args.num_epochs):
@@ -89,6 +89,8 @@ def parse(argv=None):
     parser.add_argument("--synthetic", type=int, default=0, help="N synthetic frames instead of root_dir")
     parser.add_argument("--config", default="256", choices=["toy", "256", "512"])
     parser.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    parser.add_argument("--graph", type=str2bool, default=False,
+                        help="single GPU: replay each step as one captured HIP graph (FaceVAETrainer(graph=True))")
     parser.add_argument("--dump_dir", type=str, default="")
     parser.add_argument("--init", default="ours", choices=["ours", "torch"],
                         help="rendezvous: our init_dist, or a bare torch process group (reference style)")
