@@ -2980,10 +2980,12 @@ template <typename T>
 __device__ __forceinline__ void weight_prep_body(const float* __restrict__ wp, const float* sigma, T* wk, int rows,
                                                  int Kpad, int cout, int cin_valid, int lgCin, int KS, int K,
                                                  int transposed, int bid, int nblk) {
-  const long total = (long)rows * Kpad;
+  // 32-bit index math (a weight image is < 2^31 elements; the 64-bit divisions per element
+  // dominated the batched launch)
+  const int total = rows * Kpad;
   const float inv = sigma ? 1.f / sigma[0] : 1.f;
-  for (long e = bid * (long)blockDim.x + threadIdx.x; e < total; e += (long)nblk * blockDim.x) {
-    const int row = (int)(e / Kpad), k = (int)(e - (long)row * Kpad);
+  for (int e = bid * (int)blockDim.x + threadIdx.x; e < total; e += nblk * (int)blockDim.x) {
+    const int row = e / Kpad, k = e - row * Kpad;
     float v = 0.f;
     if (k < K) {
       const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
