@@ -555,12 +555,6 @@ __global__ void bwd_from_stats_kernel(const double* st, int C, double count, flo
   }
 }
 
-// 2x2-quad kernels for the pooled BN backward (FV_POOL_QUADS=0 keeps the per-pixel ones, A/B);
-// the quads need even H and W, which AvgPool2d(2) over the layer already requires
-static int fv_pool_quads() {
-  static const int v = getenv("FV_POOL_QUADS") ? atoi(getenv("FV_POOL_QUADS")) : 1;
-  return v;
-}
 
 int grid_for(long work, int cap = 8192) {
   long g = (work + NTH - 1) / NTH;
@@ -720,7 +714,7 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
   const int nb = stream_blocks((long)n * h * w, c);
   const int P = n * h * w;
   const FastDiv fw = make_fastdiv((uint32_t)w);
-  if (pool && fv_pool_quads()) {
+  if (pool) {   // 2x2-quad kernels (even H, W: AvgPool2d(2) requires them)
     FV_REQUIRE(h % 2 == 0 && w % 2 == 0, "pooled bwd needs even h, w");
     const int Pq = P / 4;
     const FastDiv fwo = make_fastdiv((uint32_t)(w / 2));
@@ -757,7 +751,7 @@ int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, in
   const int nb = stream_blocks((long)n * h * w, c);
   const int P = n * h * w;
   const FastDiv fw = make_fastdiv((uint32_t)w);
-  if (pool && fv_pool_quads()) {
+  if (pool) {   // 2x2-quad kernels (even H, W: AvgPool2d(2) requires them)
     FV_REQUIRE(h % 2 == 0 && w % 2 == 0, "pooled bwd needs even h, w");
     const int Pq = P / 4;
     const FastDiv fwo = make_fastdiv((uint32_t)(w / 2));
@@ -808,7 +802,7 @@ int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h
   const int P = n * h * w, lgcpc = fv_ilog2(c / 8);
   const FastDiv fw = make_fastdiv((uint32_t)w);
   hipStream_t s = (hipStream_t)stream;
-  if (pool && fv_pool_quads()) {
+  if (pool) {   // 2x2-quad kernels (even H, W: AvgPool2d(2) requires them)
     FV_REQUIRE(h % 2 == 0 && w % 2 == 0, "pooled bwd needs even h, w");
     const int Pq = P / 4;
     const FastDiv fwo = make_fastdiv((uint32_t)(w / 2));

@@ -39,8 +39,6 @@ struct ConvArgs {
   int K, Kpad, nks;
   int sigmoid, nchw;
   int ntn;
-  int dbg;       // experiment knob (FV_CONV_DBG): bit0 skip MFMA (ref loop), bit1 skip DMA after
-                 // the prologue, bit2 skip epilogue, bit3 v2 fwd: reference (unpipelined) k loop
   int lgtw;       // > 0: a block's pixels are a (BM >> lgtw) x (1 << lgtw) rectangle at p0
   // sub-pixel phase of an upsample-conv (v2 MODE 2): the tile space is the LOW-res image
   // (H x W = Hin x Win, powers of two: lgw, lghw) and tile pixel (n, h, w) of phase
@@ -203,7 +201,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     }
   }
 
-  if (a.stats && !(a.dbg & 128)) {   // (bit 7: experiment, no statistics)
+  if (a.stats) {
     // BN statistics partials, one record per wave row (RM*16 pixels, record index
     // tm*WM + wm): per output channel (sum, sum of squares) over the record's valid pixels,
     // reduced over the 16 pixel lanes of each m-tile by shuffles -- no LDS, no barrier.
@@ -236,7 +234,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
 
   if constexpr (STAGED) {
     static_assert(sizeof(T) == 2, "staged epilogue is bf16 NHWC");
-    if (a.dbg & 512) return;                            // (bit 9: experiment, stop after the stats)
     constexpr int CPR = BN / 8;                         // 16-B chunks per pixel row
     __syncthreads();                                    // stats scratch / last k-step reads done
 #pragma unroll
@@ -260,7 +257,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
         const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
         const int tp = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
         const int co = co0 + ch * 8;
-        if (tp >= a.P || co >= a.Cout || (a.dbg & 256)) continue;   // (bit 8: experiment, no stores)
+        if (tp >= a.P || co >= a.Cout) continue;
         const int pix = out_pix(a, tp);
         Chunk8<bf16> v;
         v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
@@ -301,7 +298,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
       const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
       const int tp = a.lgtw ? p0 + (pl >> a.lgtw) * a.W + (pl & ((1 << a.lgtw) - 1)) : p0 + pl;
       const int co = co0 + ch * 8;
-      if (tp >= a.P || co >= a.Cout || (a.dbg & 256)) continue;
+      if (tp >= a.P || co >= a.Cout) continue;
       const int pix = out_pix(a, tp);
       Chunk8<bf16> v;
       v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
@@ -670,7 +667,6 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
     wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ swzk<BKS>(row)) << 3)) * 2);
   }
 
-  constexpr int PW = JA + JB;      // DMA pieces this wave issues per stage (upper bound)
   auto issue = [&](int ks, int buf) {
     const int k0 = ks * BKS;
     const unsigned As = sbase + buf * STAGE;
@@ -823,138 +819,6 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
   }
 }
 
-// SUBP: one sub-pixel phase of an upsample + 3x3 conv (conv_fwd_v2 MODE 2's algebra): tile
-// space = the low-res input, block phase = lid & 3 (the 4 phases of a tile are neighbours),
-// 4 taps (r', s') per chunk at input offsets (r' + pa - 1, s' + pb - 1), phase-folded weights
-// [4][rows][4 cin]; the halo is the same (TR + 2) x 66 window.
-template <int WN, int WM, int RN, int RM, bool SUBP = false>
-__global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
-conv3_halo_fwd(ConvArgs a, unsigned x_bytes) {
-  constexpr int NT = SUBP ? 4 : 9;                  // taps per 32-channel chunk
-  constexpr int NW = WN * WM;
-  constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
-  constexpr int HP = (TR + 2) * 66, HQ = (HP + 15) / 16, JH = (HQ + NW - 1) / NW;
-  constexpr int HALO = HQ * 1024;
-  constexpr int QB = BN / 16, JB = QB / NW;
-  static_assert(QB % NW == 0, "weight pieces per wave");
-  constexpr int BST = BN * 64;
-  constexpr int MAIN = 2 * HALO + 2 * BST, EPI = BM * BN * 2;
-  __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % WN, wm = wave / WN;
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  const int lid0 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int phase = SUBP ? (lid0 & 3) : 0;
-  const int lid = SUBP ? (lid0 >> 2) : lid0;
-  if constexpr (SUBP) a.sub = 1 + phase;
-  const int pa = phase >> 1, pb = phase & 1;
-  const int tn = lid % a.ntn, tm = lid / a.ntn;
-  const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
-  const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
-  const int co0 = tn * BN;
-  const int p0 = (n * a.H + th * TR) * a.W + tw * 64;
-
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
-  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
-  const int lrow = lane >> 2, lchk = lane & 3;
-  const unsigned wph = SUBP ? (unsigned)(phase * a.wphase) : 0u;   // this phase's weight block
-
-  // halo pieces of this wave: source offsets (0x80000000: outside the image -> zero fill)
-  unsigned hoff[JH];
-#pragma unroll
-  for (int j = 0; j < JH; ++j) {
-    const int hp = (wave + j * NW) * 16 + lrow;
-    const int hr = hp / 66, hc = hp - (hp / 66) * 66;
-    const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
-    const bool ok = hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-    hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + ((lchk ^ h3swz(hp)) << 3)) * 2) : 0x80000000u;
-  }
-  const int nh = (HQ - wave + NW - 1) / NW;        // halo pieces this wave issues (JH or JH - 1)
-  unsigned wbase[JB];
-#pragma unroll
-  for (int j = 0; j < JB; ++j) {
-    const int row = (wave + j * NW) * 16 + lrow;
-    wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ rswz<bf16>(row)) << 3)) * 2);
-  }
-  auto issue_b = [&](int ks) {
-    const int c = ks / NT, t = ks - c * NT;
-    const unsigned Bs = sbase + 2 * HALO + (ks & 1) * BST;
-    const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32) + wph;
-#pragma unroll
-    for (int j = 0; j < JB; ++j) dma16s(wr, Bs + (wave + j * NW) * 1024, wbase[j], k0 * 2);
-  };
-  auto issue_halo = [&](int c) {
-    const unsigned Hs = sbase + (c & 1) * HALO;
-#pragma unroll
-    for (int j = 0; j < JH; ++j)
-      if (j < JH - 1 || wave + j * NW < HQ) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], (unsigned)(c * 64));
-  };
-
-  const int lr = lane & 15, lh = lane >> 4;
-  int hpb[RM];
-#pragma unroll
-  for (int m = 0; m < RM; ++m) {
-    const int loc = wm * RM * 16 + m * 16 + lr;
-    hpb[m] = (loc >> 6) * 66 + (loc & 63);
-  }
-  f32x4 acc[RN][RM];
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nch = a.Cin >> 5, nks = NT * nch;
-  constexpr bool prio = true;
-  issue_b(0);
-  issue_halo(0);
-  for (int ks = 0; ks < nks; ++ks) {
-    const int c = ks / NT, t = ks - c * NT;
-    // step 9c+1 may leave the halo of chunk c+1 (issued last, at step 9c) in flight
-    if (t == 1 && c + 1 < nch) {
-      if (nh == JH) wait_vm<JH>();
-      else wait_vm<(JH > 0 ? JH - 1 : 0)>();
-    } else {
-      wait_vm<0>();
-    }
-    __syncthreads();
-    if (!(a.dbg & 2)) {                               // bit 1: DMA only the first stage (experiment)
-      if (ks + 1 < nks) issue_b(ks + 1);
-      if (t == 0 && c + 1 < nch) issue_halo(c + 1);
-    }
-    if (a.dbg & 1) continue;                          // bit 0: no fragment reads / MFMA (experiment)
-    // halo row / column of the tap (the halo starts one pixel above / left of the tile)
-    const int r = SUBP ? (t >> 1) + pa : t / 3, s3 = SUBP ? (t & 1) + pb : t - (t / 3) * 3;
-    const char* Hs = smem + (c & 1) * HALO;
-    const char* Bs = smem + 2 * HALO + (ks & 1) * BST;
-    Frag<bf16> fa[RN], fb[RM];
-#pragma unroll
-    for (int i = 0; i < RN; ++i) {
-      const int row = wn * RN * 16 + i * 16 + lr;
-      fa[i].lds(Bs + row * 64 + ((lh ^ rswz<bf16>(row)) << 4));
-    }
-#pragma unroll
-    for (int m = 0; m < RM; ++m) {
-      const int hp = hpb[m] + r * 66 + s3;
-      fb[m].lds(Hs + hp * 64 + ((lh ^ h3swz(hp)) << 4));
-    }
-    if (prio) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < RN; ++i)
-#pragma unroll
-      for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
-    if (prio) __builtin_amdgcn_s_setprio(0);
-  }
-  if (a.dbg & 4) {   // experiment: skip the epilogue (keep one store so the MFMAs stay live)
-    if (acc[0][0][0] == 12345.f) reinterpret_cast<float*>(a.y)[tid] = acc[RN - 1][RM - 1][3];
-    return;
-  }
-  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, SUBP ? tm * 4 + phase : tm, wn, wm, lane, tid);
-}
-
 // Software-pipelined variant: a step is a PAIR of taps (64 k), the weight stage holds both
 // taps' 32-channel slices, and the loop is conv_fwd_v2's: the fragments of the step's second
 // tap are read while the first tap's MFMAs run and the barrier sits between the two MFMA
@@ -1065,7 +929,6 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   };
 
   Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
-  const int nh = (HQ - wave + NW - 1) / NW;   // halo pieces this wave issues
   auto bcnt = [&](int j) { return j < nsteps ? (2 * j + 1 < ntap ? 2 : 1) * JB : 0; };
   // ring of NSB weight stages: stage j in buffer j % NSB, issued NSB - 1 steps ahead; the
   // barrier of step j waits for stage j + 1 only (counted vmcnt: what this wave issued in
@@ -1439,128 +1302,19 @@ conv_halo_fwd(ConvArgs a, unsigned x_bytes) {
 // Wave w: row w >> 1 and five (m-tile, n-tile) pairs of that row's 5 m-tiles x 2 n-tiles.
 // Weights wn [32][448] (n = co * 7 + s, k = r * 64 + ci, 28 KB) are staged in LDS with the halo.
 // ----------------------------------------------------------------------------------------
-constexpr int C7_TR = 4;
-__global__ void __launch_bounds__(512, 1)
-conv7_n3_fwd(ConvArgs a, unsigned x_bytes) {
-  constexpr int TW = 64, HWD = 70, HR = C7_TR + 6, CPP = 8;
-  constexpr int HCH = HR * HWD * CPP, HQ = (HCH + 63) / 64;
-  constexpr int HB = HQ * 1024;
-  constexpr int DL = C7_TR * 80 * 33 * 4;                // D tile in LDS (fp32, rows of 32 + 1 pad)
-  constexpr int WB = 32 * 448 * 2, WQ = WB / 1024;       // weights [32][448] bf16 after the halo
-  __shared__ __attribute__((aligned(1024))) char smem[(HB > DL ? HB : DL) + WB];
-  char* wl = smem + (HB > DL ? HB : DL);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_w = a.W / TW, tiles_h = a.H / C7_TR;
-  const int tile = blockIdx.x;
-  const int n = tile / (tiles_h * tiles_w);
-  const int rem = tile - n * tiles_h * tiles_w;
-  const int h0 = (rem / tiles_w) * C7_TR, w0 = (rem % tiles_w) * TW;
-  const int li = lane & 15, g = lane >> 4;
-
-  // halo: pixel (hr, hc) <- x[h0 + hr - 3][w0 + hc - 3], 16-B chunks XOR-swizzled by pixel
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
-  for (int q = wave; q < HQ; q += 8) {
-    const int L = q * 64 + lane;
-    const int hp = L >> 3, ch = L & 7;
-    const int hr = hp / HWD, hc = hp - hr * HWD;
-    const int hh = h0 + hr - 3, ww = w0 + hc - 3;
-    const int sc = ch ^ (hp & 7);
-    const bool ok = L < HCH && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-    const unsigned off = ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * 64 + sc * 8) * 2) : 0x80000000u;
-    dma16(xr, smem + q * 1024, off);
-  }
-  // weights: row n (896 B = 56 chunks) with its 16-B chunks XOR-swizzled by (n & 7)
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, WB, 0x00020000);
-  for (int q = wave; q < WQ; q += 8) {
-    const int L = q * 64 + lane;
-    const int wrow = L / 56, slot = L - wrow * 56;
-    dma16(wr, wl + q * 1024, (unsigned)(wrow * 896 + ((slot ^ (wrow & 7)) << 4)));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int row = wave >> 1, half = wave & 1;
-  // this wave's pairs: half 0 -> (m0,n0)(m0,n1)(m1,n0)(m1,n1)(m2,n0); half 1 -> (m2,n1)(m3,n0)(m3,n1)(m4,n0)(m4,n1)
-  const int mb = half ? 2 : 0;                             // first of the wave's 3 m-tiles
-  f32x4 acc[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int apix[3];                                             // halo pixel of this lane, tap row 0
-#pragma unroll
-  for (int t = 0; t < 3; ++t) apix[t] = row * HWD + min((mb + t) * 16 + li, HWD - 1);
-#pragma unroll 2
-  for (int ks = 0; ks < 14; ++ks) {
-    const int r = ks >> 1, c = (ks & 1) * 4 + g;            // tap row, this lane's 16-B chunk
-    bf16x8 bfr[2], afr[3];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int nr = t * 16 + li;
-      bfr[t] = *reinterpret_cast<const bf16x8*>(wl + nr * 896 + (((ks * 4 + g) ^ (nr & 7)) << 4));
-    }
-#pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int hp = apix[t] + r * HWD;
-      afr[t] = *reinterpret_cast<const bf16x8*>(smem + (hp * CPP + (c ^ (hp & 7))) * 16);
-    }
-    if (half == 0) {
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bfr[0], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bfr[1], acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[0], acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[1], acc[3], 0, 0, 0);
-      acc[4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bfr[0], acc[4], 0, 0, 0);
-    } else {
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bfr[1], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[0], acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[1], bfr[1], acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bfr[0], acc[3], 0, 0, 0);
-      acc[4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[2], bfr[1], acc[4], 0, 0, 0);
-    }
-  }
-  __syncthreads();                                         // halo reads done: reuse LDS for D
-  // D[row][col][n] fp32, col = m*16 + 4*(lane>>4) + i (the MFMA row), n = nt*16 + (lane & 15)
-  float* Dl = reinterpret_cast<float*>(smem);
-  const int pm[5] = {half ? 2 : 0, half ? 3 : 0, half ? 3 : 1, half ? 4 : 1, half ? 4 : 2};
-  const int pn[5] = {half ? 1 : 0, half ? 0 : 1, half ? 1 : 0, half ? 0 : 1, half ? 1 : 0};
-#pragma unroll
-  for (int i = 0; i < 5; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) Dl[(row * 80 + pm[i] * 16 + g * 4 + j) * 33 + pn[i] * 16 + li] = acc[i][j];
-  __syncthreads();
-  // out[h0+row][w0+w][co] = bias + sum_s D[row][w + s][co*7 + s]; NCHW fp32 (+ sigmoid)
-  const int HWo = a.H * a.W;
-  // a wave covers one (co, row) segment of 64 pixels = one BN-statistics record
-  for (int o = tid; o < C7_TR * TW * a.Cout; o += 512) {
-    const int co = o / (C7_TR * TW), rr = (o / TW) % C7_TR, w = o % TW;
-    float v = a.bias ? a.bias[co] : 0.f;
-#pragma unroll
-    for (int s7 = 0; s7 < 7; ++s7) v += Dl[(rr * 80 + w + s7) * 33 + co * 7 + s7];
-    if (a.stats) {
-      const float sv = wave_sum(v), qv = wave_sum(v * v);
-      const int rec = ((n * a.H + h0 + rr) * a.W + w0) >> 6;
-      if (lane == 0) {
-        a.stats[(long)(rec * 2) * a.Cout + co] = sv;
-        a.stats[(long)(rec * 2 + 1) * a.Cout + co] = qv;
-      }
-    }
-    if (a.sigmoid) v = 1.f / (1.f + expf(-v));
-    const int pix = (h0 + rr) * a.W + w0 + w;
-    if (a.nchw) reinterpret_cast<float*>(a.y)[((long)(n * a.Cout + co)) * HWo + pix] = v;
-    else reinterpret_cast<bf16*>(a.y)[((long)n * HWo + pix) * a.ldy + co] = (bf16)v;
-  }
-}
+constexpr int C7_TR = 4;   // output rows per band step of conv7_n3_fwd2 (H % C7_TR == 0)
 
 // ----------------------------------------------------------------------------------------
-// conv7_n3_fwd2: the same "column taps in N" out_conv forward, sliding down a band of rows.
-// conv7_n3_fwd stages a 10-row halo for every 4 output rows (2.5x input re-read, 598 MB of
-// HBM per launch for a 268 MB input) and waits for it with one block per CU.  Here a block
+// conv7_n3_fwd2: the "column taps in N" out_conv forward, sliding down a band of rows.
+// (Its per-tile predecessor staged a 10-row halo for every 4 output rows: 2.5x input re-read,
+// 598 MB of HBM per launch for a 268 MB input, one block per CU; 189 -> 118 us.)  Here a block
 // owns (image, 64-column strip, band of C7B_BAND output rows) and keeps a ring of 14 input
 // rows in LDS (72 pixels x 128 B = 9 pieces of 1 KB per row, so a row is whole DMA pieces):
 // while the 8 waves compute output rows 4j..4j+3 from ring rows 4j-3..4j+6, the DMA of rows
 // 4j+7..4j+10 (the next group's) is in flight.  Input bytes per launch ~1.05x the tensor.
 // The weights sit in registers as MFMA B fragments (14 k-steps x 2 n-tiles, 112 VGPRs).
 // Per group: D[row][w'][n] (fp32, the 21 used columns) through LDS, then the 7-tap column
-// sums + bias (+ sigmoid, + BN records) as in conv7_n3_fwd.
+// sums + bias (+ sigmoid, + BN records).
 // ----------------------------------------------------------------------------------------
 constexpr int C7B_SLOTS = 14, C7B_ROWPX = 72, C7B_ROWB = C7B_ROWPX * 128;   // 9216 B
 constexpr int C7B_DLD = 22;                                                // D row stride (floats)
@@ -2267,177 +2021,13 @@ conv_wgrad_v2(Wg2Args a) {
 }
 
 // ----------------------------------------------------------------------------------------
-// Weight gradient of a 3x3 stride-1 conv with a halo-staged input (bf16, cin % 32 == 0,
-// cout % 128 == 0, W % 64 == 0): dW[co][tap][ci] = sum_p dy[p][co] * x[p + off(tap)][ci].
-// A block owns 128 co x (9 taps x 32 ci) = 128 x 288 and walks 64-pixel row segments of its
-// pixel split.  Per segment the dy row (64 px x 128 co, 16 KB) and the x halo (3 rows x 66 px
-// x 32 ci, 13 KB) land in LDS by DMA through a 3-stage ring (counted vmcnt); the 9 taps read
-// shifted windows of the halo as transposed B fragments: 29 KB per 2.4 M MACs, against
-// conv_wgrad_v2's im2col tiles (64 KB per 4.2 M at 256 x 256, 32 KB per 1 M at 128 x 128).
-//   8 waves = 2 (64 co) x 4 (k-tiles of 16: 5, 5, 4, 4 of the 18), <= 20 accumulators.
-// Output: slab [split][cout][9 cin] (k = tap * cin + ci, wgrad_reduce_kernel's layout) and
-// bias slab [split][cout] (blocks of ci chunk 0).
-// ----------------------------------------------------------------------------------------
-struct H3WgArgs {
-  const void* x;
-  const void* dy;
-  float* slab;
-  float* bslab;
-  int H, W, Cin, Cout, ldd, nsegs, spb, ntile, nct;
-  unsigned xbytes, dybytes;
-};
-
-__global__ void __launch_bounds__(512, 1)
-conv3_halo_wgrad(H3WgArgs a) {
-  constexpr int BC = 128, NS = 3;
-  constexpr int DYB = 64 * BC * 2;                  // 16 pieces
-  constexpr int HPX = 3 * 66, HQ = (HPX * 64 + 1023) / 1024, HALO = HQ * 1024;   // 13 pieces
-  constexpr int BUF = DYB + HALO;
-  constexpr int JD = DYB / 1024 / 8, JH = (HQ + 7) / 8;
-  __shared__ __attribute__((aligned(1024))) char smem[NS * BUF];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wave & 1, wk = wave >> 1;
-  const int kt0 = wk < 2 ? 5 * wk : 10 + 4 * (wk - 2), nkt = wk < 2 ? 5 : 4;
-  const int li = lane & 15, g = lane >> 4;
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int tile = lid % a.ntile, sp = lid / a.ntile;   // blocks of one split share an XCD
-  const int tc = tile % a.nct, cc = tile / a.nct;
-  const int co0 = tc * BC, ci0 = cc * 32;
-  const int sw = a.W >> 6;
-  const int g0 = sp * a.spb, g1 = min(a.nsegs, g0 + a.spb);
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), 0, (int)a.dybytes, 0x00020000);
-  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
-
-  // per-lane piece constants: dy (pixel, channel) and halo (row, column, channel)
-  int dpx[JD], dco[JD];
-#pragma unroll
-  for (int j = 0; j < JD; ++j) {
-    const int o = (wave + 8 * j) * 1024 + lane * 16;
-    dpx[j] = o / (BC * 2);
-    const int b = o - dpx[j] * (BC * 2);
-    dco[j] = ((((b >> 5) ^ tswz<BC>(dpx[j])) << 4) | (((b >> 4) & 1) << 3));
-  }
-  int hhr[JH], hhc[JH], hci[JH];
-#pragma unroll
-  for (int j = 0; j < JH; ++j) {
-    const int o = (wave + 8 * j) * 1024 + lane * 16;
-    const int hp = o >> 6, b = o & 63;
-    hci[j] = ((((b >> 5) ^ tswz<32>(hp)) << 4) | (((b >> 4) & 1) << 3));
-    hhr[j] = hp < HPX ? hp / 66 : 99;
-    hhc[j] = hp - (hp / 66) * 66;
-  }
-  const int nh = (HQ - wave + 7) / 8;               // halo pieces of this wave (JH or JH - 1)
-
-  auto issue = [&](int gs, int buf) {
-    const int n = gs / (a.H * sw), rem = gs - n * a.H * sw;
-    const int h = rem / sw, w0 = (rem - h * sw) * 64;
-    const unsigned ds = sbase + buf * BUF, hs = ds + DYB;
-    const int pbase = (n * a.H + h) * a.W + w0;
-#pragma unroll
-    for (int j = 0; j < JD; ++j)
-      dma16s(dr, ds + (wave + 8 * j) * 1024, (unsigned)(((pbase + dpx[j]) * a.ldd + co0 + dco[j]) * 2), 0u);
-#pragma unroll
-    for (int j = 0; j < JH; ++j) {
-      if (j < JH - 1 || wave + 8 * j < HQ) {
-        const int ih = h + hhr[j] - 1, iw = w0 + hhc[j] - 1;
-        const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-        dma16s(xr, hs + (wave + 8 * j) * 1024,
-               ok ? (unsigned)((((n * a.H + ih) * a.W + iw) * a.Cin + ci0 + hci[j]) * 2) : 0x80000000u, 0u);
-      }
-    }
-  };
-  // wait until the stage issued `ahead` issues ago has landed (the later ones may stay in flight)
-  auto wait_stage = [&](int ahead) {
-    if (ahead >= 2) {
-      if (nh == JH) wait_vm<2 * (JD + JH)>();
-      else wait_vm<2 * (JD + JH - 1)>();
-    } else if (ahead == 1) {
-      if (nh == JH) wait_vm<JD + JH>();
-      else wait_vm<JD + JH - 1>();
-    } else {
-      wait_vm<0>();
-    }
-  };
-
-  f32x4 acc[4][5];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
-  const bool do_bias = a.bslab && cc == 0;
-  const int bco = tid & (BC - 1), bpg = tid >> 7;      // bias: channel, 16-pixel group
-
-  const int nseg = g1 - g0;
-#pragma unroll
-  for (int i = 0; i < NS - 1; ++i)
-    if (i < nseg) issue(g0 + i, i);
-  for (int i = 0; i < nseg; ++i) {
-    // stages issued after stage i: min(NS - 2, nseg - 1 - i)
-    wait_stage(min(NS - 2, nseg - 1 - i));
-    __syncthreads();                                  // stage i landed everywhere; stage i-1 retired
-    if (i + NS - 1 < nseg) issue(g0 + i + NS - 1, (i + NS - 1) % NS);
-    const char* dys = smem + (i % NS) * BUF;
-    const char* hal = dys + DYB;
-    if (do_bias) {
-#pragma unroll
-      for (int k = 0; k < 16; ++k)
-        bsum += (float)*reinterpret_cast<const bf16*>(dys + timg_off<BC>(bpg * 16 + k, bco));
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) af[q] = tfrag<BC>(dys, kk * 32, wc * 64 + q * 16, lane);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        if (j < nkt) {
-          const int kt = kt0 + j, tap = kt >> 1, cb = (kt & 1) * 16;
-          const int r = tap / 3, s3 = tap - (tap / 3) * 3;
-          const bf16x8 bfr = tfrag<32>(hal, r * 66 + kk * 32 + s3, cb, lane);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bfr, acc[q][j], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_s_setprio(0);
-    }
-  }
-  // slab[sp][co][tap * Cin + ci0 + ci]: lane holds D[co = 4g + jj][k-col = li]
-  const long K = 9L * a.Cin;
-  float* sl = a.slab + (long)sp * a.Cout * K;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    if (j < nkt) {
-      const int kt = kt0 + j, tap = kt >> 1, cb = (kt & 1) * 16;
-      const long kcol = (long)tap * a.Cin + ci0 + cb + li;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) sl[(long)(co0 + wc * 64 + q * 16 + 4 * g + jj) * K + kcol] = acc[q][j][jj];
-    }
-  }
-  if (do_bias) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);
-    red[tid] = bsum;
-    __syncthreads();
-    if (tid < BC) a.bslab[(long)sp * a.Cout + co0 + tid] = (red[tid] + red[tid + 128]) + (red[tid + 256] + red[tid + 384]);
-  }
-}
-
-// ----------------------------------------------------------------------------------------
 // Sliding-row weight gradient of a 3x3 conv with 64 input channels (AFE.down1 64 -> 128 at
 // full resolution), each operand byte read from HBM once: a block owns 128 co x ALL 9 taps x
 // 64 ci (= 128 x 576, 36 accumulators per wave) and walks the rows [h0, h1) of one 64-column
 // strip of one image.  Per row h it needs dy row h and x rows h-1, h, h+1; dy rows stream
 // through a 3-deep ring, x rows through a 5-deep ring where each row lands once and stays for
-// the three rows that read it (conv3_halo_wgrad restaged dy per 32-channel k-tile and a fresh
-// 3-row halo per segment: 2.76x the algorithmic bytes).  A "group" i = {dy row h0+i, x row
+// the three rows that read it (its tile-per-segment predecessor restaged dy per 32-channel
+// k-tile and a fresh 3-row halo per segment: 2.76x the algorithmic bytes).  A "group" i = {dy row h0+i, x row
 // h0+i+1} is issued two rows ahead; a wave's DMAs of a group are counted (wave 0 issues 4 of
 // the 25 pieces, the others 3) so the wait for group i leaves group i+1 in flight.
 //   8 waves = 2 (64 co) x 4 (9 of the 36 k-tiles of 16 = (tap, 16 ci)).
@@ -3238,13 +2828,7 @@ int launch_fwd(const ConvArgs& a, int ks, FwdTile t, int pro, int ups, int nblk,
 }
 
 // v2 (DMA-fed bf16) path: bf16, no BN prologue, cin a multiple of 64, input < 2 GB
-static int g_disable_v2 = -1;
 bool use_v2(const fv_conv_desc* d) {
-  if (g_disable_v2 < 0) {
-    const char* e = getenv("FV_DISABLE_V2");
-    g_disable_v2 = (e && e[0] == '1') ? 1 : 0;
-  }
-  if (g_disable_v2) return false;
   if (d->dtype != FV_BF16 || d->pro_act || d->cin % 64) return false;
   if (d->out_nchw_f32 || d->epi_sigmoid || d->cout % 8 || d->ldy % 8) return false;   // staged NHWC epilogue
   if (d->w % 8) return false;   // a DMA piece (8 pixels) must lie in one image row
@@ -3252,31 +2836,19 @@ bool use_v2(const fv_conv_desc* d) {
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
 
-// 3x3 halo path (conv3_halo_fwd): co per block (256 / 128 / 64), 0 when not eligible
-static int g_disable_h3 = -1;
+// 3x3 halo path (conv3_halo_fwd2 / fwd3): co per block (256 / 128 / 64), 0 when not eligible
 int halo3_bn(const fv_conv_desc* d) {
-  if (g_disable_h3 < 0) {
-    const char* e = getenv("FV_DISABLE_H3");
-    g_disable_h3 = (e && e[0] == '1') ? 1 : 0;
-  }
-  if (g_disable_h3 || !use_v2(d) || d->ksize != 3 || d->upsample || d->w % 64 || d->h % 4) return 0;
+  if (!use_v2(d) || d->ksize != 3 || d->upsample || d->w % 64 || d->h % 4) return 0;
   if ((long)d->n * d->h * d->w * d->ldy * 2 >= (1L << 31)) return 0;
   // co % 256: the pipelined pair-of-taps kernel (3 % over conv_fwd_v2's 256 x 256 tile on
-  // the res convs; FV_H3_256=0 keeps conv_fwd_v2 for A/B)
-  static const bool h3_256 = !getenv("FV_H3_256") || atoi(getenv("FV_H3_256")) != 0;
-  if (d->cout % 256 == 0) return h3_256 ? 256 : 0;
+  // the res convs)
+  if (d->cout % 256 == 0) return 256;
   // AFE.down1's forward (64 -> 128 channels, K = 576): conv_fwd_v2's 128 x 256 tile measured
   // 500 us against 543 (pipelined halo) / 579 (single-tap halo) at 256x256, B=32
-  if (d->cin == 64 && d->cout == 128 && !getenv("FV_H3_DOWN1")) return 0;
+  if (d->cin == 64 && d->cout == 128) return 0;
   return d->cout % 128 == 0 ? 128 : d->cout % 64 == 0 ? 64 : 0;
 }
 
-// wgrad v2: next-stage DMA pieces spread between MFMA rows (FV_WG_IL=0 issues them as a
-// block after the barrier, for A/B)
-static int wg_interleave() {
-  static const int v = getenv("FV_WG_IL") ? atoi(getenv("FV_WG_IL")) : 1;
-  return v;
-}
 
 // v2 tile configs: id -> (co per block, pixels per block); waves/layout in launch_v2_ks
 struct V2Cfg { int bn, bm; };
@@ -3288,13 +2860,7 @@ constexpr V2Cfg kV2Cfg[] = {
     {128, 256},   // 4: 8 waves 2x4, wave 64co x 64px
     {256, 128},   // 5: 8 waves 4x2, wave 64co x 64px
 };
-static int g_v2_force = -2;
 int v2_cfg(int rows_needed) {
-  if (g_v2_force == -2) {
-    const char* e = getenv("FV_V2_CFG");
-    g_v2_force = e ? atoi(e) : -1;
-  }
-  if (g_v2_force >= 0 && rows_needed % kV2Cfg[g_v2_force].bn == 0) return g_v2_force;
   if (rows_needed % 256 == 0) return 3;
   if (rows_needed > 64) return 0;
   if (rows_needed > 16) return 1;
@@ -3326,12 +2892,11 @@ int launch_v2_b(const ConvArgs& a, int mode, int nblk, unsigned xb, hipStream_t 
 }
 
 // 4-wave tiles stage 32-deep k slices when K is short (<= 640) or the input is upsampled:
-// there the 4-blocks-per-CU occupancy beats the deeper k step (A/B on the FaceVAE shapes;
-// FV_CONV_DBG bit 4 forces 64)
+// there the 4-blocks-per-CU occupancy beats the deeper k step (A/B on the FaceVAE shapes)
 template <int KS, int WN, int WM, int RN, int RM>
 int launch_v2_t(const ConvArgs& a, int mode, int nblk, unsigned xb, hipStream_t s) {
   if constexpr (WN * WM == 4) {
-    if (!(a.dbg & 16) && a.W % 16 == 0 && (a.Kpad <= 640 || mode != 0))
+    if (a.W % 16 == 0 && (a.Kpad <= 640 || mode != 0))
       return launch_v2_b<KS, WN, WM, RN, RM, 32>(a, mode, nblk, xb, s);
   }
   return launch_v2_b<KS, WN, WM, RN, RM, 64>(a, mode, nblk, xb, s);
@@ -3376,22 +2941,6 @@ bool use_subpix(const fv_conv_desc* d) {
   return pl % fwd_tile_v2(d->cout).bm == 0;
 }
 
-// sub-pixel phases through the halo-staged kernel: co tile (128 / 64), 0 when not eligible
-// Off by default: an alternating A/B on one box (r2, 4 reps each) put up1's forward at
-// 214.9 us through this path against 193.7 us through conv_fwd_v2 MODE 2, and up2 (64-channel
-// co tiles) was already 5 % faster on v2.  FV_H3SUB=1 turns it back on for A/B runs.
-static int g_h3sub = -1;
-int subpix_halo_bn(const fv_conv_desc* d) {
-  if (g_h3sub < 0) {
-    const char* e = getenv("FV_H3SUB");
-    g_h3sub = (e && e[0] == '1') ? 1 : 0;
-  }
-  if (!g_h3sub || !use_subpix(d)) return 0;
-  const int hl = d->h / 2, wl = d->w / 2;
-  if (wl % 64 || hl % 4 || d->cin % 32) return 0;
-  return d->cout % 128 == 0 ? 128 : 0;
-}
-
 // data gradient of an upsample + 3x3 conv computed directly at the low resolution as a
 // stride-2 4x4 conv over dy (bf16 v2 path; replaces dgrad at the high resolution followed by
 // the 2x2 sum of fv_upsample2x_bwd: 0.44x the MACs, one pass fewer)
@@ -3404,24 +2953,17 @@ bool use_dgrad_lowres(const fv_conv_desc* d) {
 }
 
 // Generator.out_conv shape: 7x7, 64 -> <= 4 channels, NCHW fp32 output (bf16 operands)
-static int g_disable_c7n = -1;
 bool use_c7n(const fv_conv_desc* d) {
-  if (g_disable_c7n < 0) {
-    const char* e = getenv("FV_DISABLE_C7N");
-    g_disable_c7n = (e && e[0] == '1') ? 1 : 0;
-  }
-  return !g_disable_c7n && d->dtype == FV_BF16 && d->ksize == 7 && d->cin == 64 && d->cin_valid == 64 &&
+  return d->dtype == FV_BF16 && d->ksize == 7 && d->cin == 64 && d->cin_valid == 64 &&
          d->cout <= 4 && !d->pro_act && !d->upsample && d->w % 64 == 0 && d->h % C7_TR == 0 &&
          (long)d->n * d->h * d->w * 64 * 2 < (1L << 31);
 }
 
 // band of output rows per block of the sliding out_conv forward (conv7_n3_fwd2): the largest
-// of 128/64/32/16/8/4 dividing H that still gives >= 256 blocks (else the smallest dividing);
-// 0 = the per-tile conv7_n3_fwd (FV_C7_V1=1 forces it, for A/B).  FV_C7_BAND=b forces a band
-// (tests: multi-group rings on small images); read per call.
-static const int g_c7_v1 = getenv("FV_C7_V1") && atoi(getenv("FV_C7_V1")) != 0;
+// of 128/64/32/16/8/4 dividing H that still gives >= 256 blocks (else the smallest dividing;
+// use_c7n guarantees H % 4 == 0).  FV_C7_BAND=b forces a band (tests: multi-group rings on
+// small images); read per call.
 static int c7n_band(const fv_conv_desc* d) {
-  if (g_c7_v1) return 0;
   if (const char* e = getenv("FV_C7_BAND")) {
     const int b = atoi(e);
     if (b >= 4 && b % 4 == 0 && d->h % b == 0) return b;
@@ -3435,30 +2977,20 @@ static int c7n_band(const fv_conv_desc* d) {
   return pick;
 }
 
-// 3x3 weight gradient with the halo-staged input: conv3_halo_wgrad2 (sliding rows, default)
-// or conv3_halo_wgrad (FV_H3W_V1=1, for A/B)
-static const int g_h3w_v1 = getenv("FV_H3W_V1") && atoi(getenv("FV_H3W_V1")) != 0;
-static int g_disable_h3w = -1;
+// 3x3 weight gradient with the halo-staged input, rows sliding down a segment
+// (conv3_halo_wgrad2; its tile-per-row-segment predecessor ran 518 us against 262 us for
+// AFE.down1)
 bool use_h3w(const fv_conv_desc* d) {
-  if (g_disable_h3w < 0) {
-    const char* e = getenv("FV_DISABLE_H3W");
-    g_disable_h3w = (e && e[0] == '1') ? 1 : 0;
-  }
   // measured against conv_wgrad_v2 (tools/convbench.py): 12 % faster on AFE.down1 (64 -> 128,
   // whose v2 tile is 128 x 128), slower where v2 runs 256 x 256 tiles (LDS fill per MAC of
   // the two is then within 20 %), so only cin == 64 takes it
-  return !g_disable_h3w && d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && !d->pro_act &&
+  return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && !d->pro_act &&
          d->cin == 64 && d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
 }
 
 // out_conv weight gradient as "row taps in N" (conv7_n3_wgrad)
-int g_disable_c7w = -1;
 bool use_c7w(const fv_conv_desc* d) {
-  if (g_disable_c7w < 0) {
-    const char* e = getenv("FV_DISABLE_C7W");
-    g_disable_c7w = (e && e[0] == '1') ? 1 : 0;
-  }
-  return !g_disable_c7w && d->dtype == FV_BF16 && d->ksize == 7 && d->cin == 64 && d->cin_valid == 64 &&
+  return d->dtype == FV_BF16 && d->ksize == 7 && d->cin == 64 && d->cin_valid == 64 &&
          d->cout <= 4 && !d->pro_act && !d->upsample && d->w % 64 == 0 &&
          (long)d->n * d->h * d->w * 64 * 2 < (1L << 31);
 }
@@ -3512,17 +3044,9 @@ constexpr Wg2Cfg kWg2Cfg[] = {
     {512, 64, 8, 1, 64, 2},    // 12
 };
 constexpr int kNumWg2Cfg = sizeof(kWg2Cfg) / sizeof(kWg2Cfg[0]);
-static int g_wg2_force = -2;
 int wg2_cfg(const fv_conv_desc* d, int K) {
-  if (g_wg2_force == -2) {
-    const char* e = getenv("FV_WG2_CFG");
-    g_wg2_force = e ? atoi(e) : -1;
-  }
   const int bc = d->cout > 128 ? 256 : d->cout > 64 ? 128 : d->cout > 16 ? 64 : 16;
-  if (g_wg2_force >= 0 && g_wg2_force < kNumWg2Cfg && kWg2Cfg[g_wg2_force].bc == bc &&
-      d->w % kWg2Cfg[g_wg2_force].px == 0 && (d->ksize == 3 || g_wg2_force <= 5))
-    return g_wg2_force;
-  // defaults from the FaceVAE-shape sweep (tools/gpu_wgsweep.sh): 384 x 64 tiles for the
+  // defaults from the FaceVAE-shape tile sweep (r1): 384 x 64 tiles for the
   // 64-channel layers (K = 1152 splits exactly), 32-pixel stages 3-deep when K is not a
   // multiple of 256 at 256 channels
   if (bc == 16) return 5;
@@ -3531,19 +3055,14 @@ int wg2_cfg(const fv_conv_desc* d, int K) {
   if (bc == 256) return K % 256 == 0 ? 0 : (d->ksize == 3 && d->w % 32 == 0 ? 6 : 1);
   return k256 ? 2 : 3;
 }
-static int g_disable_wg2 = -1;
 WgPlan plan_wgrad(const fv_conv_desc* d) {
-  if (g_disable_wg2 < 0) {
-    const char* e = getenv("FV_DISABLE_WG2");
-    g_disable_wg2 = (e && e[0] == '1') ? 1 : 0;
-  }
   WgPlan p{};
   const int K = d->ksize * d->ksize * d->cin;
   const long P = (long)d->n * d->h * d->w;
   const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
   // 32-bit buffer offsets: x and dy (channel stride = cout padded to a power of two >= 8, as
   // every caller passes; fv_conv2d_bwd_weight re-checks the real stride) must stay < 2 GB
-  p.v2 = !g_disable_wg2 && d->dtype == FV_BF16 && !d->pro_act && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
+  p.v2 = d->dtype == FV_BF16 && !d->pro_act && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
          P * pad_pow2_8(d->cout) * 2 < (1L << 31);
   // out_conv 7x7 64 -> <= 4 (v2 == 3): blocks = (image, 64-column strip, row segment), about
   // 4 per CU; slab [block][32 (r, co)][448 (s, ci)]
@@ -3563,7 +3082,7 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   }
   // 3x3 sliding-row wgrad (v2 == 5, conv3_halo_wgrad2): blocks = (image, 64-column strip,
   // row segment) x co tiles of 128, ~1 block per CU; splits = image x strip x segment
-  if (p.v2 && use_h3w(d) && !g_h3w_v1) {
+  if (p.v2 && use_h3w(d)) {
     const int strips = d->w / 64;
     p.v2 = 5;
     p.ntc = d->cout / 128;
@@ -3574,21 +3093,6 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
     p.sps = fv_cdiv(d->h, nseg);                  // rows per segment
     p.nsteps = fv_cdiv(d->h, p.sps);              // segments
     p.nsplit = d->n * strips * p.nsteps;
-    p.CW = d->cout;
-    p.KW = K;
-    return p;
-  }
-  // 3x3 halo wgrad (v2 == 4): tiles of 128 co x (9 taps x 64 ci), ~1 block per CU
-  if (p.v2 && use_h3w(d)) {
-    p.v2 = 4;
-    p.ntc = d->cout / 128;
-    p.ntk = d->cin / 32;
-    const int ntile = p.ntc * p.ntk;
-    p.nsteps = d->n * d->h * (d->w / 64);        // 64-pixel row segments
-    int ns = 256 / ntile;
-    if (ns < 1) ns = 1;
-    p.sps = fv_cdiv(p.nsteps, ns);               // segments per split
-    p.nsplit = fv_cdiv(p.nsteps, p.sps);
     p.CW = d->cout;
     p.KW = K;
     return p;
@@ -3765,13 +3269,8 @@ int fv_conv2d_dgrad_lowres(const fv_conv_desc* d) {
 }
 
 // 7x7 halo path: (cin 8 -> cout 64, TR 8, weights in LDS) or (cin 64 -> cout <= 16, TR 2)
-static int g_disable_halo = -1;
 static int halo_tr(const fv_conv_desc* d) {
-  if (g_disable_halo < 0) {
-    const char* e = getenv("FV_DISABLE_HALO");
-    g_disable_halo = (e && e[0] == '1') ? 1 : 0;
-  }
-  if (g_disable_halo || d->dtype != FV_BF16 || d->ksize != 7 || d->pro_act || d->upsample || d->w % 64) return 0;
+  if (d->dtype != FV_BF16 || d->ksize != 7 || d->pro_act || d->upsample || d->w % 64) return 0;
   int tr = 0;
   // (8-row tiles for the 8-channel side, 16 MFMAs per 8 LDS reads per wave, measured 13.28 ->
   // 13.33 ms/step in an A/B: not kept)
@@ -3794,7 +3293,6 @@ static int stats_record_pixels(const fv_conv_desc* d) {
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
   const FwdTile t = plan_tile(d);
   if (const int bn = halo3_bn(d)) return bn == 256 ? 128 : 64;   // RM * 16 pixels per wave row
-  if (subpix_halo_bn(d)) return 64;                            // RM * 16 (both co tiles)
   if (use_v2(d)) {
     if (t.bn == 64 || t.bn == 16 || (t.bn == 128 && t.bm == 256)) return t.bm / 4;
     return t.bm / 2;                                          // 128x128, 256x256, 256x128
@@ -3942,7 +3440,6 @@ static int sr_geometry(const fv_conv_desc* d, int* bp) {
   return (int)(P / 256 * nw);
 }
 
-static int g_conv_dbg = -1;
 static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
                     const float* psc, const float* psh, const void* res, void* y, float* stats,
                     hipStream_t s, const fv_store_reduce* sr = nullptr) {
@@ -3970,23 +3467,14 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   a.K = d->ksize * d->ksize * d->cin; a.Kpad = kpad_of(d->ksize, d->cin); a.nks = a.Kpad / BK;
   a.sigmoid = d->epi_sigmoid; a.nchw = d->out_nchw_f32;
   a.ntn = fv_cdiv(d->cout, t.bn);
-  if (g_conv_dbg < 0) {
-    const char* e = getenv("FV_CONV_DBG");
-    g_conv_dbg = e ? atoi(e) : 0;
-  }
-  a.dbg = g_conv_dbg;
   int st;
   if (use_c7n(d)) {
     FV_REQUIRE(!res, "out_conv kernel: no residual");
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
-    if (const int band = c7n_band(d)) {
-      const int nblk = d->n * (d->h / band) * (d->w / 64);
-      hipLaunchKernelGGL(conv7_n3_fwd2, dim3(nblk), dim3(512), 0, s, a, xb, band);
-      return fv_check_launch("conv2d_fwd_c7n2");
-    }
-    const int nblk = d->n * (d->h / C7_TR) * (d->w / 64);
-    hipLaunchKernelGGL(conv7_n3_fwd, dim3(nblk), dim3(512), 0, s, a, xb);
-    return fv_check_launch("conv2d_fwd_c7n");
+    const int band = c7n_band(d);
+    const int nblk = d->n * (d->h / band) * (d->w / 64);
+    hipLaunchKernelGGL(conv7_n3_fwd2, dim3(nblk), dim3(512), 0, s, a, xb, band);
+    return fv_check_launch("conv2d_fwd_c7n2");
   }
   if (const int tr = halo_tr(d)) {
     a.lgtw = 6;
@@ -4009,19 +3497,6 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.nks = a.Kpad / BK2;
     a.ntn = fv_cdiv(d->cout, t2.bn);
     a.wphase = fv_cdiv(d->cout, t.bn) * t.bn * a.Kpad;
-    if (const int bn = subpix_halo_bn(d)) {
-      // halo-staged phases: the low-res (TR + 2) x 66 window is staged once per 32 channels
-      // for the phase's 4 taps (conv3_halo_fwd<..., SUBP>)
-      a.lgtw = 6;
-      a.ntn = d->cout / bn;
-      const int nblk = 4 * a.ntn * d->n * (a.H / 4) * (a.W / 64);
-      const unsigned xb = (unsigned)((long)d->n * a.Hin * a.Win * d->cin * 2);
-      if (bn == 128)
-        hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4, true>), dim3(nblk), dim3(512), 0, s, a, xb);
-      else
-        hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4, true>), dim3(nblk), dim3(256), 0, s, a, xb);
-      return fv_check_launch("conv2d_fwd_subpix_halo");
-    }
     const int nblk2 = 4 * a.ntn * (a.P / t2.bm);
     const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
     st = launch_v2(a, 2, t2, 2, nblk2, (unsigned)xb, s);
@@ -4037,31 +3512,22 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.ntn = d->cout / bn;
     const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
-    // pipelined pair-of-taps kernel for every co tile (r2 convbench, 256x256 B=32: down2 dgrad
-    // 369 -> 324 us, down1 dgrad 433 -> 414 us against the single-tap loop; FV_H3_PIPE=0/1
-    // forces one for A/B)
-    static const int pipe_env = getenv("FV_H3_PIPE") ? atoi(getenv("FV_H3_PIPE")) : -1;
-    const int pipe = pipe_env >= 0 ? pipe_env : 1;
-    // linear-halo kernel (conv3_halo_fwd3); FV_H3_V3=0 falls back to fwd2 for A/B
-    static const int v3 = getenv("FV_H3_V3") ? atoi(getenv("FV_H3_V3")) : 1;
-    // (64-channel co tiles stay on fwd2: 448 -> 667 us for AFE.down1's data gradient)
-    if (pipe && v3 && bn >= 128 && a.Cin % 64 == 0) {
+    // linear-halo pair-of-taps kernel (conv3_halo_fwd3) for the 256 / 128-channel co tiles;
+    // conv3_halo_fwd2 (XOR-swizzled halo) for 64-channel co tiles (AFE.down1's data gradient:
+    // 448 us against 667 us on fwd3) and channel counts that are not a multiple of 64.
+    // (measured and not kept, r2: the single-tap halo loop -- down2 dgrad 369 vs 324 us,
+    // down1 dgrad 433 vs 414 us; a 3-deep weight ring for the 256-channel tiles, 2.5 % slower;
+    // 8-row tiles for the 64-channel co tile, 418 -> 420 us; weight-DMA pieces spread between
+    // the MFMA rows as conv_wgrad_v2 does, res conv forward 134 -> 160 us)
+    if (bn >= 128 && a.Cin % 64 == 0) {
       if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 256) {
-      static const int nsb = getenv("FV_H3_NSB") ? atoi(getenv("FV_H3_NSB")) : 2;   // 3: deeper ring (A/B: 2.5 % slower)
-      if (pipe && nsb == 2) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
-      else if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
-      else hipLaunchKernelGGL((conv3_halo_fwd<4, 2, 4, 8>), dim3(nblk), dim3(512), 0, s, a, xb);
+      hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 128) {
-      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
-      else hipLaunchKernelGGL((conv3_halo_fwd<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+      hipLaunchKernelGGL((conv3_halo_fwd2<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else {
-      // (measured and not kept: 8-row tiles, conv3_halo_fwd2<1, 8, 4, 4, 3>, AFE.down1's data
-      // gradient 418 -> 420 us; weight-DMA pieces spread between the MFMA rows as conv_wgrad_v2
-      // does, in fwd2 / fwd3: res conv forward 134 -> 160 us)
-      if (pipe) hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4, 3>), dim3(nblk), dim3(256), 0, s, a, xb);
-      else hipLaunchKernelGGL((conv3_halo_fwd<1, 4, 4, 4>), dim3(nblk), dim3(256), 0, s, a, xb);
+      hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4, 3>), dim3(nblk), dim3(256), 0, s, a, xb);
     }
     return fv_check_launch("conv2d_fwd_halo3");
   }
@@ -4162,11 +3628,6 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
     a.Cout = d->cin; a.ldy = d->cin;
     a.Kpad = 16 * t.cin; a.K = a.Kpad; a.nks = a.Kpad / BK2;
     a.ntn = fv_cdiv(d->cin, t2.bn);
-    if (g_conv_dbg < 0) {
-      const char* e = getenv("FV_CONV_DBG");
-      g_conv_dbg = e ? atoi(e) : 0;
-    }
-    a.dbg = g_conv_dbg;
     const int nblk = a.ntn * fv_cdiv(a.P, t2.bm);
     const long xb = (long)d->n * d->h * d->w * t.cin * 2;
     const int st = launch_v2(a, 4, t2, 3, nblk, (unsigned)xb, (hipStream_t)stream);
@@ -4218,17 +3679,6 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
     return fv_check_launch("conv2d_bwd_weight_halo3s");
   }
-  if (t.v2 == 4) {
-    FV_REQUIRE(P * ldy_dy * 2 < (1L << 31) && P * d->cin * 2 < (1L << 31), "wgrad: operand larger than 2 GB");
-    H3WgArgs a{};
-    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
-    a.H = d->h; a.W = d->w; a.Cin = d->cin; a.Cout = d->cout; a.ldd = ldy_dy;
-    a.nsegs = t.nsteps; a.spb = t.sps; a.ntile = t.ntc * t.ntk; a.nct = t.ntc;
-    a.xbytes = (unsigned)(P * d->cin * 2);
-    a.dybytes = (unsigned)(P * ldy_dy * 2);
-    hipLaunchKernelGGL(conv3_halo_wgrad, dim3(a.ntile * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
-    return fv_check_launch("conv2d_bwd_weight_halo3");
-  }
   if (t.v2 == 3) {
     FV_REQUIRE(ldy_dy == 8, "wgrad (out_conv 7x7): dy channel stride must be 8 (got %d)", ldy_dy);
     W7Args a{};
@@ -4269,7 +3719,7 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.fw = make_fastdiv((uint32_t)Win);
     a.fh = make_fastdiv((uint32_t)Hin);
     a.rowal = 1;
-    a.il = wg_interleave();
+    a.il = 1;
     a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
     const int nblk = 4 * t.ntk * t.ntc * t.nsplit;
@@ -4293,7 +3743,7 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.fw = make_fastdiv((uint32_t)d->w);
     a.fh = make_fastdiv((uint32_t)d->h);
     a.rowal = (d->w % t.px) == 0;
-    a.il = wg_interleave();
+    a.il = 1;
     a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
     const int nblk = t.ntk * t.ntc * t.nsplit;

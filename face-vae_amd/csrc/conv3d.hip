@@ -505,8 +505,7 @@ __global__ void __launch_bounds__(256) depth_split_kernel(const T* __restrict__ 
 }
 
 bool c32_fast(const fv_conv3d_desc* d) {
-  static const bool off = getenv("FV_DISABLE_C3") && atoi(getenv("FV_DISABLE_C3")) != 0;
-  return !off && d->dtype == FV_BF16 && d->cin == 32 && d->cout == 32 && d->w == 64 && d->h % 4 == 0 &&
+  return d->dtype == FV_BF16 && d->cin == 32 && d->cout == 32 && d->w == 64 && d->h % 4 == 0 &&
          (long)d->n * d->d * d->h * d->w * 32 * 2 < (1L << 31);
 }
 

@@ -30,7 +30,6 @@ averaging / SyncBN plumbing is testable on CPU with world_size 2.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import os
 import random
@@ -40,7 +39,6 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import ops as _ops
 
 _COMM = None          # installed communicator (RcclComm / TorchComm)
 _SYNCBN = True
@@ -160,8 +158,10 @@ def is_master() -> bool:
 def init_seeds(cuda_deterministic: bool = True):
     """distributed.py:9-21: seed = 1 + rank for python, numpy and torch (CPU and every GPU).
     train.py:12 calls it BEFORE init_dist, so the rank is 0 and every rank seeds 1 (SURVEY.md
-    Appendix A.1).  The cuDNN flags have no counterpart here (no cuDNN on this path); the
-    HIP kernels are deterministic either way (no atomics, fixed reduction orders)."""
+    Appendix A.1).  The cuDNN flags have no counterpart here (no cuDNN on this path).  The
+    FaceVAE step's HIP kernels are deterministic either way (no atomics, fixed reduction
+    orders); the exception is the §8(f)2 warp path: grid_sample3d's backward accumulates the
+    input gradient with fp32 float atomics (warp.hip), whose order is not fixed run to run."""
     seed = 1 + get_rank()
     random.seed(seed)
     np.random.seed(seed)
@@ -304,22 +304,15 @@ class DataParallel(torch.nn.Module):
 
     def _on_grad(self, p):
         bi, off = self._where[id(p)]
-        # conv weight gradients may come from the ops' side stream (ops.wgrad_stream_for): the
-        # bucket copy and the all-reduce launch are then issued there, after everything the
-        # compute stream has issued so far (BN / bias gradients), without stalling it
-        side = _ops.active_side_stream(p.grad.device) if p.grad.is_cuda else None
-        if side is not None:
-            side.wait_stream(torch.cuda.current_stream(p.grad.device))
-        with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
-            flat = self._flat_buf(bi, p.grad)
-            flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
-            if not self._armed:
-                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
-                self._armed = True
-            self._pending[bi] -= 1
-            if self._pending[bi] == 0:
-                self.launch_order.append(bi)
-                self.comm.allreduce_(self._flat[bi], op="avg", wait_back=False)
+        flat = self._flat_buf(bi, p.grad)
+        flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
+        if not self._armed:
+            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+            self._armed = True
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self.launch_order.append(bi)
+            self.comm.allreduce_(self._flat[bi], op="avg", wait_back=False)
 
     def _finish(self):
         for bi, n in enumerate(self._pending):     # params that got no grad this step

@@ -111,12 +111,7 @@ class FaceVAE(_Block):
         if x.is_cuda:
             self._sn_batch().run(self.training)   # all 15 power iterations in 4 launches
             self._wprep_batch().run(x.device)       # the generic weight layouts in one launch
-            ops.begin_forward(x.device)             # weight re-layouts may start from here (aux stream)
-        try:
-            h = self.afe.forward_2d(x)
-            mu, logstd, z = ops.reparameterise(h, eps, self.compute_dtype())
-            y = self.generator.forward_2d(z)
-        finally:
-            if x.is_cuda:
-                ops.end_forward(x.device)
+        h = self.afe.forward_2d(x)
+        mu, logstd, z = ops.reparameterise(h, eps, self.compute_dtype())
+        y = self.generator.forward_2d(z)
         return y, mu, logstd

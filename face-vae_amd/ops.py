@@ -15,7 +15,6 @@ Reference semantics restated here (file:line in Luh1124/face-vae):
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional
 
 import torch
@@ -205,37 +204,6 @@ class SNBatch:
             c._sn_pre = (sigma[i:i + 1], snaps[i][0], snaps[i][1])
 
 
-# Auxiliary stream (FV_AUX_STREAM=1 / 2; off by default): the short kernels off the critical path
-# run on the side stream, as parallel branches of the step -- the weight re-layouts of every
-# conv (they depend only on the weights and the spectral-norm pass at the start of the forward:
-# begin_forward() records that point) and, in backward, the split-K slab reduction and the
-# spectral-norm term of each weight gradient (after the wgrad kernel, which stays in line).
-# The compute stream waits for a conv's prepared weights just before its launch, and for the
-# side stream at the end of backward.  Bit-identical (tests/test_graph_gpu.py), but slower in an
-# alternating on-box A/B of the graph-replayed 256x256, B=32 step: 13.00 ms/step in line, 13.71
-# with the weight preps on the aux stream, 13.44 with the post-processing too (the data
-# gradients overlapped by slab reductions stretch 128 -> 149 us; every conv's cross-stream wait
-# is a cross-queue dependency of the graph).
-_AUX_MODE = int(os.environ.get("FV_AUX_STREAM", "0"))   # 0 off, 1 weight preps, 2 + wgrad post-processing
-_AUX = _AUX_MODE >= 1
-_AUX_BWD = _AUX_MODE >= 2
-_FWD_EVENT = {}
-
-
-def begin_forward(dev):
-    """Mark the compute-stream point the weight preparations of this forward may start from
-    (after the model's spectral-norm pass); FaceVAE.forward calls it, end_forward() clears it."""
-    if _AUX and dev.type == "cuda":
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        _FWD_EVENT[dev.index] = ev
-
-
-def end_forward(dev):
-    _FWD_EVENT.pop(dev.index, None)
-
-
-_WPREP_BATCH = os.environ.get("FV_WPREP_BATCH", "1") != "0"
 WPREP_MAX = 24
 
 
@@ -250,8 +218,6 @@ class WPrepBatch:
         self.convs = list(convs)
 
     def run(self, device):
-        if not _WPREP_BATCH:
-            return
         groups = {}
         for c in self.convs:
             key = getattr(c, "_fv_desc", None)
@@ -309,7 +275,6 @@ class ConvState:
                 self.sigma = spectral_norm_fwd(w, conv.weight_u, conv.weight_v, training)
                 self.u = conv.weight_u.clone()
                 self.v = conv.weight_v.clone()
-        self.ready = None
         self.fp8 = bool(fp8) and bool(query("fv_conv2d_fp8_supported", ctypes.byref(d)))
         if self.fp8:
             conv._fv_desc = conv._fv_prep = None
@@ -326,25 +291,6 @@ class ConvState:
         conv._fv_desc = key                # what the next forward's WPrepBatch prepares
         if pre is not None and pre[0] == key[0] and (pre[2] is not None or not need_wt):
             self.wk, self.wt = pre[1], (pre[2] if need_wt else None)
-            return
-        ev = _FWD_EVENT.get(device.index) if _AUX else None
-        if ev is not None:
-            # on the side stream from the start of the forward; the launch waits for `ready`
-            main = torch.cuda.current_stream(device)
-            side = _side_stream(device)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                self.wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
-                self.wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if need_wt else None
-                call("fv_conv_weight_prep", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
-                     stream())
-                self.ready = torch.cuda.Event()
-                self.ready.record(side)
-            for t in (self.wk, self.wt):
-                if t is not None:
-                    t.record_stream(main)
-            if self.sigma is not None:
-                self.sigma.record_stream(side)
             return
         self.wk = _empty(query("fv_conv_wk_elems", ctypes.byref(d)), dtype, device)
         self.wt = _empty(query("fv_conv_wt_elems", ctypes.byref(d)), dtype, device) if need_wt else None
@@ -363,16 +309,8 @@ def stats_geometry(cs: ConvState):
     return query("fv_conv2d_stats_blocks", d), query("fv_conv2d_stats_block_pixels", d)
 
 
-def wait_weights(cs: ConvState):
-    """Compute stream waits for the conv's weight preparation (aux stream)."""
-    if cs.ready is not None:
-        torch.cuda.current_stream().wait_event(cs.ready)
-        cs.ready = None
-
-
 def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False):
     d = cs.d
-    wait_weights(cs)
     part = None
     if stats:
         nb, _ = stats_geometry(cs)
@@ -392,16 +330,9 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
     return part
 
 
-# store-pass reductions (include/facevae.h, fv_store_reduce); FV_DISABLE_SR=1 keeps the
-# separate BN passes (A/B, and the parity tests of both forms)
-_SR_OFF = os.environ.get("FV_DISABLE_SR", "0") == "1"
-_RES_SR = os.environ.get("FV_RES_SR", "0") == "1"
-
-
+# store-pass reductions (include/facevae.h, fv_store_reduce)
 def sr_records(d, dgrad):
     """(records, pixels per record) of the store-pass reduction of a launch, or None."""
-    if _SR_OFF:
-        return None
     bp = ctypes.c_int(0)
     nrec = query("fv_conv2d_sr_records", ctypes.byref(d), int(dgrad), ctypes.byref(bp))
     return (nrec, bp.value) if nrec > 0 else None
@@ -436,81 +367,7 @@ def _dgrad_bnred(cs, dy, dx, bnred):
     return BNRecords(part, nb, bp, dx)
 
 
-# Weight gradients on a side stream (FV_WGRAD_STREAM=1; off by default): a conv's weight
-# gradient (+ its slab reduce and the spectral-norm backward term) feeds only the optimizer, so
-# it can run on a second HIP stream while the compute stream goes on with the data gradient and
-# the HBM-bound BN backward passes.  The compute stream joins the side stream at the end of
-# backward (an autograd final callback).  Used only when the conv's weight / bias have no .grad
-# yet (AccumulateGrad then stores dw without launching a kernel on the compute stream).
-# Measured at 256x256, B=32 (3 alternating runs each): 14.03 ms/step with it against 13.77 in
-# line.  The weight-gradient grids (252 blocks of 8 waves, 120 VGPRs, 128 KB LDS) hold every CU
-# for their whole 140 us, so the compute stream's kernels cannot co-reside: the BN finalize
-# launches wait 8.6 -> 99.5 us for a slot, the data gradients stretch 129 -> 182 us.
-_WG_SIDE = os.environ.get("FV_WGRAD_STREAM", "0") == "1"
-_SIDE = {}
-_JOIN = {"armed": False, "main": None}
-
-
-def _side_stream(dev):
-    s = _SIDE.get(dev.index)
-    if s is None:
-        s = torch.cuda.Stream(device=dev)
-        _SIDE[dev.index] = s
-    return s
-
-
-def wgrad_stream_for(cs: ConvState, dev):
-    """The side stream the weight gradient of cs runs on, or None (in line)."""
-    if not _WG_SIDE:
-        return None
-    b = cs.conv.bias
-    if cs.w.grad is not None or (b is not None and b.grad is not None):
-        return None
-    return _side_stream(dev)
-
-
-def _join_side():
-    main, side = _JOIN["main"], _JOIN["side"]
-    _JOIN["armed"] = False
-    _JOIN["main"] = None
-    main.wait_stream(side)
-
-
-def _arm_join(main, side):
-    """Make `main` wait for `side` when this backward pass ends (or right away outside one)."""
-    if _JOIN["armed"]:
-        return
-    _JOIN.update(armed=True, main=main, side=side)
-    try:
-        torch.autograd.Variable._execution_engine.queue_callback(_join_side)
-    except RuntimeError:             # not inside a backward pass
-        _join_side()
-
-
-def aux_stream_for(cs: ConvState, dev):
-    """The aux stream for the weight-gradient post-processing of cs, or None (in line)."""
-    if not _AUX_BWD:
-        return None
-    b = cs.conv.bias
-    if cs.w.grad is not None or (b is not None and b.grad is not None):
-        return None
-    return _side_stream(dev)
-
-
-def active_side_stream(dev):
-    """The side stream of a device when gradients may come from it (side-stream wgrads or the
-    aux stream), else None."""
-    return _side_stream(dev) if (_WG_SIDE or _AUX_BWD) else None
-
-
-def side_stream_join(device=None):
-    """Compute stream waits for every weight gradient launched so far (e.g. before reading
-    .grad outside autograd)."""
-    for s in _SIDE.values():
-        torch.cuda.current_stream(device).wait_stream(s)
-
-
-def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db, aux=None, main=None):
+def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db):
     d = cs.d
     dev = dy.device
     slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
@@ -518,24 +375,10 @@ def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db, aux=None, main=None):
     psc, psh = (pro if pro is not None else (None, None))
     _timed("wgrad", d, lambda: call("fv_conv2d_bwd_weight", ctypes.byref(d), ptr(x), ptr(psc), ptr(psh), ptr(dy),
                                     ldd, ptr(slab), ptr(bslab), stream()))
-    if aux is not None:
-        # slab reduce + spectral-norm term on the aux stream, after the wgrad kernel
-        main = torch.cuda.current_stream(dev)
-        aux.wait_stream(main)
-        with torch.cuda.stream(aux):
-            dw, db = _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab, main=main)
-        for t in (slab, bslab, cs.sigma, getattr(cs, "u", None), getattr(cs, "v", None)):
-            if t is not None:
-                t.record_stream(aux)
-        for t in (dw, db):
-            if t is not None:
-                t.record_stream(main)
-        _arm_join(main, aux)
-        return dw, db
-    return _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab, main=main)
+    return _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab)
 
 
-def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab, main=None):
+def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab):
     d = cs.d
     dev = dy.device
     dw = torch.empty_like(cs.w)
@@ -543,18 +386,18 @@ def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab, main=Non
     call("fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(dw), ptr(db), stream())
     if CHECK is not None:
         CHECK("wgrad", cs, x=x, dy=dy, ldd=ldd, dw=dw, db=db, pro=pro)
-    if cs.conv.sn and not (_sn_defer_ok(cs) and _sn_defer(cs, main)):
+    if cs.conv.sn and not (_sn_defer_ok(cs) and _sn_defer(cs)):
         spectral_norm_bwd(cs.w, dw, cs.u, cs.v, cs.sigma)
     return dw, db
 
 
-# Spectral-norm backward terms batched at the end of backward (FV_SN_BWD_BATCH, default on):
+# Spectral-norm backward terms batched at the end of backward:
 # instead of two launches per SN conv (<g, w> partials, then the rank-1 update), one
 # fv_spectral_norm_bwd_multi pair for every SN conv of the backward pass, applied in place to
 # the parameters' .grad from an autograd final callback.  Only in a single process (data-parallel
 # hooks all-reduce each gradient as it is accumulated, so the term must be in it by then) and
 # only for parameters whose .grad was None (AccumulateGrad then holds exactly this gradient).
-_SN_BATCH = os.environ.get("FV_SN_BWD_BATCH", "1") != "0"
+_SN_BATCH = True          # tests/test_graph_gpu.py flips it to compare with the per-conv launches
 _SN_DEFER = {"items": [], "armed": False, "stream": None}
 
 
@@ -574,8 +417,6 @@ def _sn_flush():
     if not layers:
         return
     with torch.cuda.stream(st):
-        for side in _SIDE.values():       # gradients finished on a side stream (aux / wgrad options)
-            st.wait_stream(side)
         for i0 in range(0, len(layers), 24):
             chunk = layers[i0:i0 + 24]
             arr = (L.SnBwdLayer * len(chunk))()
@@ -589,53 +430,27 @@ def _sn_flush():
             call("fv_spectral_norm_bwd_multi", len(chunk), ctypes.addressof(arr), ptr(ws), stream())
 
 
-def _sn_defer(cs: ConvState, main=None) -> bool:
-    """Queue cs's spectral-norm term for the end of this backward pass (applied on the compute
-    stream `main`, default the current one); False (caller applies it now) outside a backward
-    pass."""
+def _sn_defer(cs: ConvState) -> bool:
+    """Queue cs's spectral-norm term for the end of this backward pass (applied on the current
+    compute stream); False (caller applies it now) outside a backward pass."""
     if any(w is cs.w for w, _, _, _ in _SN_DEFER["items"]):
-        raise RuntimeError("spectral-norm backward batching: a conv used twice in one backward pass "
-                           "(set FV_SN_BWD_BATCH=0)")
+        raise RuntimeError("spectral-norm backward batching: a conv used twice in one backward pass")
     if not _SN_DEFER["armed"]:
         try:
             torch.autograd.Variable._execution_engine.queue_callback(_sn_flush)
         except RuntimeError:         # not inside a backward pass
             return False
         _SN_DEFER["armed"] = True
-        _SN_DEFER["stream"] = main if main is not None else torch.cuda.current_stream(cs.w.device)
+        _SN_DEFER["stream"] = torch.cuda.current_stream(cs.w.device)
     _SN_DEFER["items"].append((cs.w, cs.u, cs.v, cs.sigma))
     return True
-
-
-def _wgrad_side(side, cs: ConvState, x, dy, ldd, pro, need_db):
-    """_wgrad on the side stream, ordered after everything issued so far on the compute
-    stream; operands are recorded on the side stream so the allocator keeps them alive."""
-    main = torch.cuda.current_stream(dy.device)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        dw, db = _wgrad(cs, x, dy, ldd, pro, need_db, main=main)
-    for t in (x, dy, cs.sigma, getattr(cs, "u", None), getattr(cs, "v", None)) + tuple(pro or ()):
-        if t is not None:
-            t.record_stream(side)
-    for t in (dw, db):
-        if t is not None:
-            t.record_stream(main)
-    _arm_join(main, side)
-    return dw, db
 
 
 def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=True, bnred=None, want_recs=False):
     """-> (dx at the conv input resolution (upsample folded back), dW (param layout), db
     [, BNRecords or None when want_recs])."""
-    d = cs.d
-    dev = dy.device
-    side = wgrad_stream_for(cs, dev)
-    if side is None:
-        dw, db = _wgrad(cs, x, dy, ldd, pro, need_db, aux=aux_stream_for(cs, dev))
+    dw, db = _wgrad(cs, x, dy, ldd, pro, need_db)
     dx, recs = _dgrad(cs, dy, ldd, need_dx, bnred)
-    if side is not None:
-        # issued after the data gradient, so that kernel reaches the CUs first
-        dw, db = _wgrad_side(side, cs, x, dy, ldd, pro, need_db)
     return (dx, dw, db, recs) if want_recs else (dx, dw, db)
 
 
@@ -777,12 +592,23 @@ def bn_act_forward(y, r: BNResult, slope, pool, bn=None):
     return out
 
 
+def bn_backward_is_local(r: BNResult, comm) -> bool:
+    """True when this BN's backward needs no collective: no communicator, or eval-mode
+    statistics (running mean / var, count 0, no all-reduced record) -- the normalisation is
+    then a fixed per-channel affine map, so dx = gamma * invstd * g on every rank and dgamma /
+    dbeta are this rank's sums (averaged later with the other gradients), exactly as torch's
+    SyncBatchNorm falls back to batch_norm in eval mode (torch/nn/modules/batchnorm.py:790-826)."""
+    return comm is None or (r.count == 0 and r.stats is None)
+
+
 def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True, recs=None):
     """-> (dx of the BN input, dgamma, dbeta).  recs: the BN-backward sums already reduced by
     the dgrad that produced dout (BNRecords), replacing the reduce pass."""
     N, C, H, W = y.shape
     dev = y.device
     dc = L.dtype_code(y.dtype)
+    if bn_backward_is_local(r, comm):
+        comm = None
     ws = _empty(query("fv_bn_ws_bytes", C) // 8, F64, dev)
     dg = torch.empty(C, dtype=F32, device=dev)
     dbt = torch.empty(C, dtype=F32, device=dev)
@@ -940,7 +766,6 @@ class ResBlockFn(torch.autograd.Function):
             # them on)
             part = _empty(geo[0] * 2 * C, F32, x.device)
             sr = L.StoreReduce(1, ptr(part), None, None, None, None, None, 0.0)
-            wait_weights(cs2)
             _timed("fwd", d2, lambda: call("fv_conv2d_fwd_sr", ctypes.byref(d2), ptr(a2), ptr(cs2.wk), ptr(b2),
                                            ptr(xb), ptr(out), ctypes.byref(sr), stream()))
             if CHECK is not None:
@@ -963,13 +788,11 @@ class ResBlockFn(torch.autograd.Function):
         dout = grad_in(dout, xb.dtype)
         # (the BN-backward sums stay a separate pass here: fused into the 256-channel dgrad's
         # store pass they cost that kernel +29 us per launch against the pass's 27 us,
-        # profiles/r2b_*; FV_RES_SR=1 re-enables it for A/B)
-        br2 = (blk.bn2, r2, t1, 0.0) if _RES_SR else None
-        br1 = (blk.bn1, r1, xb, 0.0) if _RES_SR else None
-        da2, dw2, db2, rec2 = conv_backward(cs2, a2, dout, C, bnred=br2, want_recs=True)
-        dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, recs=rec2)
-        da1, dw1, db1, rec1 = conv_backward(cs1, a1, dt1, C, bnred=br1, want_recs=True)
-        dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout, recs=rec1)
+        # profiles/r2b_*)
+        da2, dw2, db2 = conv_backward(cs2, a2, dout, C)
+        dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm)
+        da1, dw1, db1 = conv_backward(cs1, a1, dt1, C)
+        dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout)
         dx = from_nhwc(dxb, x)
         return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None
 

@@ -8,8 +8,9 @@ multi-scale loop (== 2x2 average on even sizes) on the BN/act kernels.
 Same constructor arguments as the reference (layers_weight, n_scale) plus the feature-stack
 weights: the reference downloads them by URL (vgg19-dcbb9e9d.pth, vgg_face_dag.pth,
 losses.py:55-57, 80-82); there is no network here, so pass `vgg19_state_dict` /
-`vggface_state_dict` ({"features.{i}.weight", "features.{i}.bias"}, torchvision numbering) or
-get seeded random stacks (`width_div` narrows them for tests).  forward(input, target) follows
+`vggface_state_dict` ({"features.{i}.weight", "features.{i}.bias"}, torchvision numbering), or
+ask explicitly for seeded random stacks with `random_init=True` (`width_div` narrows them for
+tests); without either the constructor raises.  forward(input, target) follows
 losses.py:131-151 exactly, including the multi-scale loop's reuse of the leaked `layer` /
 `weight` (relu_5_1, 1.0) at every scale.  The target branch is computed without autograd (the
 reference detaches it).  Activations are NHWC in the compute dtype (bf16 in fp8 mode).
@@ -230,10 +231,21 @@ class VGGFeatures(nn.Module):
 class PerceptualLoss(nn.Module):
     """Drop-in for losses.PerceptualLoss (losses.py:123-151); see the module docstring."""
 
-    def __init__(self, layers_weight=None, n_scale=3, vgg19_state_dict=None, vggface_state_dict=None, width_div=1):
+    def __init__(self, layers_weight=None, n_scale=3, vgg19_state_dict=None, vggface_state_dict=None, width_div=1,
+                 random_init=False):
+        """vgg19_state_dict / vggface_state_dict: the pretrained feature stacks (torchvision
+        layout) that the reference downloads by URL (losses.py:55-57, 80-82; unavailable
+        offline).  Both are required unless `random_init=True` explicitly asks for seeded
+        He-normal stand-ins (tests, benchmarks): a perceptual loss over random features is
+        not the reference's loss, so it is never chosen silently."""
         super().__init__()
         self.layers_weight = dict(layers_weight or DEFAULT_WEIGHTS)
         self.n_scale = n_scale
+        missing = [n for n, w in (("vgg19_state_dict", vgg19_state_dict), ("vggface_state_dict", vggface_state_dict))
+                   if w is None]
+        if missing and not random_init:
+            raise ValueError(f"PerceptualLoss: {', '.join(missing)} not given -- pass the pretrained VGG weights "
+                             "(torchvision layout) or random_init=True for seeded random feature stacks")
         w19 = vgg19_state_dict if vgg19_state_dict is not None else random_vgg_state(VGG19_CFG, 19, width_div)
         w16 = vggface_state_dict if vggface_state_dict is not None else random_vgg_state(VGG16_CFG, 16, width_div)
         self.vgg19 = VGGFeatures(VGG19_CFG, VGG19_MAP, self.layers_weight.keys(), w19)

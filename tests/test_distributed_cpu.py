@@ -140,3 +140,21 @@ def test_bucket_plan_faceva_sizes():
     flat = [p for b in bs for p in b]
     assert [id(p) for p in flat] == [id(p) for p in reversed(params)]
     assert bs[0][0] is m.generator.out_conv.bias
+
+
+def test_bn_backward_collective_decision():
+    """under a communicator, an eval-mode BN (running statistics: count 0, no
+    all-reduced record) takes the local backward -- no all-reduce, k = 0 -- as in a single
+    process; training-mode BN keeps the SyncBN path."""
+    import fvamd  # noqa: F401
+    from facevae_amd import ops
+
+    class _R:
+        def __init__(self, count, stats):
+            self.count, self.stats = count, stats
+
+    comm = object()
+    assert ops.bn_backward_is_local(_R(0, None), None)
+    assert ops.bn_backward_is_local(_R(0, None), comm)                  # eval mode under DP
+    assert not ops.bn_backward_is_local(_R(None, torch.zeros(3)), comm)  # SyncBN training
+    assert ops.bn_backward_is_local(_R(128, None), None)                # single-process training

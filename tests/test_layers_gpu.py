@@ -1,5 +1,5 @@
 """Parity at the configurations the benchmark times (BASELINE.json C2: 256x256, B=32, bf16;
-C4: 512x512, B=8), two ways:
+C4: 512x512, B=8; C5's per-GPU shard: 256x256, B=64, bf16 and fp8), two ways:
 
 1. Every conv launch of one real training step (forward, data gradient, weight + bias
    gradient of all 15 convs: every kernel family at its exact B=32 / B=8 launch plan --
@@ -62,8 +62,11 @@ def _gpu_step(cfg, dtype, x, eps, checker=None):
     return init, y.detach().cpu(), R.item(), K.item(), grads, state, checker
 
 
-@pytest.mark.parametrize("H,B", [(256, 32), (512, 8)])
+@pytest.mark.parametrize("H,B", [(256, 32), (512, 8), (256, 64)])
 def test_every_conv_launch_of_the_timed_step(H, B):
+    """B=64 is config C5's per-GPU shard (global batch 512 on 8 GPUs): at that size the weight
+    gradients run their fast path under the real dy-size operand bound (conv.hip plan_wgrad),
+    so every launch plan of the B=64 step is gated here too."""
     cfg = fv.FaceVAEConfig(H=H)
     x, eps = _inputs(B, H)
     *_, chk = _gpu_step(cfg, torch.bfloat16, x, eps, lambda m: LaunchChecker(m, torch.bfloat16))
@@ -76,10 +79,27 @@ def test_every_conv_launch_of_the_timed_step(H, B):
     # 18 BatchNorm layers: forward apply (+ batch statistics), backward sums and data gradient
     assert len({r["layer"] for r in chk.rows if r["kind"] == "bn_fwd"}) == 18
     assert len({r["layer"] for r in chk.rows if r["kind"] == "dgamma"}) == 18
-    gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 5e-3,   # bgrad: dead biases cancel to ~0
+    gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 1e-4,
             "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
-    bad = [r for r in chk.rows if not (r["rel_l2"] <= gate[r["kind"]] and r["worst"] <= 1.0)]
+    bad = [r for r in chk.rows if not (r["rel_l2"] <= _gate(gate, r, cfg) and r["worst"] <= 1.0)]
     assert not bad, bad
+
+
+def _dead_biases(cfg):
+    """Conv biases whose gradient is exactly zero in exact arithmetic: a conv feeding a
+    training-mode BN (CNA blocks, the first conv of each ResBlock).
+    Their computed gradient is pure cancellation noise of sum(dy) over every pixel of the
+    batch, so its rel-L2 against an equally noisy reference grows with the pixel count (B=64:
+    5.6e-3 at AFE.down1); they are gated by the elementwise bound (2^-14 of sum |dy|) only."""
+    ocfg = O.OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent, n_res=cfg.n_res, up_seq=cfg.up_seq)
+    return {s.prefix for s in O.conv_specs(ocfg)
+            if s.block == "cna" or (s.block == "nac" and ".layers.0.layers.2" in s.prefix)}
+
+
+def _gate(gate, r, cfg):
+    if r["kind"] == "bgrad" and r["layer"] in _dead_biases(cfg):
+        return float("inf")
+    return gate[r["kind"]]
 
 
 @pytest.fixture(scope="module")
@@ -156,6 +176,26 @@ def test_bn_eval_mode_matches_oracle():
             assert torch.equal(after[k].cpu(), v.detach().cpu() if v.is_floating_point() else v), k
 
 
+def _fp8_launch_check(B):
+    x, eps = _inputs(B, 256)
+    *_, chk = _gpu_step(fv.FaceVAEConfig(), torch.float8_e4m3fn, x, eps,
+                        lambda m: LaunchChecker(m, torch.float8_e4m3fn))
+    print(f"\n[256x256 B={B} fp8] per-launch deviation\n" + chk.report())
+    kinds = [r["kind"] for r in chk.rows]
+    assert kinds.count("fwd8") == 14 and kinds.count("dgrad8") == 14       # + AFE.down2 (128 -> 256)
+    gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 1e-4, "fwd8": 5e-3, "dgrad8": 5e-3,
+            "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
+    cfg = fv.FaceVAEConfig()
+    bad = [r for r in chk.rows if not (r["rel_l2"] <= _gate(gate, r, cfg) and r["worst"] <= 1.0)]
+    assert not bad, bad
+
+
+def test_fp8_every_conv_launch_b64():
+    """fp8 mode at config C5's per-GPU shard (256x256, B=64): every launch of the step gated
+    as in the B=32 test below (fwd8 / dgrad8 rows on the dequantized e4m3 operands)."""
+    _fp8_launch_check(64)
+
+
 def test_fp8_every_conv_launch_and_step_deviation(oracle_b32):
     """fp8 mode (config C5's conv path) at 256x256, B=32: the 14 eligible convs (ResBlocks,
     Generator.in_conv, AFE.down2) run forward and data gradient on e4m3 operands -- each such launch is
@@ -163,15 +203,7 @@ def test_fp8_every_conv_launch_and_step_deviation(oracle_b32):
     other launch as in bf16 mode; the step's deviation from the fp32 oracle is reported
     (e4m3: 3 mantissa bits, ~2.6e-2 rel-L2 per conv output) and loosely gated."""
     x, eps, oo, og, osd = oracle_b32
-    *_, chk = _gpu_step(fv.FaceVAEConfig(), torch.float8_e4m3fn, x, eps,
-                        lambda m: LaunchChecker(m, torch.float8_e4m3fn))
-    print("\n[256x256 B=32 fp8] per-launch deviation\n" + chk.report())
-    kinds = [r["kind"] for r in chk.rows]
-    assert kinds.count("fwd8") == 14 and kinds.count("dgrad8") == 14       # + AFE.down2 (128 -> 256)
-    gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 5e-3, "fwd8": 5e-3, "dgrad8": 5e-3,
-            "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
-    bad = [r for r in chk.rows if not (r["rel_l2"] <= gate[r["kind"]] and r["worst"] <= 1.0)]
-    assert not bad, bad
+    _fp8_launch_check(32)
     init, y, R, K, grads, state, _ = _gpu_step(fv.FaceVAEConfig(), torch.float8_e4m3fn, x, eps)
     dev = {"image": rel(y, oo["y"]), "R": abs(R - oo["R"].item()) / oo["R"].item(),
            "K": abs(K - oo["K"].item()) / abs(oo["K"].item())}

@@ -26,3 +26,16 @@ def test_perceptual_oracle_matches_reference():
     assert abs(loss.item() - g["loss"].item()) / g["loss"].item() < 1e-6
     d = ((xr.grad.double() - g["d_input"].double()).norm() / g["d_input"].double().norm()).item()
     assert d < 1e-5
+
+
+def test_perceptual_loss_needs_weights_or_explicit_random_init():
+    """the drop-in PerceptualLoss never silently trains against random features."""
+    import pytest
+    import fvamd  # noqa: F401
+    import facevae_amd as fv
+    with pytest.raises(ValueError, match="random_init=True"):
+        fv.PerceptualLoss()
+    with pytest.raises(ValueError, match="vggface_state_dict"):
+        fv.PerceptualLoss(vgg19_state_dict=perceptual_weights(VGG19_CFG, 101))
+    crit = fv.PerceptualLoss(random_init=True, width_div=16)
+    assert crit.vgg19.last > 0 and crit.vggface.last > 0

@@ -1,10 +1,10 @@
-"""Summarise gpurun_out/ab_bench.log (tools/gpu_ab_bench.sh): ms/step per knob setting."""
+"""Summarise gpurun_out/ab.log (tools/gpu.sh ab): ms/step per knob setting."""
 import collections
 import json
 import sys
 
 cur, r = None, collections.defaultdict(list)
-for line in open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ab_bench.log"):
+for line in open(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/ab.log"):
     if line.startswith("=="):
         cur = line[3:].strip()
     elif line.startswith("{") and '"metric"' in line:
