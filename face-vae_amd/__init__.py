@@ -14,7 +14,7 @@ from .models import AFE, FaceVAE, Generator
 from .modules import (Conv2d, ConvBlock2D, ConvBlock3D, ConvTranspose2dELR, DownBlock2D, ResBlock2D, ResBlock3D,
                       SameBlock2D, UpBlock2D)
 from .optim import Adam
-from . import distributed, graph, ops, ops3d, warp
+from . import checkpoint, distributed, graph, ops, ops3d, warp
 from .graph import StepGraph
 
 __all__ = ["FaceVAEConfig", "compute_dtype", "set_compute_dtype", "KLDivergenceLoss", "L1Loss", "PerceptualLoss", "ReconLoss",

@@ -1,9 +1,12 @@
 """Build libfacevae.so for gfx950 with hipcc (in-tree; the .so travels to the GPU box).
 
-    python face-vae_amd/csrc/build.py [--jobs N] [--force]
+    python face-vae_amd/csrc/build.py [--jobs N] [--force] [--diag]
 
 Objects are compiled in parallel into face-vae_amd/csrc/build/ and linked into
 face-vae_amd/libfacevae.so.  Rebuilds only sources newer than their object.
+--diag builds the diagnostic library face-vae_amd/csrc/build_diag/libfacevae_diag.so
+(-DFV_DIAG: in-kernel clock stamps of selected kernels, tools/convbench.py --diag); the
+product never loads it.
 """
 import argparse
 import os
@@ -31,46 +34,50 @@ def _newer(src, obj):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src, force):
-    obj = os.path.join(BUILD, src + ".o")
+def _compile(src, force, build_dir=BUILD, extra=()):
+    obj = os.path.join(build_dir, src + ".o")
     if not force and not _newer(src, obj):
         return obj, None
-    cmd = [HIPCC] + FLAGS + ["-c", os.path.join(HERE, src), "-o", obj]
+    cmd = [HIPCC] + FLAGS + list(extra) + ["-c", os.path.join(HERE, src), "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC] + FLAGS + ["-x", "hip", "-c", os.path.join(HERE, src), "-o", obj]
+        cmd = [HIPCC] + FLAGS + list(extra) + ["-x", "hip", "-c", os.path.join(HERE, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, r.stderr
     return obj, None
 
 
-def build(jobs=None, force=False, verbose=True):
-    os.makedirs(BUILD, exist_ok=True)
+def build(jobs=None, force=False, verbose=True, diag=False):
+    build_dir = BUILD + "_diag" if diag else BUILD
+    out = os.path.join(build_dir, "libfacevae_diag.so") if diag else OUT
+    extra = ["-DFV_DIAG"] if diag else []
+    os.makedirs(build_dir, exist_ok=True)
     jobs = jobs or min(len(SOURCES), os.cpu_count() or 1)
     with ThreadPoolExecutor(jobs) as ex:
-        res = list(ex.map(lambda s: _compile(s, force), SOURCES))
+        res = list(ex.map(lambda s: _compile(s, force, build_dir, extra), SOURCES))
     errs = [e for _, e in res if e]
     if errs:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
     objs = [o for o, _ in res]
-    if force or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT] + objs + \
+    if force or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs + \
               ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stderr)
     if verbose:
-        print("built", OUT)
-    return OUT
+        print("built", out)
+    return out
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--diag", action="store_true")
     a = ap.parse_args()
     try:
-        build(a.jobs, a.force)
+        build(a.jobs, a.force, diag=a.diag)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -23,6 +23,24 @@ namespace {
 
 constexpr int BK = 32;  // k per main-loop step (one bf16 MFMA K, eight f32 MFMA K=4)
 
+// Diagnostic build only (build.py --diag -> libfacevae_diag.so, tools/convbench.py --diag):
+// per-wave shader-clock stamps of the res conv kernel into a device table read back with
+// fv_diag_read.  The production library compiles none of this.
+#ifdef FV_DIAG
+constexpr int DIAG_SLOTS = 8;
+__device__ unsigned long long g_diag[4096 * 8 * DIAG_SLOTS];
+#define FV_DIAG_T(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define FV_DIAG_PUT(slot, val)                                                                     \
+  do {                                                                                             \
+    const unsigned long long v_ = (val);                                                           \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                              \
+      g_diag[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * DIAG_SLOTS + (slot)] = v_; \
+  } while (0)
+#else
+#define FV_DIAG_T(var)
+#define FV_DIAG_PUT(slot, val)
+#endif
+
 struct ConvArgs {
   const void* x;
   const void* w;
@@ -1010,6 +1028,11 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   static_assert(STG * (NSB - 1) + BST + (BN - 16) * 64 < 65536, "weight fragment immediates");
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
 
+  FV_DIAG_T(d_t0);
+#ifdef FV_DIAG
+  const unsigned long long d_r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long d_tw = 0, d_ti = 0;
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % WN, wm = wave / WN;
@@ -1101,6 +1124,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     if (i < nsteps) issue_b(i, i);
   wait_vm<0>();
   __syncthreads();
+  FV_DIAG_T(d_t1);
   int pend = 0;
   if (NSB - 1 < nsteps) {
     issue_b(NSB - 1, NSB - 1);
@@ -1114,12 +1138,17 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     mfma_all(fa0, fb0);
     const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
     if (j + 1 < nsteps) {
+      FV_DIAG_T(d_wa);
       if constexpr (NSB == 2) wait_vm<0>();
       else if (pend == 2 * JB) wait_vm<2 * JB>();
       else wait_vm_dyn(pend);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      FV_DIAG_T(d_wb);
+#ifdef FV_DIAG
+      d_tw += d_wb - d_wa;
+#endif
       if (hn < nch && j == hstep) {
         issue_halo(hn);
         ++hn;
@@ -1131,12 +1160,29 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
         pend = bcnt(j + NSB);
       }
       load_frags(fa0, fb0, 2 * j + 2, bn1);
+#ifdef FV_DIAG
+      d_ti += __builtin_amdgcn_s_memtime() - d_wb;
+#endif
     }
     mfma_all(fa1, fb1);
     bj = bn1;
   }
+  FV_DIAG_T(d_t2);
   __syncthreads();
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+#ifdef FV_DIAG
+  FV_DIAG_T(d_t3);
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  FV_DIAG_PUT(0, d_t0);
+  FV_DIAG_PUT(1, d_t1);
+  FV_DIAG_PUT(2, d_t2);
+  FV_DIAG_PUT(3, d_t3);
+  FV_DIAG_PUT(4, d_tw);
+  FV_DIAG_PUT(5, d_ti);
+  FV_DIAG_PUT(6, d_r0);
+  FV_DIAG_PUT(7, ((unsigned long long)xcc << 32) | (unsigned)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // ----------------------------------------------------------------------------------------
@@ -3554,6 +3600,16 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   }
   return fv_check_launch("conv2d_fwd");
 }
+
+#ifdef FV_DIAG
+// diagnostic build: copy the stamp table (g_diag) to the host
+int fv_diag_read(unsigned long long* host, int n) {
+  const int cap = (int)(sizeof(g_diag) / sizeof(g_diag[0]));
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), (size_t)n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int fv_conv2d_fwd(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
                   const float* pro_scale, const float* pro_shift, const void* res, void* y,

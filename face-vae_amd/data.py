@@ -1,16 +1,27 @@
-"""Frame datasets for the FaceVAE trainer (dataset.py:36-150 of Luh1124/face-vae).
+"""Frame datasets for the FaceVAE trainer (dataset.py:13-193 of Luh1124/face-vae).
 
 `FramesDataset` keeps the reference constructor, directory conventions and item layout:
-`root_dir` holds one folder of PNG frames per video (`<id>#<video>.mp4/`), optionally split
-into `train/` and `test/`; with `id_sampling` the training set is the set of identities and an
-item picks a random video of the identity, then two random frames (sorted indices), returned
-as `(source, driving, source_aug, driving_aug)` float32 CHW arrays in [0, 1]
-(dataset.py:91-129).  Frames are decoded with PIL (skimage is not in this image; for uint8
-PNGs `img_as_float32` is the same division by 255).  The `*_aug` items go through
+`root_dir` holds one folder of PNG frames (or a .gif) per video (`<id>#<video>.mp4`),
+optionally split into `train/` and `test/`; with `id_sampling` the training set is the set of
+identities and an item picks a random video of the identity, then two random frames (sorted
+indices into the folder's `os.listdir` order, dataset.py:102-105), returned as `(source,
+driving, source_aug, driving_aug)` float32 CHW arrays in [0, 1] (dataset.py:91-129); a
+test-split item is the whole video, frames sorted by name (read_video, dataset.py:20-23).
+Frames are decoded with PIL (skimage / imageio are not in this image; for uint8 PNGs
+`img_as_float32` is the same division by 255).  The `*_aug` items go through
 `augmentation.AllAugmentationTransform` with the reference's default parameters (rotation
 30 degrees, perspective (30, 40), colour jitter 0.1, dataset.py:52-57), each frame on its own
 as dataset.py:122-123; they feed the keypoint / contrastive losses, not the FaceVAE path.
 
+`output="uint8"` keeps the item layout as bytes: training items are `(source, driving)` uint8
+CHW arrays (no float conversion, no augmentation in the workers: 4x fewer bytes through the
+DataLoader's worker IPC and collate).  `output="driving_uint8"` is the FaceVAE feed: the item
+is the `driving` frame alone (the same two random draws, so the same frame as the reference
+item's `driving`; `source` is not decoded -- the FaceVAE step never reads it).
+`to_device_frames` turns a collated uint8 batch into the float32 NCHW [0, 1] tensor on the
+GPU -- x / 255 in fp32, bit-identical to img_as_float32 on the CPU.
+
+`PairedDataset` is dataset.py:154-193 (source / driving pairs for animation), and
 `SyntheticFramesDataset` produces VoxCeleb-shaped frames x ~ U[0, 1) deterministically per
 index (the benchmark / test input when no dataset is on disk).
 """
@@ -24,11 +35,49 @@ import numpy as np
 from torch.utils.data import Dataset
 
 
-def _read_frame(path: str) -> np.ndarray:
+def _read_frame_u8(path: str) -> np.ndarray:
+    """HxWx3 uint8 (gray and RGBA frames converted as skimage's gray2rgb / [..., :3] would)."""
     from PIL import Image
     with Image.open(path) as im:
-        a = np.asarray(im.convert("RGB"))
-    return a.astype(np.float32) / 255.0
+        if im.mode != "RGB":
+            im = im.convert("RGB")
+        return np.asarray(im)
+
+
+def _read_frame(path: str) -> np.ndarray:
+    return _read_frame_u8(path).astype(np.float32) / 255.0
+
+
+def _read_gif_u8(path: str) -> np.ndarray:
+    """All frames of a .gif as [T, H, W, 3] uint8 (imageio.mimread + the RGBA -> RGB cut of
+    dataset.py:25-29; here through PIL's frame iterator).  .mp4 needs a video decoder, which
+    this image does not have."""
+    from PIL import Image, ImageSequence
+    with Image.open(path) as im:
+        return np.stack([np.asarray(f.convert("RGB")) for f in ImageSequence.Iterator(im)])
+
+
+def read_video_u8(name: str) -> np.ndarray:
+    """dataset.py:13-34 read_video, as uint8 [T, H, W, 3]: a folder of frames sorted by name, or
+    a .gif."""
+    if os.path.isdir(name):
+        return np.stack([_read_frame_u8(os.path.join(name, f)) for f in sorted(os.listdir(name))])
+    if name.lower().endswith(".gif"):
+        return _read_gif_u8(name)
+    if name.lower().endswith(".mp4"):
+        raise NotImplementedError(f"{name}: .mp4 decoding needs a video decoder (imageio / ffmpeg), "
+                                  "not in this image; extract the frames to a folder")
+    raise ValueError("Unknown file extensions  %s" % name)
+
+
+def to_device_frames(t, device="cuda") -> "torch.Tensor":
+    """A collated batch of frames -> float32 NCHW on `device`: uint8 (output="uint8") is moved
+    as bytes and divided by 255 there; float32 is moved as is."""
+    import torch
+    t = torch.as_tensor(t)
+    if t.dtype == torch.uint8:
+        return t.to(device, non_blocking=True).float().div_(255.0)
+    return t.to(device, non_blocking=True)
 
 
 def _train_test_split(videos: Sequence[str], random_seed: int, test_size: float = 0.2):
@@ -46,7 +95,12 @@ DEFAULT_AUGMENTATION = {
 
 class FramesDataset(Dataset):
     def __init__(self, root_dir: str, frame_shape=(256, 256, 3), id_sampling: bool = True, is_train: bool = True,
-                 random_seed: int = 0, pairs_list: Optional[str] = None, augmentation_params=DEFAULT_AUGMENTATION):
+                 random_seed: int = 0, pairs_list: Optional[str] = None, augmentation_params=DEFAULT_AUGMENTATION,
+                 output: str = "float32"):
+        if output not in ("float32", "uint8", "driving_uint8"):
+            raise ValueError("FramesDataset: output must be 'float32' (reference items), 'uint8' or "
+                             "'driving_uint8' (FaceVAE feed)")
+        self.output = output
         self.root_dir = root_dir
         self.videos = os.listdir(root_dir)
         self.frame_shape = tuple(frame_shape)
@@ -67,13 +121,11 @@ class FramesDataset(Dataset):
         self.videos = train_videos if is_train else test_videos
         self.is_train = is_train
         from .augmentation import AllAugmentationTransform
-        self.transform = AllAugmentationTransform(**(augmentation_params or {})) if is_train else None
+        self.transform = AllAugmentationTransform(**(augmentation_params or {})) \
+            if is_train and output == "float32" else None
 
     def __len__(self):
         return len(self.videos)
-
-    def _frames(self, path):
-        return sorted(os.listdir(path))
 
     def __getitem__(self, idx):
         name = self.videos[idx]
@@ -81,13 +133,26 @@ class FramesDataset(Dataset):
             path = str(np.random.choice(glob.glob(os.path.join(self.root_dir, name + "*.mp4"))))
         else:
             path = os.path.join(self.root_dir, name)
-        if not os.path.isdir(path):
-            raise NotImplementedError("FramesDataset: frame folders only (.mp4/.gif decoding needs imageio, "
-                                      "not in this image)")
-        frames = self._frames(path)
-        if self.is_train:
+        if self.is_train and os.path.isdir(path):
+            # dataset.py:102-105: two sorted random indices into the folder's os.listdir order
+            frames = os.listdir(path)
             fidx = np.sort(np.random.choice(len(frames), replace=True, size=2))
-            arr = [_read_frame(os.path.join(path, frames[i])) for i in fidx]
+            if self.output == "driving_uint8":
+                return np.ascontiguousarray(_read_frame_u8(os.path.join(path, frames[fidx[1]])).transpose(2, 0, 1))
+            arr = [_read_frame_u8(os.path.join(path, frames[i])) for i in fidx]
+        else:
+            video = read_video_u8(path)                # dataset.py:107-110
+            fidx = np.sort(np.random.choice(len(video), replace=True, size=2)) if self.is_train else range(len(video))
+            arr = video[fidx]
+        if self.output == "driving_uint8" and self.is_train:
+            return np.ascontiguousarray(arr[1].transpose(2, 0, 1))
+        if self.output != "float32":
+            if self.is_train:
+                return (np.ascontiguousarray(arr[0].transpose(2, 0, 1)),
+                        np.ascontiguousarray(arr[1].transpose(2, 0, 1)))
+            return np.ascontiguousarray(np.asarray(arr).transpose(3, 0, 1, 2))
+        arr = [a.astype(np.float32) / 255.0 for a in arr]
+        if self.is_train:
             source = np.ascontiguousarray(arr[0].transpose(2, 0, 1))
             driving = np.ascontiguousarray(arr[1].transpose(2, 0, 1))
             if self.transform is None:
@@ -96,7 +161,7 @@ class FramesDataset(Dataset):
             d_aug = np.array(self.transform([arr[1].copy()])[0], dtype=np.float32)
             return (source, driving, np.ascontiguousarray(s_aug.transpose(2, 0, 1)),
                     np.ascontiguousarray(d_aug.transpose(2, 0, 1)))
-        video = np.stack([_read_frame(os.path.join(path, f)) for f in frames])
+        video = np.stack(arr)
         return np.ascontiguousarray(video.transpose(3, 0, 1, 2))
 
 
@@ -112,6 +177,43 @@ class DatasetRepeater(Dataset):
 
     def __getitem__(self, idx):
         return self.dataset[idx % len(self.dataset)]
+
+
+class PairedDataset(Dataset):
+    """dataset.py:154-193: (driving, source) index pairs over an initial dataset -- random
+    distinct pairs (seeded) or the rows of a pairs csv (`source`, `driving` video names)."""
+
+    def __init__(self, initial_dataset, number_of_pairs, seed=0):
+        self.initial_dataset = initial_dataset
+        pairs_list = self.initial_dataset.pairs_list
+        np.random.seed(seed)
+        if pairs_list is None:
+            max_idx = min(number_of_pairs, len(initial_dataset))
+            nx, ny = max_idx, max_idx
+            xy = np.mgrid[:nx, :ny].reshape(2, -1).T
+            number_of_pairs = min(xy.shape[0], number_of_pairs)
+            self.pairs = xy.take(np.random.choice(xy.shape[0], number_of_pairs, replace=False), axis=0)
+        else:
+            import pandas as pd
+            videos = self.initial_dataset.videos
+            name_to_index = {name: index for index, name in enumerate(videos)}
+            pairs = pd.read_csv(pairs_list)
+            pairs = pairs[np.logical_and(pairs["source"].isin(videos), pairs["driving"].isin(videos))]
+            number_of_pairs = min(pairs.shape[0], number_of_pairs)
+            self.pairs = [(name_to_index[pairs["driving"].iloc[i]], name_to_index[pairs["source"].iloc[i]])
+                          for i in range(number_of_pairs)]
+            self.start_frames = []
+
+    def __len__(self):
+        return len(self.pairs)
+
+    def __getitem__(self, idx):
+        pair = self.pairs[idx]
+        first = self.initial_dataset[pair[0]]
+        second = self.initial_dataset[pair[1]]
+        first = {"driving_" + key: value for key, value in first.items()}
+        second = {"source_" + key: value for key, value in second.items()}
+        return {**first, **second}
 
 
 class SyntheticFramesDataset(Dataset):

@@ -19,6 +19,7 @@ import torch.distributed as dist
 
 from . import config as _config
 from . import distributed
+from .data import to_device_frames
 from .losses import KLDivergenceLoss, ReconLoss
 from .models import FaceVAE
 from .optim import Adam
@@ -114,8 +115,10 @@ class FaceVAETrainer:
     def step(self):
         """One epoch over the dataloader (logger.py:135-184)."""
         for idx, batch in enumerate(self.dataloader):
-            s, d, s_a, d_a = batch
-            d = d.cuda(non_blocking=True)
+            # (source, driving, source_aug, driving_aug) float32 items, (source, driving) uint8, or
+            # the driving frames alone (FramesDataset(output="driving_uint8")): the VAE trains on
+            # `driving`
+            d = to_device_frames(batch[1] if isinstance(batch, (list, tuple)) else batch, "cuda")
             out = self.train_step(d, self.sample_eps(d))
             self.log_iter({k: v.detach().float().cpu().numpy() for k, v in out.items() if k != "y"})
         self.log_epoch()

@@ -96,3 +96,120 @@ def test_frames_dataset_items(tmp_path):
     loader = torch.utils.data.DataLoader(rep, batch_size=4, num_workers=2)
     b = next(iter(loader))
     assert [tuple(t.shape) for t in b] == [(4, 3, 64, 64)] * 2 + [(4, 3, 256, 256)] * 2
+
+
+def _tree(tmp_path, H=32, frames=5):
+    from PIL import Image
+    rng = np.random.default_rng(5)
+    for vid in ("id0#a.mp4", "id1#b.mp4"):
+        for split in ("train", "test"):
+            d = tmp_path / split / vid
+            d.mkdir(parents=True)
+            for f in range(frames):
+                Image.fromarray((rng.random((H, H, 3)) * 255).astype(np.uint8)).save(d / f"{f:07d}.png")
+    return tmp_path
+
+
+def test_training_frames_follow_os_listdir_order(tmp_path, monkeypatch):
+    """dataset.py:102-105: the two sorted random indices select from os.listdir(path) as it
+    comes (test items read_video: sorted by name)."""
+    import os
+    from facevae_amd import data as D
+    _tree(tmp_path)
+    real = os.listdir
+    seen = []
+
+    def rev(p):
+        out = real(p)
+        if str(p).endswith(".mp4"):
+            out = sorted(out, reverse=True)        # a directory order that is not name order
+            seen.append(out)
+        return out
+    monkeypatch.setattr(D.os, "listdir", rev)
+    ds = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), id_sampling=False, is_train=True,
+                         augmentation_params=None, output="uint8")
+    np.random.seed(3)
+    s, d = ds[0]
+    np.random.seed(3)
+    fidx = np.sort(np.random.choice(5, replace=True, size=2))
+    frames = seen[-1]
+    path = os.path.join(str(tmp_path), "train", ds.videos[0])
+    assert np.array_equal(s, D._read_frame_u8(os.path.join(path, frames[fidx[0]])).transpose(2, 0, 1))
+    assert np.array_equal(d, D._read_frame_u8(os.path.join(path, frames[fidx[1]])).transpose(2, 0, 1))
+
+
+def test_uint8_feed_matches_float32_items(tmp_path):
+    """output="uint8" + to_device_frames (here on the CPU) gives the float32 frames of the
+    reference layout bit for bit (x / 255 in fp32 = img_as_float32)."""
+    from facevae_amd import data as D
+    _tree(tmp_path)
+    f32 = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), id_sampling=True, is_train=True,
+                          augmentation_params=None)
+    u8 = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), id_sampling=True, is_train=True,
+                         augmentation_params=None, output="uint8")
+    for i in range(2):
+        np.random.seed(10 + i)
+        s, d, _, _ = f32[i]
+        np.random.seed(10 + i)
+        s8, d8 = u8[i]
+        assert s8.dtype == np.uint8 and s8.shape == (3, 32, 32)
+        assert torch.equal(D.to_device_frames(torch.from_numpy(s8), "cpu"), torch.from_numpy(s))
+        assert torch.equal(D.to_device_frames(torch.from_numpy(d8), "cpu"), torch.from_numpy(d))
+    loader = torch.utils.data.DataLoader(DatasetRepeater(u8, 2), batch_size=4, num_workers=2)
+    b = next(iter(loader))
+    assert len(b) == 2 and b[1].dtype == torch.uint8 and tuple(b[1].shape) == (4, 3, 32, 32)
+    ev = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), id_sampling=False, is_train=False, output="uint8")
+    assert ev[0].shape == (3, 5, 32, 32) and ev[0].dtype == np.uint8
+
+
+def test_gif_video_and_paired_dataset(tmp_path):
+    """read_video of a .gif (dataset.py:24-30, PIL frames instead of imageio.mimread) and
+    PairedDataset's seeded pairs (dataset.py:154-193)."""
+    from PIL import Image
+    from facevae_amd import data as D
+    rng = np.random.default_rng(6)
+    frames = [Image.fromarray((rng.random((16, 16, 3)) * 255).astype(np.uint8)).convert("P", palette=Image.ADAPTIVE)
+              for _ in range(4)]
+    p = tmp_path / "v.gif"
+    frames[0].save(p, save_all=True, append_images=frames[1:])
+    v = D.read_video_u8(str(p))
+    assert v.shape == (4, 16, 16, 3) and v.dtype == np.uint8
+    for i, f in enumerate(frames):
+        assert np.array_equal(v[i], np.asarray(f.convert("RGB")))
+    import pytest
+    with pytest.raises(NotImplementedError):
+        D.read_video_u8(str(tmp_path / "x.mp4"))
+
+    class _Init:
+        pairs_list = None
+        videos = ["a", "b", "c"]
+
+        def __len__(self):
+            return 3
+
+        def __getitem__(self, i):
+            return {"video": i}
+    pd_ = D.PairedDataset(_Init(), 5, seed=0)
+    assert len(pd_) == 5
+    item = pd_[0]
+    assert set(item) == {"driving_video", "source_video"}
+    np.random.seed(0)
+    xy = np.mgrid[:3, :3].reshape(2, -1).T
+    ref = xy.take(np.random.choice(9, 5, replace=False), axis=0)
+    assert np.array_equal(np.asarray(pd_.pairs), ref)
+
+
+def test_driving_feed_is_the_reference_driving_frame(tmp_path):
+    """output="driving_uint8": the same two random draws as the reference item, only the
+    driving frame decoded -- equal to the float32 item's `driving` after x / 255."""
+    from facevae_amd import data as D
+    _tree(tmp_path)
+    f32 = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), is_train=True, augmentation_params=None)
+    dv = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), is_train=True, output="driving_uint8")
+    for i in range(2):
+        np.random.seed(20 + i)
+        _, d, _, _ = f32[i]
+        np.random.seed(20 + i)
+        d8 = dv[i]
+        assert d8.dtype == np.uint8 and d8.shape == (3, 32, 32)
+        assert torch.equal(D.to_device_frames(torch.from_numpy(d8), "cpu"), torch.from_numpy(d))

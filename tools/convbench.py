@@ -53,6 +53,36 @@ def timeit(fn, iters):
     return e0.elapsed_time(e1) / iters * 1e3   # us
 
 
+def diag_summary():
+    """Per-wave clock stamps of the last halo-3x3 forward launch (diagnostic library):
+    prologue (entry -> first barrier), main loop (of which: waits + barriers, the post-barrier
+    issue block), epilogue, in shader cycles; the in-kernel clock from s_memtime / s_memrealtime
+    (100 MHz) and the launch span."""
+    n = 4096 * 8 * 8
+    buf = (ctypes.c_ulonglong * n)()
+    lib = L.load()
+    lib.fv_diag_read.restype = ctypes.c_int
+    if lib.fv_diag_read(buf, n) != 0:
+        return None
+    import numpy as np
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+    t = t[t[:, 0] != 0]
+    if len(t) == 0:
+        return None
+    pro, loop, epi = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
+    r0, r3 = t[:, 6], t[:, 7] & 0xffffffff
+    r3 = r0 - (r0 & 0xffffffff) + r3 + np.where(r3 < (r0 & 0xffffffff), 1 << 32, 0)
+    clk = (t[:, 3] - t[:, 0]) / np.maximum(r3 - r0, 1) * 0.1          # GHz
+    span_us = (r3.max() - r0.min()) / 100.0
+    starts = np.sort(np.unique(r0))
+    out = {"waves": int(len(t)), "prologue": int(pro.mean()), "loop": int(loop.mean()), "loop_wait": int(t[:, 4].mean()),
+           "loop_issue": int(t[:, 5].mean()), "epilogue": int(epi.mean()), "clock_ghz": round(float(np.median(clk)), 3),
+           "span_us": round(float(span_us), 1),
+           "wave_life_us": round(float(np.median(r3 - r0)) / 100.0, 1),
+           "start_spread_us": round(float((starts[-1] - starts[0]) / 100.0), 1)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
@@ -61,7 +91,12 @@ def main():
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="")
     ap.add_argument("--dtype", default="bf16", help="bf16 | fp32 | fp8 (fp8 rows added for eligible layers)")
+    ap.add_argument("--diag", action="store_true",
+                    help="load the diagnostic library (build.py --diag) and print the in-kernel clock stamps "
+                         "of the halo 3x3 forward after each layer's forward timing")
     a = ap.parse_args()
+    if a.diag:
+        L.LIB_PATH = os.path.join(ROOT, "face-vae_amd", "csrc", "build_diag", "libfacevae_diag.so")
     fp8 = a.dtype == "fp8"
     dtype = torch.bfloat16 if a.dtype in ("bf16", "fp8") else torch.float32
     kinds = a.only.split(",")
@@ -123,6 +158,8 @@ def main():
                                        None, None, y.data_ptr(), None if nchw else part.data_ptr(), L.stream()),
                         a.iters)
             row["fwd_us"], row["fwd_tf"] = round(us, 1), round(flop / us / 1e6, 1)
+            if a.diag:
+                row["diag_fwd"] = diag_summary()
         dy = (torch.randn(B, ldd, H, H, device="cuda") * 0.1).to(dtype).contiguous(memory_format=CL)
         if "dgrad" in kinds and name != "in7":
             dx = torch.empty(B, cp, H, H, dtype=dtype, device="cuda", memory_format=CL)

@@ -4,8 +4,11 @@ torch DataLoader, with and without the *_aug augmentation, on a synthetic frame 
     python tools/databench.py [--workers 16] [--videos 64] [--frames 8] [--items 512]
 
 Prints one JSON line: items/s and frames/s (an item = source + driving, 2 decoded frames) for
-each mode.  The FaceVAE step consumes `driving` only, so the decode-only rate is
-the one that bounds it; the augmented rate bounds the full GeneratorFull inputs.
+each mode: the FaceVAE feed (FramesDataset(output="driving_uint8"): the driving frame as bytes,
+converted to float32 on the GPU when there is one; images/s), the (source, driving) uint8
+items, the reference's float32 items without and with the *_aug augmentation.  The FaceVAE
+step consumes `driving` only, so the feed rate is the one that bounds it; the
+augmented rate bounds the full GeneratorFull inputs.
 """
 import argparse
 import json
@@ -38,16 +41,25 @@ def make_tree(root, videos, frames, H):
                 Image.fromarray((np.clip(img, 0, 1) * 255).astype(np.uint8)).save(os.path.join(d, f"{f:07d}.png"))
 
 
-def rate(ds, workers, items, batch):
+def rate(ds, workers, items, batch, to_gpu=False):
+    """Items/s out of a DataLoader (shuffled, pinned memory as train.py); to_gpu: each batch's
+    `driving` also goes through to_device_frames (H2D + the uint8 -> float32 division)."""
+    from facevae_amd.data import to_device_frames
     loader = torch.utils.data.DataLoader(DatasetRepeater(ds, 1000), batch_size=batch, num_workers=workers,
-                                         shuffle=True, drop_last=True, persistent_workers=workers > 0)
+                                         shuffle=True, drop_last=True, persistent_workers=workers > 0,
+                                         pin_memory=to_gpu)
     it = iter(loader)
     next(it)                                   # worker start-up
     t0 = time.perf_counter()
     n = 0
     while n < items:
         b = next(it)
-        n += b[0].shape[0]
+        d = b[1] if isinstance(b, (list, tuple)) else b
+        if to_gpu:
+            to_device_frames(d, "cuda")
+        n += d.shape[0]
+    if to_gpu:
+        torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return n / dt
 
@@ -64,6 +76,13 @@ def main():
     with tempfile.TemporaryDirectory() as root:
         make_tree(root, a.videos, a.frames, a.res)
         out = {"workers": a.workers, "res": a.res}
+        gpu = torch.cuda.is_available()
+        feed = FramesDataset(root, frame_shape=(a.res, a.res, 3), output="driving_uint8")
+        r = rate(feed, a.workers, a.items, a.batch, to_gpu=gpu)
+        out.update(facevae_feed_images_per_s=round(r, 1), facevae_feed_to_gpu=gpu)
+        feed = FramesDataset(root, frame_shape=(a.res, a.res, 3), output="uint8")
+        r = rate(feed, a.workers, a.items, a.batch, to_gpu=gpu)
+        out.update(uint8_items_per_s=round(r, 1), uint8_frames_per_s=round(2 * r, 1))
         plain = FramesDataset(root, frame_shape=(a.res, a.res, 3), augmentation_params=None)
         r = rate(plain, a.workers, a.items, a.batch)
         out.update(decode_items_per_s=round(r, 1), decode_frames_per_s=round(2 * r, 1))

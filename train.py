@@ -8,7 +8,8 @@ seeds 1), one process per GPU via mp.spawn, a DistributedSampler over
 DatasetRepeater(FramesDataset(root_dir), 100), and the Logger surface (here FaceVAETrainer:
 .load_cpk(ckp), .step() per epoch).  Extra flags: --synthetic N (N synthetic frames instead
 of a dataset), --config toy|256|512, --backend nccl|gloo (gloo: several ranks on one GPU),
---dump_dir (each rank writes its final state_dict; used by the tests).
+--feed driving_uint8|uint8|float32 (data feed format, see data.py), --dump_dir (each rank writes its final
+state_dict; used by the tests).
 """
 import argparse
 import os
@@ -47,8 +48,12 @@ def main(proc, args):
     if args.synthetic:
         trainset = SyntheticFramesDataset(args.synthetic, cfg.H)
     else:
-        trainset = DatasetRepeater(FramesDataset(root_dir=args.root_dir, frame_shape=(cfg.H, cfg.H, 3)),
-                                   num_repeats=100)
+        # --feed driving_uint8 (default): the driving frame alone leaves the workers as bytes and
+        # becomes float32 [0, 1] on the GPU (bit-identical to the reference's img_as_float32; the
+        # FaceVAE step reads only `driving`, so neither `source` nor the *_aug copies are made);
+        # --feed uint8: (source, driving) bytes; --feed float32: the reference items
+        trainset = DatasetRepeater(FramesDataset(root_dir=args.root_dir, frame_shape=(cfg.H, cfg.H, 3),
+                                                 output=args.feed), num_repeats=100)
     trainsampler = data.distributed.DistributedSampler(trainset, num_replicas=world_size, rank=proc)
     trainloader = data.DataLoader(trainset, batch_size=args.batch_size, num_workers=args.num_workers,
                                   pin_memory=True, sampler=trainsampler)
@@ -91,6 +96,8 @@ def parse(argv=None):
     parser.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     parser.add_argument("--graph", type=str2bool, default=False,
                         help="single GPU: replay each step as one captured HIP graph (FaceVAETrainer(graph=True))")
+    parser.add_argument("--feed", default="driving_uint8", choices=["driving_uint8", "uint8", "float32"],
+                        help="FramesDataset output: uint8 frames converted on the GPU, or the reference's float32 items")
     parser.add_argument("--dump_dir", type=str, default="")
     parser.add_argument("--init", default="ours", choices=["ours", "torch"],
                         help="rendezvous: our init_dist, or a bare torch process group (reference style)")
