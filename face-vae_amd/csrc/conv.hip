@@ -36,9 +36,43 @@ __device__ unsigned long long g_diag[4096 * 8 * DIAG_SLOTS];
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096)                                              \
       g_diag[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * DIAG_SLOTS + (slot)] = v_; \
   } while (0)
+// kernel entry / after the prologue barrier / around each main-loop wait + barrier / after
+// the post-barrier issue block / after the main loop / at the end
+#define FV_DIAG_BEGIN()                                                \
+  FV_DIAG_T(d_t0);                                                     \
+  const unsigned long long d_r0 = __builtin_amdgcn_s_memrealtime();    \
+  unsigned long long d_tw = 0, d_ti = 0, d_wb = 0
+#define FV_DIAG_PROLOGUE() FV_DIAG_T(d_t1)
+#define FV_DIAG_WAIT_BEGIN() FV_DIAG_T(d_wa)
+#define FV_DIAG_WAIT_END()                   \
+  do {                                       \
+    d_wb = __builtin_amdgcn_s_memtime();     \
+    d_tw += d_wb - d_wa;                     \
+  } while (0)
+#define FV_DIAG_ISSUE_END() (d_ti += __builtin_amdgcn_s_memtime() - d_wb)
+#define FV_DIAG_LOOP_END() FV_DIAG_T(d_t2)
+#define FV_DIAG_END()                                                                       \
+  do {                                                                                      \
+    FV_DIAG_T(d_t3);                                                                        \
+    unsigned xcc_;                                                                          \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                     \
+    FV_DIAG_PUT(0, d_t0);                                                                   \
+    FV_DIAG_PUT(1, d_t1);                                                                   \
+    FV_DIAG_PUT(2, d_t2);                                                                   \
+    FV_DIAG_PUT(3, d_t3);                                                                   \
+    FV_DIAG_PUT(4, d_tw);                                                                   \
+    FV_DIAG_PUT(5, d_ti);                                                                   \
+    FV_DIAG_PUT(6, d_r0);                                                                   \
+    FV_DIAG_PUT(7, ((unsigned long long)xcc_ << 32) | (unsigned)__builtin_amdgcn_s_memrealtime()); \
+  } while (0)
 #else
-#define FV_DIAG_T(var)
-#define FV_DIAG_PUT(slot, val)
+#define FV_DIAG_BEGIN()
+#define FV_DIAG_PROLOGUE()
+#define FV_DIAG_WAIT_BEGIN()
+#define FV_DIAG_WAIT_END()
+#define FV_DIAG_ISSUE_END()
+#define FV_DIAG_LOOP_END()
+#define FV_DIAG_END()
 #endif
 
 struct ConvArgs {
@@ -856,6 +890,7 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   constexpr int MAIN = 2 * HALO + NSB * STG, EPI = BM * BN * 2;
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
 
+  FV_DIAG_BEGIN();
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % WN, wm = wave / WN;
@@ -958,6 +993,7 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
     if (i < nsteps) issue_b(i, i);
   wait_vm<0>();
   __syncthreads();
+  FV_DIAG_PROLOGUE();
   int pend = 0;                                 // DMAs this wave issued in the previous step
   if (NSB - 1 < nsteps) {
     issue_b(NSB - 1, NSB - 1);
@@ -977,12 +1013,14 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
     if (j + 1 < nsteps) {
       // the weight stage is issued LAST in a step, so the count left in flight is that
       // stage's alone (a halo issued before it is waited for one step later)
+      FV_DIAG_WAIT_BEGIN();
       if constexpr (NSB == 2) wait_vm<0>();     // stage j + 1 was the one issued last
       else if (pend == 2 * JB) wait_vm<2 * JB>();
       else wait_vm_dyn(pend);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      FV_DIAG_WAIT_END();
       if (hn < nch && j == hstep) {
         issue_halo(hn);
         ++hn;
@@ -994,12 +1032,15 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
         pend = bcnt(j + NSB);
       }
       load_frags(fa0, fb0, 2 * j + 2, bn1);
+      FV_DIAG_ISSUE_END();
     }
     if (two) mfma_all(fa1, fb1);
     bj = bn1;
   }
+  FV_DIAG_LOOP_END();
   __syncthreads();
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+  FV_DIAG_END();
 }
 
 // Linear-halo variant of conv3_halo_fwd2: every LDS fragment address is a per-lane base
@@ -1028,11 +1069,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   static_assert(STG * (NSB - 1) + BST + (BN - 16) * 64 < 65536, "weight fragment immediates");
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
 
-  FV_DIAG_T(d_t0);
-#ifdef FV_DIAG
-  const unsigned long long d_r0 = __builtin_amdgcn_s_memrealtime();
-  unsigned long long d_tw = 0, d_ti = 0;
-#endif
+  FV_DIAG_BEGIN();
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % WN, wm = wave / WN;
@@ -1124,7 +1161,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     if (i < nsteps) issue_b(i, i);
   wait_vm<0>();
   __syncthreads();
-  FV_DIAG_T(d_t1);
+  FV_DIAG_PROLOGUE();
   int pend = 0;
   if (NSB - 1 < nsteps) {
     issue_b(NSB - 1, NSB - 1);
@@ -1138,17 +1175,14 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     mfma_all(fa0, fb0);
     const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
     if (j + 1 < nsteps) {
-      FV_DIAG_T(d_wa);
+      FV_DIAG_WAIT_BEGIN();
       if constexpr (NSB == 2) wait_vm<0>();
       else if (pend == 2 * JB) wait_vm<2 * JB>();
       else wait_vm_dyn(pend);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      FV_DIAG_T(d_wb);
-#ifdef FV_DIAG
-      d_tw += d_wb - d_wa;
-#endif
+      FV_DIAG_WAIT_END();
       if (hn < nch && j == hstep) {
         issue_halo(hn);
         ++hn;
@@ -1160,29 +1194,15 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
         pend = bcnt(j + NSB);
       }
       load_frags(fa0, fb0, 2 * j + 2, bn1);
-#ifdef FV_DIAG
-      d_ti += __builtin_amdgcn_s_memtime() - d_wb;
-#endif
+      FV_DIAG_ISSUE_END();
     }
     mfma_all(fa1, fb1);
     bj = bn1;
   }
-  FV_DIAG_T(d_t2);
+  FV_DIAG_LOOP_END();
   __syncthreads();
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
-#ifdef FV_DIAG
-  FV_DIAG_T(d_t3);
-  unsigned xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  FV_DIAG_PUT(0, d_t0);
-  FV_DIAG_PUT(1, d_t1);
-  FV_DIAG_PUT(2, d_t2);
-  FV_DIAG_PUT(3, d_t3);
-  FV_DIAG_PUT(4, d_tw);
-  FV_DIAG_PUT(5, d_ti);
-  FV_DIAG_PUT(6, d_r0);
-  FV_DIAG_PUT(7, ((unsigned long long)xcc << 32) | (unsigned)__builtin_amdgcn_s_memrealtime());
-#endif
+  FV_DIAG_END();
 }
 
 // ----------------------------------------------------------------------------------------
@@ -3564,7 +3584,14 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // (measured and not kept, r2: the single-tap halo loop -- down2 dgrad 369 vs 324 us,
     // down1 dgrad 433 vs 414 us; a 3-deep weight ring for the 256-channel tiles, 2.5 % slower;
     // 8-row tiles for the 64-channel co tile, 418 -> 420 us; weight-DMA pieces spread between
-    // the MFMA rows as conv_wgrad_v2 does, res conv forward 134 -> 160 us)
+    // the MFMA rows as conv_wgrad_v2 does, res conv forward 134 -> 160 us.  r3, res conv forward
+    // in alternating runs on one box: halo chunks issued after the weight stage and left in
+    // flight one step longer 126 -> 133 us; a ping-pong schedule (waves 4-7 one phase behind,
+    // each wave's fragment reads + DMA issue beside its SIMD partner's MFMAs, 3-stage ring,
+    // 2 barriers per step) 134 -> 142 us; 128 co x 512 px tiles, 25 instead of 40 KB of LDS-DMA
+    // per step, 153 -> 157 (fwd2) / 161 us (ping-pong).  The clock-stamp build (build.py --diag)
+    // puts the step at ~3400 cycles against 2048 of MFMA issue; with the MFMAs removed the
+    // ping-pong loop still took 92 % of its time, with the fragment reads removed 65 %.)
     if (bn >= 128 && a.Cin % 64 == 0) {
       if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
@@ -3608,6 +3635,11 @@ int fv_diag_read(unsigned long long* host, int n) {
   if (n > cap) n = cap;
   if (hipDeviceSynchronize() != hipSuccess) return 1;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_diag), (size_t)n * sizeof(unsigned long long)) == hipSuccess ? 0 : 1;
+}
+int fv_diag_clear(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_diag)) != hipSuccess) return 1;
+  return hipMemset(p, 0, sizeof(g_diag)) == hipSuccess ? 0 : 1;
 }
 #endif
 

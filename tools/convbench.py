@@ -64,6 +64,7 @@ def diag_summary():
     lib.fv_diag_read.restype = ctypes.c_int
     if lib.fv_diag_read(buf, n) != 0:
         return None
+    lib.fv_diag_clear()
     import numpy as np
     t = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
     t = t[t[:, 0] != 0]
@@ -94,9 +95,12 @@ def main():
     ap.add_argument("--diag", action="store_true",
                     help="load the diagnostic library (build.py --diag) and print the in-kernel clock stamps "
                          "of the halo 3x3 forward after each layer's forward timing")
+    ap.add_argument("--lib", default="", help="another build of libfacevae.so (A/B of two builds on one box)")
     a = ap.parse_args()
     if a.diag:
         L.LIB_PATH = os.path.join(ROOT, "face-vae_amd", "csrc", "build_diag", "libfacevae_diag.so")
+    elif a.lib:
+        L.LIB_PATH = os.path.abspath(a.lib)
     fp8 = a.dtype == "fp8"
     dtype = torch.bfloat16 if a.dtype in ("bf16", "fp8") else torch.float32
     kinds = a.only.split(",")
@@ -154,6 +158,8 @@ def main():
                                            wt8.data_ptr(), wdq.data_ptr(), dxf.data_ptr(), L.stream()), a.iters)
                 row["fp8_dgrad_us"], row["fp8_dgrad_tf"] = round(us, 1), round(flop / us / 1e6, 1)
         if "fwd" in kinds:
+            if a.diag:
+                L.load().fv_diag_clear()
             us = timeit(lambda: L.call("fv_conv2d_fwd", ctypes.byref(d), x.data_ptr(), wk.data_ptr(), None, None,
                                        None, None, y.data_ptr(), None if nchw else part.data_ptr(), L.stream()),
                         a.iters)
@@ -163,9 +169,13 @@ def main():
         dy = (torch.randn(B, ldd, H, H, device="cuda") * 0.1).to(dtype).contiguous(memory_format=CL)
         if "dgrad" in kinds and name != "in7":
             dx = torch.empty(B, cp, H, H, dtype=dtype, device="cuda", memory_format=CL)
+            if a.diag:
+                L.load().fv_diag_clear()
             us = timeit(lambda: L.call("fv_conv2d_bwd_data", ctypes.byref(d), dy.data_ptr(), ldd, wt.data_ptr(),
                                        dx.data_ptr(), L.stream()), a.iters)
             row["dgrad_us"], row["dgrad_tf"] = round(us, 1), round(flop / us / 1e6, 1)
+            if a.diag:
+                row["diag_dgrad"] = diag_summary()
         if "wgrad" in kinds:
             slab = torch.empty(L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), device="cuda")
             bslab = torch.empty(L.query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), device="cuda")

@@ -10,7 +10,8 @@
 #   prof            rocprofv3 --kernel-trace --stats of bench.py $BENCH_ARGS     -> gpurun_out/prof_$TAG
 #   pmc             HBM-traffic / MFMA-busy counter passes of bench.py (tools/pmc_collect.py)
 #   convbench       tools/convbench.py $CB_ARGS                                 -> gpurun_out/convbench.log
-#   cbab            alternating convbench runs of $VARIANTS (env strings), $REPS rounds
+#   cbab            alternating convbench runs of $VARIANTS (";"-separated "ENV=.. -- convbench args"
+#                   strings, e.g. "-- --lib face-vae_amd/csrc/build_ab/libfacevae_base.so;"), $REPS rounds
 #   convpmc         SQ stall-anatomy counter passes over tools/convbench.py ($CB_ARGS)
 #   configs         bench lines of the other BASELINE configs on one GPU (512x512 B=8; B=64 bf16 / fp8)
 set -o pipefail
@@ -89,11 +90,14 @@ step_cbab() {
   IFS=';' read -ra VS <<< "$VARIANTS"
   for i in $(seq 1 ${REPS:-2}); do
     for v in "${VS[@]}"; do
+      local envs="${v%%--*}" args=""
+      [[ "$v" == *--* ]] && args="${v#*--}"
       echo "== $v" >> $O/cbab.log
-      env FV_X=0 $v timeout -k 10 200 python tools/convbench.py ${CB_ARGS:-} >> $O/cbab.log 2>&1 || { tail -20 $O/cbab.log; return 1; }
+      env FV_X=0 $envs timeout -k 10 200 python tools/convbench.py ${CB_ARGS:-} $args >> $O/cbab.log 2>&1 \
+        || { tail -20 $O/cbab.log; return 1; }
     done
   done
-  grep -v "amdgpu.ids\|^$" $O/cbab.log | head -120
+  python tools/showbench.py < $O/cbab.log | head -150
 }
 
 step_convpmc() {
