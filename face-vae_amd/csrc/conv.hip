@@ -109,6 +109,7 @@ struct ConvArgs {
   float* sprec;
   const float *bnm, *bni, *bng, *bnb;
   float bns;
+  int wus;        // halo 3x3 kernels: bytes per tap unit of the stage-major weights (rows * 64)
 };
 
 // output pixel of tile-space pixel p (identity unless a sub-pixel phase is set)
@@ -917,23 +918,24 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
     const bool ok = hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
     hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + ((lchk ^ h3swz(hp)) << 3)) * 2) : 0x80000000u;
   }
+  // stage-major weights (weight_prep_body smaj, as conv3_halo_fwd3): piece jb of tap unit u is
+  // the contiguous KB at u * ustep + (co0 + (wave + jb * NW) * 16) * 64
   unsigned wbase[JB];
 #pragma unroll
   for (int j = 0; j < JB; ++j) {
     const int row = (wave + j * NW) * 16 + lrow;
-    wbase[j] = (unsigned)(((co0 + row) * a.Kpad + ((lchk ^ rswz<bf16>(row)) << 3)) * 2);
+    wbase[j] = (unsigned)((co0 + row) * 64 + ((lchk ^ rswz<bf16>(row)) << 4));
   }
+  const unsigned ustep = (unsigned)a.wus;
   const int nch = a.Cin >> 5, ntap = 9 * nch, nsteps = (ntap + 1) >> 1;
   auto issue_b = [&](int j, int buf) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int u = 2 * j + h;
       if (u < ntap) {
-        const int c = u / 9, t = u - c * 9;
         const unsigned Bs = sbase + 2 * HALO + buf * STG + h * BST;
-        const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
 #pragma unroll
-        for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase[jb], k0 * 2);
+        for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase[jb], (unsigned)u * ustep);
       }
     }
   };
@@ -1098,20 +1100,22 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     const bool ok = hp < HP && ch < 4 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
     hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
   }
-  // weight rows of piece jb are row0 + jb * NW * 16 (same chunk swizzle): one base register,
-  // the piece step goes into the scalar offset
-  const unsigned wbase = (unsigned)(((co0 + wave * 16 + lrow) * a.Kpad + ((lchk ^ rswz<bf16>(lrow)) << 3)) * 2);
-  const unsigned wstep = (unsigned)(NW * 16 * a.Kpad * 2);
+  // Weights are stage-major (weight_prep_body smaj): tap unit u = c * 9 + t is a [Cout][32]
+  // block, so the 16 rows of a DMA piece are one contiguous KB (8 whole 128-B lines; the
+  // [co][Kpad] rows made every piece 16 separate 64-B segments).  Piece jb of unit u starts at
+  // u * ustep + (co0 + (wave + jb * NW) * 16) * 64; the lane's source chunk carries the LDS
+  // chunk swizzle.
+  const unsigned wbase = (unsigned)((co0 + wave * 16 + lrow) * 64 + ((lchk ^ rswz<bf16>(lrow)) << 4));
+  const unsigned wstep = (unsigned)(NW * 16 * 64);
+  const unsigned ustep = (unsigned)a.wus;
   const int nch = a.Cin >> 5, nsteps = 9 * nch / 2;
   auto issue_b = [&](int j, int buf) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int u = 2 * j + h;
-      const int c = u / 9, t = u - c * 9;
       const unsigned Bs = sbase + buf * STG + h * BST;
-      const unsigned k0 = (unsigned)((t << a.lgCin) + c * 32);
 #pragma unroll
-      for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, k0 * 2 + jb * wstep);
+      for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, (unsigned)u * ustep + jb * wstep);
     }
   };
   // one weight DMA piece q (0 .. 2 JB - 1) of stage j: tap half q / JB, row piece q % JB
@@ -2632,16 +2636,29 @@ conv_halo_wgrad(HaloWgArgs a) {
 // ----------------------------------------------------------------------------------------
 // weight re-layout (+ 1/sigma) and slab reduction
 // ----------------------------------------------------------------------------------------
+// smaj (the layout conv3_halo_fwd3 reads, h3s_layout): stage-major [u = c * 9 + tap][row][32]
+// with c the 32-channel chunk, so every 16-row DMA piece of a weight stage is one contiguous
+// 1 KB (8 whole 128-B lines) instead of 16 row segments of 64 B.  Requires KS == 3,
+// Kpad == 9 * Cin and Cin % 32 == 0.
 template <typename T>
 __device__ __forceinline__ void weight_prep_body(const float* __restrict__ wp, const float* sigma, T* wk, int rows,
                                                  int Kpad, int cout, int cin_valid, int lgCin, int KS, int K,
-                                                 int transposed, int bid, int nblk) {
+                                                 int transposed, int bid, int nblk, int smaj = 0) {
   // 32-bit index math (a weight image is < 2^31 elements; the 64-bit divisions per element
   // dominated the batched launch)
   const int total = rows * Kpad;
   const float inv = sigma ? 1.f / sigma[0] : 1.f;
   for (int e = bid * (int)blockDim.x + threadIdx.x; e < total; e += nblk * (int)blockDim.x) {
-    const int row = e / Kpad, k = e - row * Kpad;
+    int row, k;
+    if (smaj) {
+      const int q = e >> 5, u = q / rows;
+      row = q - u * rows;
+      const int c = u / 9, t = u - c * 9;
+      k = (t << lgCin) + c * 32 + (e & 31);
+    } else {
+      row = e / Kpad;
+      k = e - row * Kpad;
+    }
     float v = 0.f;
     if (k < K) {
       const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
@@ -2660,19 +2677,20 @@ __device__ __forceinline__ void weight_prep_body(const float* __restrict__ wp, c
 template <typename T>
 __global__ void weight_prep_kernel(const float* __restrict__ wp, const float* sigma, T* wk,
                                    int rows, int Kpad, int cout, int cin_valid, int lgCin, int KS,
-                                   int K, int transposed) {
-  weight_prep_body<T>(wp, sigma, wk, rows, Kpad, cout, cin_valid, lgCin, KS, K, transposed, blockIdx.x, gridDim.x);
+                                   int K, int transposed, int smaj) {
+  weight_prep_body<T>(wp, sigma, wk, rows, Kpad, cout, cin_valid, lgCin, KS, K, transposed, blockIdx.x, gridDim.x,
+                      smaj);
 }
 
 // both layouts in one launch: blocks [0, nb1) write wk, the rest wt
-struct WPrepJob { void* out; int rows, Kpad, lgCin, K, transposed, nb; };
+struct WPrepJob { void* out; int rows, Kpad, lgCin, K, transposed, nb, smaj; };
 template <typename T>
 __global__ void weight_prep2_kernel(const float* __restrict__ wp, const float* sigma, int cout, int cin_valid, int KS,
                                     WPrepJob j0, WPrepJob j1) {
   const bool second = (int)blockIdx.x >= j0.nb;
   const WPrepJob& j = second ? j1 : j0;
   weight_prep_body<T>(wp, sigma, (T*)j.out, j.rows, j.Kpad, cout, cin_valid, j.lgCin, KS, j.K, j.transposed,
-                      second ? blockIdx.x - j0.nb : blockIdx.x, j.nb);
+                      second ? blockIdx.x - j0.nb : blockIdx.x, j.nb, j.smaj);
 }
 
 // one launch for the generic weight layouts of many convs (fv_conv_weight_prep_multi): job j
@@ -2681,7 +2699,7 @@ struct WPrepMJob {
   const float* w;
   const float* sigma;
   void* out;
-  int rows, Kpad, lgCin, K, transposed, nb, cout, cin_valid, KS, blk0;
+  int rows, Kpad, lgCin, K, transposed, nb, cout, cin_valid, KS, blk0, smaj;
 };
 struct WPrepMulti {
   int n;
@@ -2694,7 +2712,7 @@ __global__ void weight_prep_multi_kernel(WPrepMulti m) {
   const WPrepMJob& j = m.j[blockIdx.y];
   if ((int)blockIdx.x >= j.nb) return;
   weight_prep_body<T>(j.w, j.sigma, (T*)j.out, j.rows, j.Kpad, j.cout, j.cin_valid, j.lgCin, j.KS, j.K, j.transposed,
-                      blockIdx.x, j.nb);
+                      blockIdx.x, j.nb, j.smaj);
 }
 
 // sub-pixel phase weights of an upsample + 3x3 conv: for phase (pa, pb) the 2x2 tap (r', s')
@@ -3376,6 +3394,26 @@ int fv_conv2d_stats_blocks(const fv_conv_desc* d) {
   return fv_cdiv((long)d->n * d->h * d->w, stats_record_pixels(d));
 }
 
+static fv_conv_desc dgrad_desc(const fv_conv_desc* d);
+
+// the launch of forward-conv descriptor fd runs a halo 3x3 kernel (conv_run's halo3 branch:
+// conv3_halo_fwd3 / fwd2), whose weights are prepared stage-major (weight_prep_body smaj) with
+// wk_rows(fd) rows per tap unit
+static bool h3s_layout(const fv_conv_desc* fd) {
+  return !use_c7n(fd) && !halo_tr(fd) && !use_subpix(fd) && halo3_bn(fd) != 0;
+}
+static int wk_rows(const fv_conv_desc* fd) {
+  const FwdTile t = fwd_tile(fd->cout);
+  return fv_cdiv(fd->cout, t.bn) * t.bn;
+}
+// ... for the forward weights (wk) and the data gradient's transposed weights (wt) of conv d
+static int smaj_wk(const fv_conv_desc* d) { return h3s_layout(d) ? 1 : 0; }
+static int smaj_wt(const fv_conv_desc* d) {
+  if (use_dgrad_lowres(d)) return 0;
+  const fv_conv_desc t = dgrad_desc(d);
+  return h3s_layout(&t) ? 1 : 0;
+}
+
 int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma, void* wk,
                         void* wt, void* stream) {
   int st = check_desc(d);
@@ -3388,8 +3426,10 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     // the common case: forward and transposed layouts in one launch
     const FwdTile tk = fwd_tile(d->cout), tt = fwd_tile(d->cin);
     const int cin_t = pad_pow2_8(d->cout);
-    WPrepJob j0{wk, fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin), ks * ks * d->cin, 0, 0};
-    WPrepJob j1{wt, fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t), ks * ks * cin_t, 1, 0};
+    WPrepJob j0{wk, fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin), ks * ks * d->cin, 0, 0,
+                smaj_wk(d)};
+    WPrepJob j1{wt, fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t), ks * ks * cin_t, 1, 0,
+                smaj_wt(d)};
     j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 4096);
     j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 4096);
     if (d->dtype == FV_BF16)
@@ -3418,10 +3458,10 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     if (d->dtype == FV_BF16)
       hipLaunchKernelGGL(weight_prep_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wk,
-                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0);
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0, smaj_wk(d));
     else
       hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(nb), dim3(256), 0, s, w_param, sigma, (float*)wk,
-                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0);
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0, 0);
     if ((st = fv_check_launch("weight_prep"))) return st;
   }
   if (wt && use_dgrad_lowres(d)) {
@@ -3441,10 +3481,10 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     if (d->dtype == FV_BF16)
       hipLaunchKernelGGL(weight_prep_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wt,
-                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(cin_t), ks, ks * ks * cin_t, 1);
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(cin_t), ks, ks * ks * cin_t, 1, smaj_wt(d));
     else
       hipLaunchKernelGGL(weight_prep_kernel<float>, dim3(nb), dim3(256), 0, s, w_param, sigma, (float*)wt,
-                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(cin_t), ks, ks * ks * cin_t, 1);
+                         rows, Kp, d->cout, d->cin_valid, fv_ilog2(cin_t), ks, ks * ks * cin_t, 1, 0);
     if ((st = fv_check_launch("weight_prep_t"))) return st;
   }
   return FV_OK;
@@ -3471,7 +3511,7 @@ int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* con
     const int ks = d->ksize;
     const FwdTile tk = fwd_tile(d->cout);
     WPrepMJob j0{w_params[i], sigmas[i], wks[i], fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin),
-                 ks * ks * d->cin, 0, 0, d->cout, d->cin_valid, ks, 0};
+                 ks * ks * d->cin, 0, 0, d->cout, d->cin_valid, ks, 0, smaj_wk(d)};
     j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 256);
     nb_total = std::max(nb_total, j0.nb);
     m.j[m.n++] = j0;
@@ -3479,7 +3519,7 @@ int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* con
       const FwdTile tt = fwd_tile(d->cin);
       const int cin_t = pad_pow2_8(d->cout);
       WPrepMJob j1{w_params[i], sigmas[i], wts[i], fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t),
-                   ks * ks * cin_t, 1, 0, d->cout, d->cin_valid, ks, 0};
+                   ks * ks * cin_t, 1, 0, d->cout, d->cin_valid, ks, 0, smaj_wt(d)};
       j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 256);
       nb_total = std::max(nb_total, j1.nb);
       m.j[m.n++] = j1;
@@ -3575,6 +3615,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   if (const int bn = halo3_bn(d)) {
     FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");
     a.lgtw = 6;
+    a.wus = wk_rows(d) * 64;
     a.ntn = d->cout / bn;
     const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
@@ -3591,7 +3632,11 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // 2 barriers per step) 134 -> 142 us; 128 co x 512 px tiles, 25 instead of 40 KB of LDS-DMA
     // per step, 153 -> 157 (fwd2) / 161 us (ping-pong).  The clock-stamp build (build.py --diag)
     // puts the step at ~3400 cycles against 2048 of MFMA issue; with the MFMAs removed the
-    // ping-pong loop still took 92 % of its time, with the fragment reads removed 65 %.)
+    // ping-pong loop still took 92 % of its time, with the fragment reads removed 65 %.
+    // Stage-major weights (every DMA piece one contiguous KB, weight_prep_body smaj): res
+    // fwd / dgrad 127 / 121.5 -> 122 / 117 us, down2 dgrad 317 -> 301 us (kept).  The weights
+    // off the LDS-DMA path -- each wave's A fragments loaded to registers two / one taps ahead,
+    // the halo register-staged, one barrier per 32-channel chunk: 126 -> 134 us (not kept).)
     if (bn >= 128 && a.Cin % 64 == 0) {
       if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);

@@ -41,6 +41,12 @@ def check_state(sd, ref, cfg, steps, tol):
             assert torch.equal(a, v), k
         elif k in dead:
             assert (a - v).abs().max().item() <= 2 * cfg.lr * steps + 1e-7, k
+        elif k.endswith(".running_mean"):
+            # the batch mean of a conv output carries that conv's (dead) bias, which Adam moves
+            # by up to ±lr per step in a rounding-noise direction (above); the running mean takes
+            # momentum (0.1) of it per step: |delta| <= 0.1 * 2 * lr * steps on top of rel < tol
+            # (seen at 2.5e-5 relative on another host CPU's summation order)
+            assert rel(a, v) < tol or (a - v).abs().max().item() <= 0.2 * cfg.lr * steps + 1e-7, k
         else:
             assert rel(a, v) < tol, k
 
@@ -139,8 +145,15 @@ def test_block_cases(name):
     assert rel(y, c["y"]) < 1e-6
     (y * c["gy"]).sum().backward()
     assert rel(x.grad, c["gx"]) < 1e-5
+    gscale = max(gr.abs().max().item() for gr in c["grads"].values())
     for k, gr in c["grads"].items():
-        assert rel(sdp["m." + k].grad, gr) < 1e-5, k
+        g = sdp["m." + k].grad
+        if gr.abs().max().item() < 1e-4 * gscale:
+            # a conv bias feeding a training-mode BN (dead_bias_keys): its gradient is rounding
+            # noise whose digits follow the host CPU's summation order -- absolute bound only
+            assert (g - gr).abs().max().item() <= 1e-4 * gscale, k
+        else:
+            assert rel(g, gr) < 1e-5, k
     for k, v in c["state"].items():
         if v.is_floating_point():
             assert rel(sdp["m." + k].detach(), v) < 1e-6, k
