@@ -1362,6 +1362,180 @@ conv_halo_fwd(ConvArgs a, unsigned x_bytes) {
 }
 
 // ----------------------------------------------------------------------------------------
+// conv7c4_fwd: 7x7, <= 4 valid input channels (stored as 8) -> 64 output channels:
+// AFE.in_conv 3 -> 64 forward (models.py:932) and Generator.out_conv's data gradient (3 -> 64).
+// conv_halo_fwd<7, 8, ...> pads K to 49 taps x 8 channels = 416 (62 % zeros) and restages the
+// 54 KB weight image in every one of its 8192 blocks (the LDS-DMA of the weights, not the
+// MFMAs, set its 153-191 us).  Here:
+//  * K packs 2 taps x 4 channels per 16-B fragment chunk: k = r * 32 + s * 4 + ci (s = 7 and
+//    ci >= cin_valid are zero weights), K = 7 x 32 = 224 -> 7 MFMA k-steps instead of 13; the
+//    A fragment of lane (pixel i, chunk g) is halo pixels (i + 2g, i + 2g + 1) of row r, 8 B
+//    each (two ds_read_b64 from the 16-B NHWC pixels);
+//  * persistent blocks (2 per CU): the 64 x 224 weight image is staged ONCE per block, the
+//    halos of the next two tiles are in flight (3-buffer ring) while the current one computes;
+//  * a minimal epilogue (bias preloaded, NHWC bf16 stores widened to 16 B), so no load in the
+//    loop waits behind the halo DMA; ONE BN (sum, sum^2) record per 256-pixel tile (the 8
+//    waves' partials summed through LDS after the tile's barrier: 4.2 MB of records instead
+//    of 33.5 MB of scattered 32-B stores).
+// Tile: 4 rows x 64 columns x 64 co; wave w owns pixels [32w, 32w + 32) x all 64 co.
+// ----------------------------------------------------------------------------------------
+constexpr int C74_TR = 4, C74_HW = 71, C74_HR = C74_TR + 6;          // halo row: 64 + 6 + 1 (zero) px
+constexpr int C74_K = 224, C74_WROW = C74_K / 8 + 1;                 // 16-B chunks per LDS weight row
+constexpr int C74_WQ = (64 * C74_WROW + 63) / 64;                    // 1-KB weight pieces
+constexpr int C74_HQ = (C74_HR * C74_HW + 63) / 64;                  // 1-KB halo pieces (16 B / px)
+__global__ void __launch_bounds__(512, 4)
+conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
+  constexpr int WB = C74_WQ * 1024, HB = C74_HQ * 1024, NHB = 3;   // 3-deep halo ring
+  constexpr int SB = 8 * 2 * 64 * 4;                                 // per-wave BN partials of a tile
+  __shared__ __attribute__((aligned(1024))) char smem[WB + NHB * HB + 2 * SB];
+  float* const sred = reinterpret_cast<float*>(smem + WB + NHB * HB);   // [2 tiles][wave][2][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, g = lane >> 4;
+  const int tiles_w = a.W >> 6, tiles_h = a.H / C74_TR;
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
+
+  // halo pieces of this wave (pixel L = q * 64 + lane of the 10 x 71 halo, 16 B each)
+  auto issue_halo = [&](int tile, int buf) {
+    const int n = tile / (tiles_h * tiles_w), rem = tile - n * tiles_h * tiles_w;
+    const int h0 = (rem / tiles_w) * C74_TR, w0 = (rem % tiles_w) * 64;
+    for (int q = wave; q < C74_HQ; q += 8) {
+      const int L = q * 64 + lane;
+      const int hr = L / C74_HW, hc = L - (L / C74_HW) * C74_HW;
+      const int hh = h0 + hr - 3, ww = w0 + hc - 3;
+      const bool ok = L < C74_HR * C74_HW && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+      dma16s(xr, sbase + WB + buf * HB + q * 1024, ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * 8) * 2) : 0x80000000u, 0u);
+    }
+  };
+  for (int q = wave; q < C74_WQ; q += 8) {
+    const int L = q * 64 + lane;
+    const int row = L / C74_WROW, ch = L - (L / C74_WROW) * C74_WROW;
+    const bool ok = row < 64 && ch < C74_K / 8;
+    dma16s(wr, sbase + q * 1024, ok ? (unsigned)((row * C74_K + ch * 8) * 2) : 0x80000000u, 0u);
+  }
+  int tile = blockIdx.x;
+  if (tile < ntiles) issue_halo(tile, 0);
+  if (tile + (int)gridDim.x < ntiles) issue_halo(tile + gridDim.x, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  float bv[4][4];
+#pragma unroll
+  for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[nn][i] = a.bias ? a.bias[nn * 16 + g * 4 + i] : 0.f;
+  // halo pixel of this lane's output pixel (tap (0, 0)) per m-tile; the tile is 4 rows x 64
+  int hbase[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int loc = wave * 32 + m * 16 + li;
+    hbase[m] = (loc >> 6) * C74_HW + (loc & 63);
+  }
+  int buf = 0, it = 0;
+  for (; tile < ntiles; tile += gridDim.x, ++it) {
+    // BN record of the previous tile: its 8 waves' partials (published by the last barrier),
+    // summed in wave order by 128 threads -> one [2][64] record per tile (256 pixels)
+    if (a.stats && it > 0 && tid < 128) {
+      const float* sp = sred + ((it - 1) & 1) * (SB / 4) + tid;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += sp[w * 128];
+      a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
+    }
+    // the halo two tiles ahead goes into the buffer the previous tile released at its barrier
+    const int ahead = tile + 2 * gridDim.x;
+    if (ahead < ntiles) issue_halo(ahead, buf == 0 ? 2 : buf - 1);
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc[nn][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* hs = smem + WB + buf * HB;
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+      bf16x8 bfr[4], afr[2];
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+        bfr[nn] = *reinterpret_cast<const bf16x8*>(smem + ((nn * 16 + li) * C74_WROW + r * 4 + g) * 16);
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const char* p = hs + (hbase[m] + r * C74_HW + 2 * g) * 16;
+        const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 16);
+        afr[m] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) acc[nn][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nn], afr[m], acc[nn][m], 0, 0, 0);
+    }
+    // epilogue: bias, BN records (one per 32-pixel wave row, as conv_epilogue), NHWC stores
+    const int n = tile / (tiles_h * tiles_w), rem = tile - n * tiles_h * tiles_w;
+    const int p0 = (n * a.H + (rem / tiles_w) * C74_TR) * a.W + (rem % tiles_w) * 64;
+#pragma unroll
+    for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[nn][m][i] += bv[nn][i];
+    if (a.stats) {
+      float* sw = sred + (it & 1) * (SB / 4) + wave * 128;
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn) {
+        float sv[4], qv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v0 = acc[nn][0][i], v1 = acc[nn][1][i];
+          sv[i] = row16_sum(v0 + v1);
+          qv[i] = row16_sum(v0 * v0 + v1 * v1);
+        }
+        const int ii = li & 3;
+        const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
+        const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
+        const float val = li < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
+        if (li < 8) sw[(li >> 2) * 64 + nn * 16 + g * 4 + ii] = val;
+      }
+    }
+    // 16-B stores (the guide's T21 widening, 16-lane rows): lane (li, g) holds channels
+    // nt * 16 + g * 4 .. + 3 of every n-tile nt; one v_permlane16_swap per dword of an n-tile
+    // pair (2q, 2q + 1) leaves lane g with the 8 contiguous channels (2q + (g & 1)) * 16 +
+    // (g >> 1) * 8 .. + 7: 4 dwordx4 stores per lane and tile instead of 8 dwordx2
+    auto pk = [](float lo, float hi) {
+      const bf16 t[2] = {(bf16)lo, (bf16)hi};
+      return *reinterpret_cast<const unsigned*>(t);
+    };
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int loc = wave * 32 + m * 16 + li;
+      bf16* yp = reinterpret_cast<bf16*>(a.y) + (long)(p0 + (loc >> 6) * a.W + (loc & 63)) * a.ldy;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const f32x4 va = acc[2 * q][m], vb = acc[2 * q + 1][m];
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pk(va[0], va[1]), pk(vb[0], vb[1]), false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pk(va[2], va[3]), pk(vb[2], vb[3]), false, false);
+        *reinterpret_cast<uint4*>(yp + (2 * q + (g & 1)) * 16 + (g >> 1) * 8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+    // the next tile's halo was issued a whole tile earlier; younger than it are the previous
+    // tile's >= 4 stores, this tile's DMA (if any) and this tile's >= 4 stores, so vmcnt(8)
+    // has it landed (in-order counting); the barrier publishes it to all waves and releases
+    // this tile's buffer (raw barrier: __syncthreads() would also drain the stores)
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+  if (a.stats && it > 0 && tid < 128) {
+    const float* sp = sred + ((it - 1) & 1) * (SB / 4) + tid;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += sp[w * 128];
+    a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // 7x7 conv with a 64-channel input and <= 4 output channels (Generator.out_conv 64 -> 3,
 // models.py:1099 + sigmoid 1110), "column taps in N": for every input pixel w' of a row the
 // block computes D[h][w'][(co, s)] = sum_{r, ci} x[h + r - 3][w'][ci] * W[co][ci][r][s]
@@ -2636,7 +2810,8 @@ conv_halo_wgrad(HaloWgArgs a) {
 // ----------------------------------------------------------------------------------------
 // weight re-layout (+ 1/sigma) and slab reduction
 // ----------------------------------------------------------------------------------------
-// smaj (the layout conv3_halo_fwd3 reads, h3s_layout): stage-major [u = c * 9 + tap][row][32]
+// smaj 2: the packed 7x7 layout of conv7c4_fwd ([row][224], 2 taps x 4 channels per 16 B).
+// smaj 1 (the layout conv3_halo_fwd3 reads, h3s_layout): stage-major [u = c * 9 + tap][row][32]
 // with c the 32-channel chunk, so every 16-row DMA piece of a weight stage is one contiguous
 // 1 KB (8 whole 128-B lines) instead of 16 row segments of 64 B.  Requires KS == 3,
 // Kpad == 9 * Cin and Cin % 32 == 0.
@@ -2650,18 +2825,31 @@ __device__ __forceinline__ void weight_prep_body(const float* __restrict__ wp, c
   const float inv = sigma ? 1.f / sigma[0] : 1.f;
   for (int e = bid * (int)blockDim.x + threadIdx.x; e < total; e += nblk * (int)blockDim.x) {
     int row, k;
-    if (smaj) {
-      const int q = e >> 5, u = q / rows;
-      row = q - u * rows;
-      const int c = u / 9, t = u - c * 9;
-      k = (t << lgCin) + c * 32 + (e & 31);
+    bool kin;
+    int tap, c;
+    if (smaj == 2) {            // conv7c4_fwd: [row][224], k = r * 32 + s * 4 + ci (s = 7: zero)
+      row = e / C74_K;
+      k = e - row * C74_K;
+      const int sk = (k >> 2) & 7;
+      kin = sk < 7;
+      tap = (k >> 5) * 7 + sk;
+      c = k & 3;
     } else {
-      row = e / Kpad;
-      k = e - row * Kpad;
+      if (smaj) {
+        const int q = e >> 5, u = q / rows;
+        row = q - u * rows;
+        const int cc = u / 9, t = u - cc * 9;
+        k = (t << lgCin) + cc * 32 + (e & 31);
+      } else {
+        row = e / Kpad;
+        k = e - row * Kpad;
+      }
+      kin = k < K;
+      tap = k >> lgCin;
+      c = k & ((1 << lgCin) - 1);
     }
     float v = 0.f;
-    if (k < K) {
-      const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
+    if (kin) {
       const int r = tap / KS, s = tap - (tap / KS) * KS;
       if (!transposed) {        // wk[co][(r,s,ci)] = W[co][ci][r][s]
         if (row < cout && c < cin_valid) v = wp[(((long)row * cin_valid + c) * KS + r) * KS + s];
@@ -3365,6 +3553,11 @@ static int halo_tr(const fv_conv_desc* d) {
   return tr;
 }
 
+// the launch of forward-conv descriptor fd runs conv7c4_fwd (packed 7x7 weights, smaj 2)
+static bool use_c74(const fv_conv_desc* fd) {
+  return halo_tr(fd) == 4 && fd->cin == 8 && fd->cin_valid <= 4 && fd->cout == 64 && fd->ldy == 64 &&
+         !fd->epi_sigmoid && !fd->out_nchw_f32;
+}
 static FwdTile plan_tile(const fv_conv_desc* d) {
   const int tr = halo_tr(d);
   if (tr) return {d->cout <= 16 ? 16 : 64, tr * 64};
@@ -3374,6 +3567,7 @@ static FwdTile plan_tile(const fv_conv_desc* d) {
 // pixels per BN-statistics record = the pixels of one wave row of the tile (BM / WM)
 static int stats_record_pixels(const fv_conv_desc* d) {
   if (use_c7n(d)) return 64;                                  // one 64-pixel row segment
+  if (use_c74(d)) return C74_TR * 64;                         // one record per tile
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
   const FwdTile t = plan_tile(d);
   if (const int bn = halo3_bn(d)) return bn == 256 ? 128 : 64;   // RM * 16 pixels per wave row
@@ -3406,13 +3600,16 @@ static int wk_rows(const fv_conv_desc* fd) {
   const FwdTile t = fwd_tile(fd->cout);
   return fv_cdiv(fd->cout, t.bn) * t.bn;
 }
+static int lay_of(const fv_conv_desc* fd) { return use_c74(fd) ? 2 : h3s_layout(fd) ? 1 : 0; }
 // ... for the forward weights (wk) and the data gradient's transposed weights (wt) of conv d
-static int smaj_wk(const fv_conv_desc* d) { return h3s_layout(d) ? 1 : 0; }
+static int smaj_wk(const fv_conv_desc* d) { return lay_of(d); }
 static int smaj_wt(const fv_conv_desc* d) {
   if (use_dgrad_lowres(d)) return 0;
   const fv_conv_desc t = dgrad_desc(d);
-  return h3s_layout(&t) ? 1 : 0;
+  return lay_of(&t);
 }
+// row length of a prepared image: the packed 7x7 layout's rows are C74_K long
+static int kpad_lay(int lay, int kpad) { return lay == 2 ? C74_K : kpad; }
 
 int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float* sigma, void* wk,
                         void* wt, void* stream) {
@@ -3426,10 +3623,10 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     // the common case: forward and transposed layouts in one launch
     const FwdTile tk = fwd_tile(d->cout), tt = fwd_tile(d->cin);
     const int cin_t = pad_pow2_8(d->cout);
-    WPrepJob j0{wk, fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin), ks * ks * d->cin, 0, 0,
-                smaj_wk(d)};
-    WPrepJob j1{wt, fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t), ks * ks * cin_t, 1, 0,
-                smaj_wt(d)};
+    WPrepJob j0{wk, fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_lay(smaj_wk(d), kpad_of(ks, d->cin)), fv_ilog2(d->cin),
+                ks * ks * d->cin, 0, 0, smaj_wk(d)};
+    WPrepJob j1{wt, fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_lay(smaj_wt(d), kpad_of(ks, cin_t)), fv_ilog2(cin_t),
+                ks * ks * cin_t, 1, 0, smaj_wt(d)};
     j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 4096);
     j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 4096);
     if (d->dtype == FV_BF16)
@@ -3453,7 +3650,7 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     if ((st = fv_check_launch("weight_prep_subpix"))) return st;
   } else if (wk) {
     const FwdTile t = fwd_tile(d->cout);
-    const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_of(ks, d->cin);
+    const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_lay(smaj_wk(d), kpad_of(ks, d->cin));
     const long tot = (long)rows * Kp;
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     if (d->dtype == FV_BF16)
@@ -3476,7 +3673,7 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   } else if (wt) {
     const int cin_t = pad_pow2_8(d->cout);
     const FwdTile t = fwd_tile(d->cin);
-    const int rows = fv_cdiv(d->cin, t.bn) * t.bn, Kp = kpad_of(ks, cin_t);
+    const int rows = fv_cdiv(d->cin, t.bn) * t.bn, Kp = kpad_lay(smaj_wt(d), kpad_of(ks, cin_t));
     const long tot = (long)rows * Kp;
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     if (d->dtype == FV_BF16)
@@ -3510,7 +3707,8 @@ int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* con
     FV_REQUIRE(w_params[i] && wks[i], "weight_prep_multi: null pointer (conv %d)", i);
     const int ks = d->ksize;
     const FwdTile tk = fwd_tile(d->cout);
-    WPrepMJob j0{w_params[i], sigmas[i], wks[i], fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_of(ks, d->cin), fv_ilog2(d->cin),
+    WPrepMJob j0{w_params[i], sigmas[i], wks[i], fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_lay(smaj_wk(d), kpad_of(ks, d->cin)),
+                 fv_ilog2(d->cin),
                  ks * ks * d->cin, 0, 0, d->cout, d->cin_valid, ks, 0, smaj_wk(d)};
     j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 256);
     nb_total = std::max(nb_total, j0.nb);
@@ -3518,7 +3716,8 @@ int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* con
     if (wts[i]) {
       const FwdTile tt = fwd_tile(d->cin);
       const int cin_t = pad_pow2_8(d->cout);
-      WPrepMJob j1{w_params[i], sigmas[i], wts[i], fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_of(ks, cin_t), fv_ilog2(cin_t),
+      WPrepMJob j1{w_params[i], sigmas[i], wts[i], fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_lay(smaj_wt(d), kpad_of(ks, cin_t)),
+                   fv_ilog2(cin_t),
                    ks * ks * cin_t, 1, 0, d->cout, d->cin_valid, ks, 0, smaj_wt(d)};
       j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 256);
       nb_total = std::max(nb_total, j1.nb);
@@ -3581,6 +3780,13 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     const int nblk = d->n * (d->h / band) * (d->w / 64);
     hipLaunchKernelGGL(conv7_n3_fwd2, dim3(nblk), dim3(512), 0, s, a, xb, band);
     return fv_check_launch("conv2d_fwd_c7n2");
+  }
+  if (use_c74(d)) {
+    FV_REQUIRE(!res, "packed 7x7 conv: no residual");
+    const int ntiles = d->n * (d->h / C74_TR) * (d->w / 64);
+    const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
+    hipLaunchKernelGGL(conv7c4_fwd, dim3(std::min(ntiles, 512)), dim3(512), 0, s, a, xb, ntiles);
+    return fv_check_launch("conv2d_fwd_c74");
   }
   if (const int tr = halo_tr(d)) {
     a.lgtw = 6;
