@@ -133,9 +133,7 @@ def pmc_counters(cfg, B, dtype, fam, avg_ms):
                     "algorithmic_bytes": 2 * (B * cfg.latent_hw ** 2 * cfg.up_seq[0] * 2) + cfg.up_seq[0] ** 2 * 9 * 2})
     if "mfma_busy_frac" in dom:
         out.update({"mfma_busy_counter": round(dom["mfma_busy_frac"], 4),
-                    "eff_clock_ghz": round(dom["eff_clock_ghz"], 3) if dom.get("eff_clock_ghz") else None,
-                    "mfma_busy_counter_step": round(d["step"]["mfma_busy_frac_all_kernels"], 4)
-                    if d.get("step") else None})
+                    "eff_clock_ghz": round(dom["eff_clock_ghz"], 3) if dom.get("eff_clock_ghz") else None})
     return out
 
 

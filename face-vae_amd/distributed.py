@@ -42,6 +42,17 @@ import torch.distributed as dist
 
 _COMM = None          # installed communicator (RcclComm / TorchComm)
 _SYNCBN = True
+_SEGMENTS = None      # graph.SegmentRecorder while a multi-process step is being captured
+
+
+def _deferred(op):
+    """Inside a segmented capture (graph.StepGraph at world > 1) a collective is not issued: it
+    ends the current graph segment and is recorded as `op`, which the replay runs eagerly
+    between the segments.  Returns True when the call was deferred."""
+    if _SEGMENTS is None:
+        return False
+    _SEGMENTS.cut(op)
+    return True
 
 FIRST_BUCKET_MB = 1.0   # torch/nn/parallel/distributed.py _DEFAULT_FIRST_BUCKET_BYTES
 
@@ -79,17 +90,23 @@ class RcclComm:
     def allreduce_(self, t: torch.Tensor, op: str = "sum", wait_back: bool = True):
         """In-place all-reduce (op "sum" or "avg") on the comm stream; with wait_back the
         caller's stream waits for it (SyncBN), otherwise the caller fences later (buckets)."""
+        if _deferred(lambda: self.allreduce_(t, op, wait_back)):
+            return t
         L = self._L
         return self._launch(lambda s: L.call("fv_comm_allreduce", self._h, t.data_ptr(), t.numel(),
                                              L.dtype_code(t.dtype), 1 if op == "avg" else 0, s), t, wait_back)
 
     def broadcast_(self, t: torch.Tensor, root: int = 0, wait_back: bool = True):
+        if _deferred(lambda: self.broadcast_(t, root, wait_back)):
+            return t
         L = self._L
         return self._launch(lambda s: L.call("fv_comm_broadcast", self._h, t.data_ptr(), t.numel(),
                                              L.dtype_code(t.dtype), root, s), t, wait_back)
 
     def fence(self, device=None):
         """Make the caller's stream wait for every collective issued so far."""
+        if _deferred(lambda: self.fence(device)):
+            return
         torch.cuda.current_stream(device).wait_stream(self.stream)
 
     def destroy(self):
@@ -107,12 +124,16 @@ class TorchComm:
         self.world_size = dist.get_world_size(group)
 
     def allreduce_(self, t, op="sum", wait_back=True):
+        if _deferred(lambda: self.allreduce_(t, op, wait_back)):
+            return t
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         if op == "avg":
             t.div_(self.world_size)
         return t
 
     def broadcast_(self, t, root=0, wait_back=True):
+        if _deferred(lambda: self.broadcast_(t, root, wait_back)):
+            return t
         dist.broadcast(t, src=root, group=self.group)
         return t
 

@@ -16,7 +16,16 @@ hipGraphLaunch.  Everything the step does on the host is frozen into the graph a
 
 Inputs are static tensors: the caller refreshes them in place (`copy_`) between replays.
 Outputs are the tensors the step function returned during capture (overwritten by every
-replay).  Single process only: RCCL collectives (DataParallel, SyncBN) stay on the eager path.
+replay).
+
+Several processes (world > 1: DataParallel bucket all-reduces, SyncBN statistics and backward
+sums): the step is captured as SEGMENTS.  Every collective (and the comm-stream fence before
+the optimizer) ends the current segment instead of being issued (`distributed._deferred`); the
+replay runs segment 0, the first collective eagerly on its recorded tensor, segment 1, ... --
+~40 graph launches and the collectives, instead of ~400 ctypes launches per step.  All segments
+share one private memory pool and are replayed in capture order, so a tensor a segment writes
+and the next collective reads keeps its address.  Collectives themselves are never captured
+(an RCCL call inside a capture is not relied on).
 """
 from __future__ import annotations
 
@@ -25,6 +34,48 @@ from typing import Callable, Sequence
 import torch
 
 from . import _lib as L
+
+
+def _detached(out):
+    """Step outputs without their autograd graphs (tensors detached, containers rebuilt)."""
+    if isinstance(out, torch.Tensor):
+        return out.detach()
+    if isinstance(out, dict):
+        return {k: _detached(v) for k, v in out.items()}
+    if isinstance(out, (list, tuple)):
+        return type(out)(_detached(v) for v in out)
+    return out
+
+
+class SegmentRecorder:
+    """Graph segments of one captured step and the eager operations between them."""
+
+    def __init__(self):
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs = []
+        self.ops = []
+
+    def begin(self):
+        # relaxed: the backward's collectives (SyncBN sums, gradient buckets) run on the autograd
+        # engine's device thread, so a segment is ended (and the next begun) on another thread
+        # than the one that began the capture -- allowed only for relaxed-mode captures
+        g = torch.cuda.CUDAGraph()
+        g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+        self.graphs.append(g)
+
+    def cut(self, op):
+        self.graphs[-1].capture_end()
+        self.ops.append(op)
+        self.begin()
+
+    def end(self):
+        self.graphs[-1].capture_end()
+
+    def replay(self):
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.ops):
+                self.ops[i]()
 
 
 class StepGraph:
@@ -42,9 +93,8 @@ class StepGraph:
     def capture(self, before_capture: Callable = None):
         """Run `warmup` eager steps (real training steps) on a side stream, then capture one
         (`before_capture()` runs in between, e.g. to arm a kernel timer)."""
-        if torch.distributed.is_available() and torch.distributed.is_initialized() \
-                and torch.distributed.get_world_size() > 1:
-            raise RuntimeError("StepGraph: single-process steps only (collectives stay eager)")
+        from . import distributed as D
+        segmented = D.get_comm() is not None and D.get_comm().world_size > 1
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
@@ -52,7 +102,11 @@ class StepGraph:
             for i in range(self.warmup):
                 if i == self.warmup - 1:
                     L.staging.begin_record()
-                self.warm_out = self.step_fn()     # the last warm-up step's outputs (it trained)
+                # the last warm-up step's outputs (it trained), detached: a live graph of the
+                # warm-up step would keep its AccumulateGrad nodes -- bound to the warm-up stream
+                # -- for the captured backward, whose gradient hooks would then run on that stream
+                # (a fork the segmented capture cannot end a segment across)
+                self.warm_out = _detached(self.step_fn())
         cur.wait_stream(side)
         torch.cuda.synchronize()
         for o in self.optimizers:
@@ -60,10 +114,26 @@ class StepGraph:
         if before_capture is not None:
             before_capture()
         self._bufs = L.staging.begin_capture()
-        self.graph = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(self.graph):
-                self.out = self.step_fn()
+            if segmented:
+                rec = SegmentRecorder()
+                cap = torch.cuda.Stream()
+                cap.wait_stream(cur)
+                torch.cuda.synchronize()
+                D._SEGMENTS = rec
+                try:
+                    with torch.cuda.stream(cap):
+                        rec.begin()
+                        self.out = self.step_fn()
+                        rec.end()
+                finally:
+                    D._SEGMENTS = None
+                cur.wait_stream(cap)
+                self.graph = rec
+            else:
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph):
+                    self.out = self.step_fn()
         finally:
             L.staging.end()
         if L.staging.i != len(self._bufs):

@@ -62,10 +62,11 @@ class FaceVAETrainer:
         self.kl, self.recon = KLDivergenceLoss(), ReconLoss()
         self.weights = {"R": self.cfg.w_R, "K": self.cfg.w_K}
         self._eps_gen = None
-        # graph=True (single process): train_step replays one captured HIP graph per batch shape
-        # (graph.StepGraph); the batch is copied into static input buffers first.  A batch of
-        # another shape (e.g. the last, smaller one) runs eagerly.
-        self.graph = bool(graph) and self.ddp is None
+        # graph=True: train_step replays one captured HIP graph per batch shape (graph.StepGraph;
+        # under DataParallel the graph segments between the collectives); the batch is copied
+        # into static input buffers first.  A batch of another shape (e.g. the last, smaller
+        # one, the same on every rank) runs eagerly.
+        self.graph = bool(graph)
         self._sg = None
 
     # ---------------------------------------------------------------- one iteration

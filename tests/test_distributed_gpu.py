@@ -261,3 +261,96 @@ def test_dataparallel_eval_mode_backward_is_local():
         (y * g.cuda()).sum().backward()
         assert _rel(y_r, y.detach().cpu()) < 1e-6
         assert _rel(gx, xs.grad.cpu()) < 1e-5
+
+
+def _graph_worker(rank, port, q, dtype_name):
+    """Rank of the segmented-capture test: model A steps once eagerly, is captured as graph
+    segments (every SyncBN / bucket collective and the pre-optimizer fence a segment boundary)
+    and replayed twice; model B, the same initial weights, takes three eager steps.  Same
+    collectives in the same order on both ranks."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import fvamd  # noqa: F401
+        import facevae_amd as fv
+        D = fv.distributed
+        torch.cuda.set_device(0)
+        comm = D.TorchComm()
+        D.install(comm, syncbn=True)
+        dtype = getattr(torch, dtype_name)
+        cfg = fv.FaceVAEConfig.toy()
+        x, eps = _inputs(cfg.H, cfg.latent, cfg.latent_hw)
+        sl = slice(PER_RANK * rank, PER_RANK * (rank + 1))
+        xs, es = x[sl].cuda(), eps[sl].cuda()
+        runs = {}
+        for mode in ("graph", "eager"):
+            torch.manual_seed(10 + rank)
+            m = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(dtype)
+            dp = D.DataParallel(m, comm)
+            opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
+            losses = []
+
+            def step():
+                opt.zero_grad(set_to_none=True)
+                y, mu, logstd = dp(xs, es)
+                loss = cfg.w_R * fv.ReconLoss()((xs, y)) + cfg.w_K * fv.KLDivergenceLoss()((mu, logstd))
+                loss.backward()
+                opt.step()
+                return loss
+
+            if mode == "graph":
+                sg = fv.StepGraph(step, [opt], warmup=1).capture()
+                nseg = len(sg.graph.graphs)
+                losses.append(sg.warm_out.item())
+                for _ in range(2):
+                    losses.append(sg.replay().item())
+            else:
+                nseg = 0
+                for _ in range(3):
+                    losses.append(step().item())
+            torch.cuda.synchronize()
+            runs[mode] = (losses, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}, nseg)
+        buf = io.BytesIO()
+        torch.save((rank, runs["graph"][0], runs["eager"][0], runs["graph"][1], runs["eager"][1], runs["graph"][2]),
+                   buf)
+        q.put(buf.getvalue())
+    except Exception as e:
+        buf = io.BytesIO()
+        torch.save((rank, repr(e), None, None, None, None), buf)
+        q.put(buf.getvalue())
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype_name", ["float32", "bfloat16"])
+def test_dataparallel_segmented_graph_matches_eager(dtype_name):
+    """the world > 1 step captured as graph segments between its collectives
+    (graph.StepGraph) trains exactly as the eager DataParallel + SyncBN step: 3 steps (1 eager
+    warm-up + 2 replays) vs 3 eager steps from the same weights, on both ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_graph_worker, args=(r, port, q, dtype_name)) for r in range(WORLD)]
+    for p in ps:
+        p.start()
+    out = sorted([torch.load(io.BytesIO(q.get(timeout=240)), weights_only=True) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in out:
+        assert r[2] is not None, f"rank {r[0]} failed: {r[1]}"
+    for p in ps:
+        assert p.exitcode == 0
+    for rank, lg, le, sdg, sde, nseg in out:
+        # SyncBN forward + backward all-reduces per BN, the bucket all-reduces and the fence
+        assert nseg > 10, nseg
+        for a, b in zip(lg, le):
+            assert abs(a - b) <= 1e-6 * abs(b), (rank, lg, le)
+        for k in sde:
+            if sde[k].is_floating_point():
+                assert _rel(sdg[k], sde[k]) < 1e-6, (rank, k)
+            else:
+                assert torch.equal(sdg[k], sde[k]), (rank, k)

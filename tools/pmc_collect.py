@@ -22,12 +22,16 @@ import json
 import re
 
 # bench family -> (kernel-name pattern, total grid size in work-items) of the 256->256 res conv
-# at 64x64, B=32 (bench.py's dominant kernel)
+# at 64x64, B=32 (bench.py's dominant kernel).  Forward and data gradient run the same kernel
+# on the same grid: a step dispatches it 13 times in the forward (Generator.in_conv + 12 res
+# convs), then 13 times in the backward, so in dispatch order launch i is a forward launch when
+# (i // FWD_PER_STEP) is even.
 DOMS = {
     "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2>"), 512 * 512),
     "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2>"), 512 * 512),
     "wgrad": (re.compile(r"conv_wgrad_v2<3, 256, 256, 2, 4, 64, 2, false, false>"), 252 * 512),
 }
+FWD_PER_STEP = 13
 RES_FLOP = 2.0 * 32 * 64 * 64 * 256 * 256 * 9     # one res-conv launch, B=32 (154.6 GFLOP)
 SIMDS = 1024
 XCDS = 8
@@ -38,33 +42,56 @@ def family(name):
     return (m.group(1) + (m.group(2) or "")) if m else name[:60]
 
 
-def dom_of(name, grid):
-    return [f for f, (pat, g) in DOMS.items() if pat.search(name) and grid == g]
+def dom_of(name, grid, k):
+    """Dominant families of a dispatch; k = its index among the dispatches of the same kernel
+    and grid (dispatch order) separates the forward from the data-gradient launches."""
+    fams = [f for f, (pat, g) in DOMS.items() if pat.search(name) and grid == g]
+    if "fwd" in fams and "dgrad" in fams:
+        fams = ["fwd" if (k // FWD_PER_STEP) % 2 == 0 else "dgrad"]
+    return fams
+
+
+def _rows(paths, key):
+    """CSV rows sorted by dispatch order, each with its index among same-kernel, same-grid rows"""
+    rows = [r for p in paths for r in csv.DictReader(open(p))]
+    rows.sort(key=lambda r: int(r.get(key) or 0))
+    seen = collections.Counter()
+    for r in rows:
+        grid = int(r.get("Grid_Size", 0) or r.get("Grid_Size_X", 0) or 0)
+        k = (r["Kernel_Name"], grid)
+        yield r, grid, seen[k]
+        seen[k] += 1
 
 
 def counters(dirs):
-    """(family, counter) -> [values], ('dom:'+fam, counter) -> [values]"""
+    """(family, counter) -> [values], ('dom:'+fam, counter) -> [values]; each pass directory
+    is its own run, so dispatch order is counted per pass and per counter"""
     out = collections.defaultdict(list)
     for d in dirs:
-        for p in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-            for r in csv.DictReader(open(p)):
+        paths = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+        rows = [r for p in paths for r in csv.DictReader(open(p))]
+        for c in sorted({r["Counter_Name"] for r in rows}):
+            sub = [r for r in rows if r["Counter_Name"] == c]
+            sub.sort(key=lambda r: int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0))
+            seen = collections.Counter()
+            for r in sub:
+                grid = int(r.get("Grid_Size", 0) or 0)
                 v = float(r["Counter_Value"])
-                c = r["Counter_Name"]
                 out[(family(r["Kernel_Name"]), c)].append(v)
-                for f in dom_of(r["Kernel_Name"], int(r.get("Grid_Size", 0) or 0)):
+                for f in dom_of(r["Kernel_Name"], grid, seen[(r["Kernel_Name"], grid)]):
                     out[("dom:" + f, c)].append(v)
+                seen[(r["Kernel_Name"], grid)] += 1
     return out
 
 
 def durations(d):
     out = collections.defaultdict(list)
-    for p in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
-        for r in csv.DictReader(open(p)):
-            ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            grid = int(r.get("Grid_Size", 0) or r.get("Grid_Size_X", 0) or 0)
-            out[family(r["Kernel_Name"])].append(ns)
-            for f in dom_of(r["Kernel_Name"], grid):
-                out["dom:" + f].append(ns)
+    paths = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)
+    for r, grid, k in _rows(paths, "Start_Timestamp"):
+        ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        out[family(r["Kernel_Name"])].append(ns)
+        for f in dom_of(r["Kernel_Name"], grid, k):
+            out["dom:" + f].append(ns)
     return out
 
 
@@ -120,8 +147,12 @@ def main():
         tot_gui += gsum
         tot_ns += sum(dur.get(k, []))
     if tot_gui:
+        # GRBM_GUI_ACTIVE over-counts dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md, DVFS
+        # give-back): the all-kernel figure is biased by the step's ~150 short launches, so it
+        # is reported with that caveat and bench.py does not quote it
         out["step"] = {"mfma_busy_frac_all_kernels": tot_busy / (tot_gui / XCDS * SIMDS),
-                       "eff_clock_ghz_all_kernels": (tot_gui / XCDS) / tot_ns if tot_ns else None}
+                       "eff_clock_ghz_all_kernels": (tot_gui / XCDS) / tot_ns if tot_ns else None,
+                       "caveat": "short-dispatch bias of GRBM_GUI_ACTIVE; read the per-family records"}
     print(json.dumps(out, indent=1))
 
 

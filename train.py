@@ -58,7 +58,7 @@ def main(proc, args):
     trainloader = data.DataLoader(trainset, batch_size=args.batch_size, num_workers=args.num_workers,
                                   pin_memory=True, sampler=trainsampler)
     logger = fv.FaceVAETrainer(args.ckp_dir, args.vis_dir, trainloader, args.lr, log_file_name=args.log_file,
-                               cfg=cfg, graph=args.graph and world_size == 1)
+                               cfg=cfg, graph=args.graph)
     if args.ckp > 0:
         logger.load_cpk(args.ckp)
     for _ in range(args.num_epochs):
@@ -95,7 +95,8 @@ def parse(argv=None):
     parser.add_argument("--config", default="256", choices=["toy", "256", "512"])
     parser.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     parser.add_argument("--graph", type=str2bool, default=False,
-                        help="single GPU: replay each step as one captured HIP graph (FaceVAETrainer(graph=True))")
+                        help="replay each step as a captured HIP graph (FaceVAETrainer(graph=True); several GPUs: graph "
+                             "segments between the collectives)")
     parser.add_argument("--feed", default="driving_uint8", choices=["driving_uint8", "uint8", "float32"],
                         help="FramesDataset output: uint8 frames converted on the GPU, or the reference's float32 items")
     parser.add_argument("--dump_dir", type=str, default="")
