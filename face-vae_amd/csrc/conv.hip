@@ -3117,6 +3117,7 @@ int halo3_bn(const fv_conv_desc* d) {
   if (d->cout % 256 == 0) return 256;
   // AFE.down1's forward (64 -> 128 channels, K = 576): conv_fwd_v2's 128 x 256 tile measured
   // 500 us against 543 (pipelined halo) / 579 (single-tap halo) at 256x256, B=32
+  // (r3, stage-major weights: still 527 vs 503 us in alternating convbench runs)
   if (d->cin == 64 && d->cout == 128) return 0;
   return d->cout % 128 == 0 ? 128 : d->cout % 64 == 0 ? 64 : 0;
 }
