@@ -110,6 +110,7 @@ struct ConvArgs {
   const float *bnm, *bni, *bng, *bnb;
   float bns;
   int wus;        // halo 3x3 kernels: bytes per tap unit of the stage-major weights (rows * 64)
+  unsigned* roll; // fp8: the operand's delayed-scaling site, rolled by block 0 (fp8_site_roll)
 };
 
 // output pixel of tile-space pixel p (identity unless a sub-pixel phase is set)
@@ -4410,6 +4411,77 @@ __global__ void __launch_bounds__(256) quantize_fp8_kernel(const T* __restrict__
   }
 }
 
+// ---- delayed scaling (per operand site: a conv's activation or output-gradient operand) ----
+// site = uint32[FP8_SITE]: [0, 16) amax history (float bits), [16] amax of the call in flight
+// (float bits, atomicMax: deterministic, max is order-free), [17] history write index, [18] dq
+// of the call in flight.  A call quantizes with s = pow2 scale of max(history) in ONE pass
+// (values beyond 448 / s saturate, as delayed scaling does) and accumulates its own amax; the
+// conv consuming the operand moves that amax into the history (fp8_site_roll, block 0 at its
+// start: every quantize block has finished by then and only dq is read concurrently).  The
+// site's first call quantizes exactly (amax pass + quantize pass) and fills the history.
+constexpr int FP8_SITE = 32, FP8_HIST = 16;
+__device__ __forceinline__ float site_hist_max(const unsigned* st) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < FP8_HIST; ++i) m = fmaxf(m, __uint_as_float(st[i]));
+  return m;
+}
+__device__ __forceinline__ void fp8_site_roll(unsigned* st) {
+  const unsigned p = st[17] % FP8_HIST;
+  st[p] = st[16];
+  st[16] = 0u;
+  st[17] = p + 1;
+}
+// exact first call: fills the whole history with this call's amax
+__global__ void fp8_site_seed_kernel(const float* part, int np, unsigned* st) {
+  __shared__ float sh[4];
+  const float m = amax_of_parts(part, np, sh);
+  if (threadIdx.x < FP8_HIST) st[threadIdx.x] = __float_as_uint(m);
+  if (threadIdx.x == 0) {
+    st[16] = 0u;
+    st[17] = 0u;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) quantize_fp8_delayed_kernel(const T* __restrict__ x, long n, unsigned* st,
+                                                                   uint8_t* __restrict__ y) {
+  const float s = pow2_scale_of(site_hist_max(st));
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[18] = __float_as_uint(1.f / s);
+  float m = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i * 8 < n; i += (long)gridDim.x * 256) {
+    const long e = i * 8;
+    if (e + 8 <= n) {
+      Chunk8<T> c;
+      c.load(x + e);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = c.get(j);
+        m = fmaxf(m, fabsf(v[j]));
+        v[j] = fminf(fmaxf(v[j] * s, -448.f), 448.f);
+      }
+      uint2 o;
+      o.x = pack4_fp8(v[0], v[1], v[2], v[3]);
+      o.y = pack4_fp8(v[4], v[5], v[6], v[7]);
+      *reinterpret_cast<uint2*>(y + e) = o;
+    } else {
+      for (long j = e; j < n; ++j) {
+        const float f = Elt<T>::to_f(x[j]);
+        m = fmaxf(m, fabsf(f));
+        const int q = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(f * s, -448.f), 448.f), 0.f, 0, false);
+        y[j] = (uint8_t)(q & 0xff);
+      }
+    }
+  }
+  m = wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(st + 16, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+}
+
 // fp8 weights: wk [rows][9 cin] (k = tap * cin + ci) and / or the transposed, flipped wt
 // [rows_t][9 cout] (k = tap' * cout + co), both scaled by s = pow2 scale of amax(|w| / sigma);
 // dq[0] = 1 / s.  The amax partials of |w| come from amax_kernel<float> over w_param.
@@ -4485,6 +4557,9 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   constexpr int MAIN = 2 * HALO + 2 * BST, EPI = BM * BN * 2;
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
 
+  // the delayed-scaling site of this launch's activation operand: its dq (read below by every
+  // block) was fixed by the quantize pass; block 0 moves that pass's amax into the history
+  if (a.roll && blockIdx.x == 0 && threadIdx.x == 0) fp8_site_roll(a.roll);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % WN, wm = wave / WN;
@@ -4609,10 +4684,12 @@ bool fp8_ok(const fv_conv_desc* d) {
 }
 
 int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, const float* dq_x, const uint8_t* w8,
-                 const float* dq_w, const float* bias, const void* res, void* y, float* stats, hipStream_t s) {
+                 const float* dq_w, const float* bias, const void* res, void* y, float* stats, hipStream_t s,
+                 unsigned* roll = nullptr) {
   ConvArgs a{};
   a.x = x8; a.w = w8; a.bias = bias; a.res = res; a.y = y; a.stats = stats;
   a.dq0 = dq_x; a.dq1 = dq_w;
+  a.roll = roll;
   a.N = d->n; a.H = d->h; a.W = d->w; a.Hin = d->h; a.Win = d->w;
   a.P = d->n * d->h * d->w;
   a.Cin = cin; a.lgCin = fv_ilog2(cin);
@@ -4648,6 +4725,30 @@ int fv_quantize_fp8(int dtype_in, const void* x, long count, uint8_t* y, float* 
                        (const float*)ws, nb, y, dq);
   }
   return fv_check_launch("quantize_fp8");
+}
+
+size_t fv_fp8_site_bytes(void) { return FP8_SITE * sizeof(unsigned); }
+
+int fv_quantize_fp8_site(int dtype_in, const void* x, long count, uint8_t* y, void* site, int seeded, void* ws,
+                         void* stream) {
+  FV_REQUIRE(x && y && site && ws && count > 0, "quantize_fp8_site: bad args");
+  FV_REQUIRE(dtype_in == FV_BF16 || dtype_in == FV_F32, "quantize_fp8_site: input must be bf16 or f32");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned* st = (unsigned*)site;
+  const long chunks = (count + 7) / 8;
+  const int nb = (int)std::min<long>(FP8_NPART, std::max<long>(1, (chunks + 255) / 256));
+  if (!seeded) {
+    // exact first call: amax pass, quantize pass (dq into the site), history filled
+    int rc = fv_quantize_fp8(dtype_in, x, count, y, (float*)(st + 18), ws, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(fp8_site_seed_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, nb, st);
+    return fv_check_launch("fp8_site_seed");
+  }
+  if (dtype_in == FV_BF16)
+    hipLaunchKernelGGL(quantize_fp8_delayed_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)x, count, st, y);
+  else
+    hipLaunchKernelGGL(quantize_fp8_delayed_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)x, count, st, y);
+  return fv_check_launch("quantize_fp8_delayed");
 }
 
 int fv_conv2d_fp8_supported(const fv_conv_desc* d) {
@@ -4691,6 +4792,29 @@ int fv_conv2d_fwd_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_d
   FV_REQUIRE(x8 && x_dq && wk && w_dq && y, "null pointer");
   FV_REQUIRE(!(res && stats), "fp8 conv: residual and BN statistics in one call are not supported");
   return conv_fp8_run(d, d->cin, d->cout, x8, x_dq, wk, w_dq, bias, res, y, stats, (hipStream_t)stream);
+}
+
+int fv_conv2d_fwd_fp8_site(const fv_conv_desc* d, const uint8_t* x8, void* site, const uint8_t* wk, const float* w_dq,
+                           const float* bias, const void* res, void* y, float* stats, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fp8_ok(d), "fp8 conv: unsupported descriptor");
+  FV_REQUIRE(x8 && site && wk && w_dq && y, "null pointer");
+  FV_REQUIRE(!(res && stats), "fp8 conv: residual and BN statistics in one call are not supported");
+  unsigned* sp = (unsigned*)site;
+  return conv_fp8_run(d, d->cin, d->cout, x8, (const float*)(sp + 18), wk, w_dq, bias, res, y, stats,
+                      (hipStream_t)stream, sp);
+}
+
+int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void* site, const uint8_t* wt,
+                                const float* wt_dq, void* dx, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fp8_ok(d), "fp8 conv: unsupported descriptor");
+  FV_REQUIRE(dy8 && site && wt && wt_dq && dx, "null pointer");
+  unsigned* sp = (unsigned*)site;
+  return conv_fp8_run(d, d->cout, d->cin, dy8, (const float*)(sp + 18), wt, wt_dq, nullptr, nullptr, dx, nullptr,
+                      (hipStream_t)stream, sp);
 }
 
 int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const float* dy_dq, const uint8_t* wt,

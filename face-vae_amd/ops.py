@@ -27,7 +27,8 @@ F32 = torch.float32
 F64 = torch.float64
 # fp8 compute mode (BASELINE config C5): activations and gradients stay bf16 in HBM; the 3x3
 # convs the fp8 kernels support run forward and data gradient on per-tensor scaled OCP e4m3
-# operands (fv_*_fp8), everything else as in bf16 mode
+# operands (fv_*_fp8_site: delayed scaling from a per-operand amax history, one quantize pass),
+# everything else as in bf16 mode
 FP8 = torch.float8_e4m3fn
 
 
@@ -36,13 +37,27 @@ def storage(mode: torch.dtype) -> torch.dtype:
     return torch.bfloat16 if mode == FP8 else mode
 
 
-def quantize_fp8(t: torch.Tensor):
-    """(uint8 e4m3 copy of a dense tensor, dq = 1 / scale as a 1-element device tensor)."""
+def fp8_site(conv, which: str, device):
+    """Delayed-scaling state of one fp8 operand of `conv` ("x": forward input, "dy": output
+    gradient): [device buffer (fv_fp8_site_bytes), seeded flag].  Kept on the conv module, so
+    the amax history spans steps (include/facevae.h, fv_quantize_fp8_site)."""
+    sites = conv.__dict__.setdefault("_fv_fp8_sites", {})
+    st = sites.get(which)
+    if st is None or st[0].device != device:
+        st = [torch.zeros(query("fv_fp8_site_bytes") // 4, dtype=torch.int32, device=device), False]
+        sites[which] = st
+    return st
+
+
+def quantize_fp8_site(t: torch.Tensor, site):
+    """(uint8 e4m3 copy of t quantized with the site's delayed scale, dq view [1] fp32); the
+    first call of a site quantizes exactly and seeds its history."""
     y = _empty(t.numel(), torch.uint8, t.device)
-    dq = _empty(1, F32, t.device)
     ws = _empty(query("fv_fp8_ws_bytes") // 4, F32, t.device)
-    call("fv_quantize_fp8", L.dtype_code(t.dtype), ptr(t), t.numel(), ptr(y), ptr(dq), ptr(ws), stream())
-    return y, dq
+    call("fv_quantize_fp8_site", L.dtype_code(t.dtype), ptr(t), t.numel(), ptr(y), ptr(site[0]), int(site[1]),
+         ptr(ws), stream())
+    site[1] = True
+    return y, site[0][18:19].view(F32)
 
 
 def pad_pow2(c: int) -> int:
@@ -317,8 +332,9 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
         part = _empty(nb * 2 * d.cout, F32, x.device)
     psc, psh = (pro if pro is not None else (None, None))
     if cs.fp8:
-        x8, xdq = quantize_fp8(x)
-        _timed("fwd", d, lambda: call("fv_conv2d_fwd_fp8", ctypes.byref(d), ptr(x8), ptr(xdq), ptr(cs.wk),
+        site = fp8_site(cs.conv, "x", x.device)
+        x8, xdq = quantize_fp8_site(x, site)
+        _timed("fwd", d, lambda: call("fv_conv2d_fwd_fp8_site", ctypes.byref(d), ptr(x8), ptr(site[0]), ptr(cs.wk),
                                       ptr(cs.wdq), ptr(bias), ptr(res), ptr(y), ptr(part), stream()))
         if CHECK is not None:
             CHECK("fwd", cs, x=x, bias=bias, pro=pro, res=res, y=y, q8=(x8, xdq))
@@ -461,10 +477,11 @@ def _dgrad(cs: ConvState, dy, ldd, need_dx, bnred):
     if not need_dx:
         return None, None
     if cs.fp8:
-        dy8, dydq = quantize_fp8(dy)
+        site = fp8_site(cs.conv, "dy", dy.device)
+        dy8, dydq = quantize_fp8_site(dy, site)
         dx = torch.empty((d.n, d.cin, d.h, d.w), dtype=dy.dtype, device=dev, memory_format=CL)
-        _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data_fp8", ctypes.byref(d), ptr(dy8), ptr(dydq), ptr(cs.wt),
-                                        ptr(cs.wdq), ptr(dx), stream()))
+        _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data_fp8_site", ctypes.byref(d), ptr(dy8), ptr(site[0]),
+                                        ptr(cs.wt), ptr(cs.wdq), ptr(dx), stream()))
         if CHECK is not None:
             CHECK("dgrad", cs, dy=dy, ldd=ldd, dx=dx, q8=(dy8, dydq))
         return dx, None

@@ -221,6 +221,21 @@ int fv_conv2d_fp8_stats_block_pixels(const fv_conv_desc* d);
 /* dx [n][h][w][cin] bf16 from dy8 [n][h][w][cout] fp8 and wt */
 int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const float* dy_dq,
                            const uint8_t* wt, const float* wt_dq, void* dx, void* stream);
+/* Delayed scaling (the product path): a "site" (fv_fp8_site_bytes, zero-initialised device
+ * memory, one per conv operand: activation or output gradient) keeps a 16-deep amax history.
+ * fv_quantize_fp8_site quantizes in ONE pass with s from max(history) (saturating at +-448)
+ * and records the call's amax; seeded = 0 (the site's first call) quantizes exactly
+ * (amax pass + quantize pass) and fills the history.  The *_site convs read dq from the site
+ * and move the recorded amax into the history (so a site's calls must alternate quantize ->
+ * conv, in stream order).  Replaces the per-call amax pass of fv_quantize_fp8. */
+size_t fv_fp8_site_bytes(void);
+int fv_quantize_fp8_site(int dtype_in, const void* x, long count, uint8_t* y, void* site, int seeded,
+                         void* ws, void* stream);
+int fv_conv2d_fwd_fp8_site(const fv_conv_desc* d, const uint8_t* x8, void* site, const uint8_t* wk,
+                           const float* w_dq, const float* bias, const void* res, void* y, float* stats,
+                           void* stream);
+int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void* site, const uint8_t* wt,
+                                const float* wt_dq, void* dx, void* stream);
 /* layout probe: c[16][16] = a[16][128] . b[16][128]^T through one scaled fp8 MFMA tile */
 int fv_fp8_mfma_probe(const uint8_t* a, const uint8_t* b, float* c, void* stream);
 

@@ -109,3 +109,43 @@ def test_conv_fp8_fwd_and_dgrad(case):
     dev = rel(y, F.conv2d(x, w, b, padding=1))
     print(f"\n[fp8 conv {case}] output rel-L2 vs unquantized fp32 conv: {dev:.3e}")
     assert dev < 0.1
+
+
+def test_delayed_scaling_site():
+    """fv_quantize_fp8_site: the first call is exact (bytes and dq of fv_quantize_fp8); later
+    calls quantize with the pow2 scale of the 16-deep amax history, saturating at +-448, and the
+    consuming *_site conv moves each call's amax into the history."""
+    N, C, H, W = 2, 128, 4, 64
+    d = ops.desc(torch.bfloat16, N, H, W, C, C, C, C, 3)
+    w = (torch.randn(C, C, 3, 3, generator=torch.Generator().manual_seed(7)) / (C * 9) ** 0.5).cuda()
+    wk = torch.empty(L.query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), dtype=torch.uint8, device="cuda")
+    wdq = torch.empty(1, device="cuda")
+    ws = torch.empty(L.query("fv_fp8_ws_bytes") // 4, device="cuda")
+    L.call("fv_conv_weight_prep_fp8", ctypes.byref(d), w.data_ptr(), None, wk.data_ptr(), None, wdq.data_ptr(),
+           ws.data_ptr(), L.stream())
+    y = torch.empty(N, C, H, W, dtype=torch.bfloat16, device="cuda").contiguous(memory_format=CL)
+    site = [torch.zeros(L.query("fv_fp8_site_bytes") // 4, dtype=torch.int32, device="cuda"), False]
+
+    def conv(x8):
+        L.call("fv_conv2d_fwd_fp8_site", ctypes.byref(d), x8.data_ptr(), site[0].data_ptr(), wk.data_ptr(),
+               wdq.data_ptr(), None, None, y.data_ptr(), None, L.stream())
+
+    g = torch.Generator().manual_seed(8)
+    x1 = torch.randn(N, C, H, W, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    x2 = (x1.float() * 5.0).to(torch.bfloat16).contiguous(memory_format=CL)       # amax grows 5x
+    q1, dq1 = ops.quantize_fp8_site(x1, site)
+    e1, edq1 = quant(x1)
+    torch.cuda.synchronize()
+    assert torch.equal(q1, e1) and dq1.item() == edq1.item()
+    conv(q1)
+    q2, dq2 = ops.quantize_fp8_site(x2, site)        # delayed: x1's scale, x2 saturates
+    torch.cuda.synchronize()
+    s1 = 1.0 / edq1.item()
+    assert dq2.item() == edq1.item()
+    ref2 = (x2.float() * s1).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(q2, ref2.permute(0, 2, 3, 1).reshape(-1).view(torch.uint8))       # NHWC bytes
+    conv(q2)
+    q3, dq3 = ops.quantize_fp8_site(x2, site)        # the history now holds x2's amax
+    e3, edq3 = quant(x2)
+    torch.cuda.synchronize()
+    assert dq3.item() == edq3.item() and torch.equal(q3, e3)
