@@ -163,6 +163,8 @@ _SIGS = {
     "fv_reparam_ws_bytes": (c_size_t, [c_int, c_int, c_int]),
     "fv_reparam_kl_fwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P, P, P]),
     "fv_reparam_bwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P, P]),
+    "fv_reparam_kl_bwd": (c_int, [c_int, P, P, c_int, c_int, c_int, P, P, P, P, P, P]),
+    "fv_reparam_tiled": (c_int, [c_int, c_int]),
     "fv_kl_fwd": (c_int, [c_int, P, P, c_long, P, P, P]),
     "fv_kl_bwd": (c_int, [c_int, P, P, c_long, P, P, P, P]),
     "fv_mse_fwd": (c_int, [P, P, c_long, P, P, P]),

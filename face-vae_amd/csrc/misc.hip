@@ -134,8 +134,10 @@ __global__ void reparam_fwd_kernel(const T* __restrict__ h, const float* __restr
   float fz[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) fz[j] = m.get(j) + expf(s.get(j)) * ep[(size_t)j * HW];
-  m.store(mu + p * L + cg * 8);
-  s.store(ls + p * L + cg * 8);
+  if (mu) {
+    m.store(mu + p * L + cg * 8);
+    s.store(ls + p * L + cg * 8);
+  }
   Chunk8<T> o;
   o.set8(fz);
   o.store(z + p * L + cg * 8);
@@ -143,12 +145,15 @@ __global__ void reparam_fwd_kernel(const T* __restrict__ h, const float* __restr
 
 template <typename T>
 __global__ void reparam_bwd_kernel(const T* __restrict__ h, const float* __restrict__ eps, int L, int HW, int cpc,
-                                   const T* dz, const T* dmu, const T* dls, T* __restrict__ dh) {
+                                   const T* dz, const T* dmu, const T* dls, const float* klg, float kln,
+                                   T* __restrict__ dh) {
   const int hw = blockIdx.x * blockDim.x + threadIdx.x;
   if (hw >= HW) return;
   const int n = blockIdx.y / cpc, cg = blockIdx.y - (blockIdx.y / cpc) * cpc;
   const size_t p = (size_t)n * HW + hw;
-  Chunk8<T> s, gz, gm, gs;
+  const float kg = klg ? klg[0] * kln : 0.f;
+  Chunk8<T> m, s, gz, gm, gs;
+  if (klg) m.load(h + p * 2 * L + cg * 8); else m.zero();
   s.load(h + p * 2 * L + L + cg * 8);
   if (dz) gz.load(dz + p * L + cg * 8); else gz.zero();
   if (dmu) gm.load(dmu + p * L + cg * 8); else gm.zero();
@@ -157,8 +162,9 @@ __global__ void reparam_bwd_kernel(const T* __restrict__ h, const float* __restr
   float om[8], os[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    om[j] = gz.get(j) + gm.get(j);
-    os[j] = gz.get(j) * expf(s.get(j)) * ep[(size_t)j * HW] + gs.get(j);
+    const float ex = expf(s.get(j));
+    om[j] = gz.get(j) + gm.get(j) + kg * m.get(j);
+    os[j] = gz.get(j) * ex * ep[(size_t)j * HW] + gs.get(j) + kg * (ex * ex - 1.f);
   }
   Chunk8<T> a, b;
   a.set8(om);
@@ -204,8 +210,10 @@ __global__ void __launch_bounds__(NTH) reparam_fwd_tiled(const T* __restrict__ h
       fz[j] = mv + ex * es[(g * 8 + j) * (RP_PX + 1) + px];
       kl += -0.5f - sv + 0.5f * mv * mv + 0.5f * ex * ex;
     }
-    m.store(mu + p * L + g * 8);
-    s.store(ls + p * L + g * 8);
+    if (mu) {
+      m.store(mu + p * L + g * 8);
+      s.store(ls + p * L + g * 8);
+    }
     Chunk8<T> o;
     o.set8(fz);
     o.store(z + p * L + g * 8);
@@ -226,7 +234,7 @@ __global__ void __launch_bounds__(NTH) reparam_fwd_tiled(const T* __restrict__ h
 template <typename T>
 __global__ void __launch_bounds__(NTH) reparam_bwd_tiled(const T* __restrict__ h, const float* __restrict__ eps,
                                                           int L, int HW, const T* dz, const T* dmu, const T* dls,
-                                                          T* __restrict__ dh) {
+                                                          const float* klg, float kln, T* __restrict__ dh) {
   extern __shared__ float es[];
   const int tpb = HW / RP_PX;
   const int n = blockIdx.x / tpb, hw0 = (blockIdx.x - n * tpb) * RP_PX;
@@ -240,10 +248,12 @@ __global__ void __launch_bounds__(NTH) reparam_bwd_tiled(const T* __restrict__ h
   }
   __syncthreads();
   const int G = L / 8;
+  const float kg = klg ? klg[0] * kln : 0.f;
   for (int it = tid; it < RP_PX * G; it += NTH) {
     const int px = it / G, g = it - px * G;
     const size_t p = (size_t)n * HW + hw0 + px;
-    Chunk8<T> s, gz, gm, gs;
+    Chunk8<T> m, s, gz, gm, gs;
+    if (klg) m.load(h + p * 2 * L + g * 8); else m.zero();
     s.load(h + p * 2 * L + L + g * 8);
     if (dz) gz.load(dz + p * L + g * 8); else gz.zero();
     if (dmu) gm.load(dmu + p * L + g * 8); else gm.zero();
@@ -251,8 +261,9 @@ __global__ void __launch_bounds__(NTH) reparam_bwd_tiled(const T* __restrict__ h
     float om[8], os[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      om[j] = gz.get(j) + gm.get(j);
-      os[j] = gz.get(j) * expf(s.get(j)) * es[(g * 8 + j) * (RP_PX + 1) + px] + gs.get(j);
+      const float ex = expf(s.get(j));
+      om[j] = gz.get(j) + gm.get(j) + kg * m.get(j);
+      os[j] = gz.get(j) * ex * es[(g * 8 + j) * (RP_PX + 1) + px] + gs.get(j) + kg * (ex * ex - 1.f);
     }
     Chunk8<T> a, b;
     a.set8(om);
@@ -751,11 +762,13 @@ size_t fv_reparam_ws_bytes(int n, int L, int hw) {
 
 static size_t reparam_lds(int L) { return (size_t)L * (RP_PX + 1) * sizeof(float); }
 
+int fv_reparam_tiled(int L, int hw) { return hw % RP_PX == 0 && reparam_lds(L) <= 64 * 1024; }
+
 int fv_reparam_kl_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu, void* logstd,
                       void* z, float* kl, void* ws, void* stream) {
-  FV_REQUIRE(h && eps && mu && logstd && z && L % 8 == 0, "reparam: bad args (L %% 8 == 0)");
+  FV_REQUIRE(h && eps && z && L % 8 == 0 && !mu == !logstd, "reparam: bad args (L %% 8 == 0)");
   hipStream_t s = (hipStream_t)stream;
-  if (hw % RP_PX == 0 && reparam_lds(L) <= 64 * 1024) {
+  if (fv_reparam_tiled(L, hw)) {
     FV_REQUIRE(!kl || ws, "reparam: KL output needs the workspace");
     const int nb = n * (hw / RP_PX);
     double* part = kl ? (double*)ws : nullptr;
@@ -780,7 +793,7 @@ int fv_reparam_kl_fwd(int dtype, const void* h, const float* eps, int n, int L, 
                        (float*)mu, (float*)logstd, (float*)z);
   int st = fv_check_launch("reparam_fwd");
   if (st || !kl) return st;
-  FV_REQUIRE(ws, "reparam: KL output needs the workspace");
+  FV_REQUIRE(ws && mu, "reparam: the KL of an untiled shape needs the workspace and the mu/logstd outputs");
   return fv_kl_fwd(dtype, mu, logstd, (long)n * L * hw, kl, ws, stream);
 }
 
@@ -789,29 +802,35 @@ int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int
   return fv_reparam_kl_fwd(dtype, h, eps, n, L, hw, mu, logstd, z, nullptr, nullptr, stream);
 }
 
-int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw, const void* dz,
-                   const void* dmu, const void* dlogstd, void* dh, void* stream) {
+int fv_reparam_kl_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw, const void* dz,
+                      const void* dmu, const void* dlogstd, const float* kl_grad, void* dh, void* stream) {
   FV_REQUIRE(h && eps && dh && L % 8 == 0, "reparam bwd: bad args");
   hipStream_t s = (hipStream_t)stream;
-  if (hw % RP_PX == 0 && reparam_lds(L) <= 64 * 1024) {
+  const float kln = (float)(1.0 / ((double)n * L * hw));
+  if (fv_reparam_tiled(L, hw)) {
     const int nb = n * (hw / RP_PX);
     if (dtype == FV_BF16)
       hipLaunchKernelGGL(reparam_bwd_tiled<bf16>, dim3(nb), dim3(NTH), reparam_lds(L), s, (const bf16*)h, eps, L, hw,
-                         (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, (bf16*)dh);
+                         (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, kl_grad, kln, (bf16*)dh);
     else
       hipLaunchKernelGGL(reparam_bwd_tiled<float>, dim3(nb), dim3(NTH), reparam_lds(L), s, (const float*)h, eps, L,
-                         hw, (const float*)dz, (const float*)dmu, (const float*)dlogstd, (float*)dh);
+                         hw, (const float*)dz, (const float*)dmu, (const float*)dlogstd, kl_grad, kln, (float*)dh);
     return fv_check_launch("reparam_bwd_tiled");
   }
   FV_REQUIRE(n * (L / 8) <= 65535, "reparam: too many (image, channel-group) rows");
   const dim3 grid(fv_cdiv(hw, NTH), n * (L / 8));
   if (dtype == FV_BF16)
     hipLaunchKernelGGL(reparam_bwd_kernel<bf16>, grid, dim3(NTH), 0, s, (const bf16*)h, eps, L, hw, L / 8,
-                       (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, (bf16*)dh);
+                       (const bf16*)dz, (const bf16*)dmu, (const bf16*)dlogstd, kl_grad, kln, (bf16*)dh);
   else
     hipLaunchKernelGGL(reparam_bwd_kernel<float>, grid, dim3(NTH), 0, s, (const float*)h, eps, L, hw, L / 8,
-                       (const float*)dz, (const float*)dmu, (const float*)dlogstd, (float*)dh);
+                       (const float*)dz, (const float*)dmu, (const float*)dlogstd, kl_grad, kln, (float*)dh);
   return fv_check_launch("reparam_bwd");
+}
+
+int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw, const void* dz,
+                   const void* dmu, const void* dlogstd, void* dh, void* stream) {
+  return fv_reparam_kl_bwd(dtype, h, eps, n, L, hw, dz, dmu, dlogstd, nullptr, dh, stream);
 }
 
 static int reduce_scalar(int kind, int dtype, const void* a, const void* b, long count, float* loss, void* ws,

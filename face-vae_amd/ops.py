@@ -902,26 +902,35 @@ class ReparamFn(torch.autograd.Function):
     """mu = h[:, :L], logstd = h[:, L:], z = mu + exp(logstd) * eps (models.py:559-561).
     The same pass also reduces the KL of (mu, logstd) (losses.py:392); `reparameterise`
     tags mu with it so that KLDivergenceLoss on exactly this (mu, logstd) pair reuses the
-    value instead of re-reading both tensors."""
+    value instead of re-reading both tensors, and hands its gradient back through `holder`
+    (`KLFn.backward`), which this backward folds into dh (fv_reparam_kl_bwd): no separate KL
+    backward pass, no dmu / dlogstd tensors.  On the tiled shapes mu and logstd are the
+    channel slices of the NHWC h itself (no copies written)."""
 
     @staticmethod
     def forward(ctx, h, eps, dtype, holder):
+        ctx.set_materialize_grads(False)
         hb, C2 = to_nhwc(h, dtype)
         N, _, H, W = h.shape
         Lc = C2 // 2
         e32 = eps.float().contiguous()
         if tuple(e32.shape) != (N, Lc, H, W):
             raise RuntimeError(f"eps must be [N, {Lc}, {H}, {W}]")
-        mu = torch.empty((N, Lc, H, W), dtype=dtype, device=h.device, memory_format=CL)
-        ls = torch.empty_like(mu)
-        z = torch.empty_like(mu)
+        z = torch.empty((N, Lc, H, W), dtype=dtype, device=h.device, memory_format=CL)
+        if query("fv_reparam_tiled", Lc, H * W):
+            mu, ls = None, None
+        else:
+            mu, ls = torch.empty_like(z), torch.empty_like(z)
         kl = torch.empty((), dtype=F32, device=h.device)
         ws = _empty(query("fv_reparam_ws_bytes", N, Lc, H * W) // 8 + 1, F64, h.device)
         call("fv_reparam_kl_fwd", L.dtype_code(dtype), ptr(hb), ptr(e32), N, Lc, H * W, ptr(mu), ptr(ls), ptr(z),
              ptr(kl), ptr(ws), stream())
+        if mu is None:
+            mu, ls = hb[:, :Lc], hb[:, Lc:]
         holder["kl"] = kl
         ctx.save_for_backward(h, hb, e32)
         ctx.dtype = dtype
+        ctx.holder = holder
         return mu, ls, z
 
     @staticmethod
@@ -929,11 +938,12 @@ class ReparamFn(torch.autograd.Function):
         h, hb, e32 = ctx.saved_tensors
         N, C2, H, W = hb.shape
         dt = ctx.dtype
-        dh = torch.empty_like(hb)
-        call("fv_reparam_bwd", L.dtype_code(dt), ptr(hb), ptr(e32), N, C2 // 2, H * W,
+        klg = ctx.holder.pop("kl_grad", None)
+        dh = torch.empty_like(hb, memory_format=CL)
+        call("fv_reparam_kl_bwd", L.dtype_code(dt), ptr(hb), ptr(e32), N, C2 // 2, H * W,
              ptr(grad_in(dz, dt) if dz is not None else None),
              ptr(grad_in(dmu, dt) if dmu is not None else None),
-             ptr(grad_in(dls, dt) if dls is not None else None), ptr(dh), stream())
+             ptr(grad_in(dls, dt) if dls is not None else None), ptr(klg), ptr(dh), stream())
         return from_nhwc(dh, h), None, None, None
 
 
@@ -950,9 +960,10 @@ class KLFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mu, logstd):
         pre = getattr(mu, "_fv_kl", None)
+        ctx.holder = None
         if pre is not None and pre[0] is logstd and mu._version == pre[2] and logstd._version == pre[3]:
-            ctx.save_for_backward(mu, logstd)      # value reduced by the reparameterisation pass
-            return pre[1].clone()
+            ctx.holder = pre[4]                    # value reduced by the reparameterisation pass,
+            return pre[1].clone()                  # gradient folded into its backward
         if mu.dtype not in (F32, torch.bfloat16):
             mu, logstd = mu.float(), logstd.float()
         mu, logstd = _same_layout(mu, logstd)
@@ -964,8 +975,12 @@ class KLFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        g = g.float().reshape(())
+        if ctx.holder is not None:
+            prev = ctx.holder.get("kl_grad")
+            ctx.holder["kl_grad"] = g.contiguous() if prev is None else prev + g
+            return None, None
         mu, ls = ctx.saved_tensors
-        g = g.float().contiguous()
         dmu = torch.empty_like(mu) if ctx.needs_input_grad[0] else None
         dls = torch.empty_like(ls) if ctx.needs_input_grad[1] else None
         call("fv_kl_bwd", L.dtype_code(mu.dtype), ptr(mu), ptr(ls), mu.numel(), ptr(g), ptr(dmu), ptr(dls), stream())
@@ -1014,7 +1029,7 @@ def reparameterise(h, eps, mode):
     dtype = storage(mode)
     holder = {}
     mu, ls, z = ReparamFn.apply(h, eps, dtype, holder)
-    mu._fv_kl = (ls, holder["kl"], mu._version, ls._version)
+    mu._fv_kl = (ls, holder["kl"], mu._version, ls._version, holder)
     return mu, ls, z
 
 

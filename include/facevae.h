@@ -435,9 +435,19 @@ int fv_reparam_fwd(int dtype, const void* h, const float* eps, int n, int L, int
 size_t fv_reparam_ws_bytes(int n, int L, int hw);
 int fv_reparam_kl_fwd(int dtype, const void* h, const float* eps, int n, int L, int hw, void* mu,
                       void* logstd, void* z, float* kl, void* ws, void* stream);
-/* dh = [dz + dmu | dz*exp(logstd)*eps + dlogstd]; dmu/dlogstd may be NULL */
+/* 1 when (L, hw) runs the tiled reparameterisation (hw % 32 == 0, L <= 496): only then may
+ * fv_reparam_kl_fwd leave mu/logstd NULL (the caller reads them as channel slices of h) while
+ * still reducing the KL */
+int fv_reparam_tiled(int L, int hw);
+/* dh = [dz + dmu | dz*exp(logstd)*eps + dlogstd]; dz/dmu/dlogstd may be NULL */
 int fv_reparam_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw,
                    const void* dz, const void* dmu, const void* dlogstd, void* dh, void* stream);
+/* the same plus the KL gradient (KLDivergenceLoss backward, losses.py:392) folded in:
+ * kl_grad = device fp32 dLoss/dKL (NULL: none); dh += kl_grad / (n L hw) *
+ * [mu | exp(2 logstd) - 1] -- the separate fv_kl_bwd pass and its dmu/dlogstd tensors vanish */
+int fv_reparam_kl_bwd(int dtype, const void* h, const float* eps, int n, int L, int hw,
+                      const void* dz, const void* dmu, const void* dlogstd, const float* kl_grad,
+                      void* dh, void* stream);
 int fv_kl_fwd(int dtype, const void* mu, const void* logstd, long count, float* loss, void* ws,
               void* stream);
 int fv_kl_bwd(int dtype, const void* mu, const void* logstd, long count, const float* gout,

@@ -206,6 +206,38 @@ def test_spectral_norm():
     assert rel(gc, wr.grad) < 1e-5
 
 
+@pytest.mark.parametrize("uses", ["kl", "z", "kl+mu", "kl_twice"])
+@pytest.mark.parametrize("H", [8, 6])
+def test_reparam_kl_gradient_routes(H, uses):
+    """The KL gradient folded into the reparameterisation backward (fv_reparam_kl_bwd): KL
+    alone, z alone, KL plus another loss on mu (dmu and the folded term together), KL counted
+    twice -- each against torch autograd on the same fp32 values."""
+    g = gen(12)
+    N, Lc = 2, 16
+    h = torch.randn(N, 2 * Lc, H, H, generator=g) * 0.5
+    eps = torch.randn(N, Lc, H, H, generator=g)
+    gz = torch.randn(N, Lc, H, H, generator=g)
+
+    def loss(mu, ls, z, kl):
+        if uses == "kl":
+            return 2.0 * kl(mu, ls)
+        if uses == "z":
+            return (z.float() * gz.to(z.device)).sum()
+        if uses == "kl+mu":
+            return kl(mu, ls) + (mu.float() * gz.to(mu.device)).sum()
+        return kl(mu, ls) + 0.5 * kl(mu, ls)
+
+    hr = h.clone().requires_grad_(True)
+    mu_r, ls_r = hr[:, :Lc], hr[:, Lc:]
+    loss(mu_r, ls_r, mu_r + torch.exp(ls_r) * eps,
+         lambda m, s: torch.mean(-0.5 - s + 0.5 * m ** 2 + 0.5 * torch.exp(2 * s))).backward()
+    hc = h.cuda().contiguous(memory_format=CL).requires_grad_(True)
+    mu, ls, z = ops.reparameterise(hc, eps.cuda(), torch.float32)
+    loss(mu, ls, z, lambda m, s: fv.KLDivergenceLoss()((m, s))).backward()
+    torch.cuda.synchronize()
+    assert rel(hc.grad, hr.grad) < 1e-5
+
+
 @pytest.mark.parametrize("H", [8, 6])          # 8: tiled reparam + fused KL; 6: hw % 32 != 0 fallback
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_losses_and_reparam(dtype, H):
@@ -231,6 +263,8 @@ def test_losses_and_reparam(dtype, H):
     K2 = fv.KLDivergenceLoss()((mu.detach().clone(), ls.detach().clone()))
     assert abs(K.item() - K2.item()) < 1e-5 * abs(K2.item())
     assert rel(hc.grad.float(), hr.grad) < tol * 2
+    assert torch.equal(mu.float().cpu(), h.to(dtype).float()[:, :Lc]) and torch.equal(
+        ls.float().cpu(), h.to(dtype).float()[:, Lc:])
     # MSE / L1 on fp32 NCHW images
     a = torch.rand(2, 3, 16, 16, generator=g)
     b = torch.rand(2, 3, 16, 16, generator=g)
