@@ -153,6 +153,9 @@ _SIGS = {
     "fv_bn_bwd_finalize_dev": (c_int, [P, c_int, P, P, P, P, P]),
     "fv_bn_act_bwd_apply": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P, P, P, P, c_float,
                                     c_int, P, P, P, P]),
+    "fv_bn_act_fwd_q8": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P, c_float, P, P, P, P]),
+    "fv_bn_act_bwd_apply_q8": (c_int, [c_int, P, P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, P, P, P,
+                                       P, P]),
     "fv_nchw_to_nhwc": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),
     "fv_nhwc_to_nchw": (c_int, [c_int, P, c_int, c_int, c_int, c_int, P, P]),
     "fv_cast": (c_int, [c_int, P, c_int, P, c_long, P]),

@@ -257,6 +257,43 @@ __global__ void act_fwd_kernel(const T* __restrict__ y, int W, int C, int ldc, i
   st8<T>(out + (size_t)(row * Wo + j) * C + c, o);
 }
 
+// act_fwd (no pool, dense channels) that also writes an e4m3 copy of its output for an fp8 conv:
+// the bf16-rounded output quantized with the delayed scale of the consumer's site (exactly what
+// a separate quantize pass over `out` would write), the block amax into the site's in-flight
+// slot.  Flat grid-stride over 8-channel chunks; the stride is a multiple of C/8, so each thread
+// keeps one chunk's scale / shift.
+template <typename T>
+__global__ void __launch_bounds__(NTH) act_fwd_q8_kernel(const T* __restrict__ y, int n8, int lgcpc,
+                                                         const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, float slope,
+                                                         T* __restrict__ out, uint8_t* __restrict__ out8,
+                                                         unsigned* st) {
+  const float s = pow2_scale_of(site_hist_max(st));
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[18] = __float_as_uint(1.f / s);
+  const int e0 = blockIdx.x * NTH + threadIdx.x;
+  const int c = (e0 & ((1 << lgcpc) - 1)) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    sc[q] = scale[c + q];
+    sh[q] = shift[c + q];
+  }
+  float m = 0.f;
+  for (int e = e0; e < n8; e += gridDim.x * NTH) {
+    float f[8], o[8];
+    ld8<T>(y + (size_t)e * 8, f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = fv_act(f[q] * sc[q] + sh[q], slope);
+    Chunk8<T> ch;
+    ch.set8(o);
+    ch.store(out + (size_t)e * 8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = ch.get(q);
+    *reinterpret_cast<uint2*>(out8 + (size_t)e * 8) = q8_pack(o, s, m);
+  }
+  q8_block_amax(m, st);
+}
+
 // per-thread copy of one 8-channel chunk's BN parameters
 struct BnChunk {
   float mean[8], inv[8], gam[8], bet[8];
@@ -535,6 +572,50 @@ __global__ void act_bwd_apply_kernel(const T* __restrict__ dout, const T* __rest
     }
     st8<T>(dx + (size_t)p * ldc + c, o);
   }
+}
+
+// act_bwd_apply (no pool, dense channels) that also writes the e4m3 copy of dx for the fp8 data
+// gradient consuming it (see act_fwd_q8_kernel)
+template <typename T>
+__global__ void __launch_bounds__(NTH) act_bwd_apply_q8_kernel(
+    const T* __restrict__ dout, const T* __restrict__ y, int P, int C, int lgcpc, const float* mean,
+    const float* invstd, const float* gamma, const float* beta, float slope, const float* __restrict__ k,
+    const T* __restrict__ addend, T* __restrict__ dx, uint8_t* __restrict__ dx8, unsigned* st) {
+  const float s = pow2_scale_of(site_hist_max(st));
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[18] = __float_as_uint(1.f / s);
+  const int total = P << lgcpc;
+  const int e0 = blockIdx.x * NTH + threadIdx.x;
+  const int c = (e0 & ((1 << lgcpc) - 1)) * 8;
+  BnChunk bp;
+  bp.load(mean, invstd, gamma, beta, c);
+  float k0[8], k1[8], gi[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    k0[q] = k[c + q];
+    k1[q] = k[C + c + q];
+    gi[q] = bp.gam[q] * bp.inv[q];
+  }
+  const FastDiv unused = {0u, 0u};
+  float m = 0.f;
+  for (int e = e0; e < total; e += gridDim.x * NTH) {
+    const int p = e >> lgcpc;
+    float g[8], yh[8], o[8];
+    grad_g<T>(dout, y, p, unused, 0, C, C, c, 0, bp, slope, g, yh);
+    float ad[8];
+    if (addend) ld8<T>(addend + (size_t)p * C + c, ad);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      o[q] = gi[q] * (g[q] - k0[q] - yh[q] * k1[q]);
+      if (addend) o[q] += ad[q];
+    }
+    Chunk8<T> ch;
+    ch.set8(o);
+    ch.store(dx + (size_t)p * C + c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = ch.get(q);
+    *reinterpret_cast<uint2*>(dx8 + (size_t)p * C + c) = q8_pack(o, s, m);
+  }
+  q8_block_amax(m, st);
 }
 
 // BN backward from the [3][C] (count, sum g, sum g*yhat) totals of store-pass records
@@ -826,6 +907,53 @@ int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h
                        (const float*)y, P, fw, w, c, ldc, lgcpc, mean, invstd, gamma, beta, slope, pool, k,
                        (const float*)addend, (float*)dx);
   return fv_check_launch("bn_bwd_apply");
+}
+
+// fp8 (e4m3) copy of the output beside it, for a consumer conv in fp8 mode (delayed scaling:
+// include/facevae.h, fv_quantize_fp8_site).  2048 blocks: one site atomic per block.
+constexpr int Q8_BLOCKS = 2048;
+
+int fv_bn_act_fwd_q8(int dtype, const void* y, int n, int h, int w, int c, const float* scale,
+                     const float* shift, float slope, void* out, void* out8, void* site, void* stream) {
+  int st = check_c(c, c);
+  if (st) return st;
+  FV_REQUIRE(y && scale && shift && out && out8 && site, "bn_act_fwd_q8: null pointer");
+  const long n8 = (long)n * h * w * (c / 8);
+  FV_REQUIRE(n8 * 8 < (1L << 31), "bn: tensor too large for 32-bit indexing");
+  const int lgcpc = fv_ilog2(c / 8);
+  const int nb = grid_for(n8, Q8_BLOCKS);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(act_fwd_q8_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)y, (int)n8, lgcpc, scale,
+                       shift, slope, (bf16*)out, (uint8_t*)out8, (unsigned*)site);
+  else
+    hipLaunchKernelGGL(act_fwd_q8_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)y, (int)n8, lgcpc, scale,
+                       shift, slope, (float*)out, (uint8_t*)out8, (unsigned*)site);
+  return fv_check_launch("bn_act_fwd_q8");
+}
+
+int fv_bn_act_bwd_apply_q8(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
+                           const float* mean, const float* invstd, const float* gamma, const float* beta,
+                           float slope, const float* k, const void* addend, void* dx, void* dx8, void* site,
+                           void* stream) {
+  int st = check_c(c, c);
+  if (st) return st;
+  FV_REQUIRE(dout && y && mean && invstd && gamma && beta && k && dx && dx8 && site,
+             "bn_act_bwd_apply_q8: null pointer");
+  FV_REQUIRE((long)n * h * w * c < (1L << 31), "bn: tensor too large for 32-bit indexing");
+  const long work = (long)n * h * w * (c / 8);
+  const int P = n * h * w, lgcpc = fv_ilog2(c / 8);
+  const int nb = grid_for(work, Q8_BLOCKS);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == FV_BF16)
+    hipLaunchKernelGGL(act_bwd_apply_q8_kernel<bf16>, dim3(nb), dim3(NTH), 0, s, (const bf16*)dout, (const bf16*)y,
+                       P, c, lgcpc, mean, invstd, gamma, beta, slope, k, (const bf16*)addend, (bf16*)dx,
+                       (uint8_t*)dx8, (unsigned*)site);
+  else
+    hipLaunchKernelGGL(act_bwd_apply_q8_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)dout,
+                       (const float*)y, P, c, lgcpc, mean, invstd, gamma, beta, slope, k, (const float*)addend,
+                       (float*)dx, (uint8_t*)dx8, (unsigned*)site);
+  return fv_check_launch("bn_bwd_apply_q8");
 }
 
 }  // extern "C"

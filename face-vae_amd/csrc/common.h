@@ -128,3 +128,54 @@ static inline FastDiv make_fastdiv(uint32_t d) {
   return {(uint32_t)m, s};
 }
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
+// ------------------------------------------------------------------------------------
+// fp8 (e4m3) delayed-scaling sites, shared by the quantize passes (conv.hip) and the BN passes
+// that write an fp8 copy of their output (bn.hip).  site = uint32[FP8_SITE]: [0, 16) amax
+// history (float bits), [16] amax of the call in flight (float bits, atomicMax: max is
+// order-free, so deterministic), [17] history write index, [18] dq of the call in flight.
+// ------------------------------------------------------------------------------------
+constexpr int FP8_SITE = 32, FP8_HIST = 16;
+
+// largest power of two s with amax * s <= 448
+__device__ __forceinline__ float pow2_scale_of(float amax) {
+  if (!(amax > 0.f) || !isfinite(amax)) return 1.f;
+  return exp2f(floorf(log2f(448.f / amax)));
+}
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (uint32_t)v;
+}
+__device__ __forceinline__ float site_hist_max(const unsigned* st) {
+  float m = 0.f;
+#pragma unroll
+  for (int i = 0; i < FP8_HIST; ++i) m = fmaxf(m, __uint_as_float(st[i]));
+  return m;
+}
+// 8 values -> 8 e4m3 bytes with the call's scale s (saturating at +-448); m = running amax of
+// the unscaled values
+__device__ __forceinline__ uint2 q8_pack(const float* v, float s, float& m) {
+  float q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m = fmaxf(m, fabsf(v[j]));
+    q[j] = fminf(fmaxf(v[j] * s, -448.f), 448.f);
+  }
+  uint2 o;
+  o.x = pack4_fp8(q[0], q[1], q[2], q[3]);
+  o.y = pack4_fp8(q[4], q[5], q[6], q[7]);
+  return o;
+}
+// block (blockDim.x threads, a multiple of 64, no early exits) amax -> the site's in-flight slot
+__device__ __forceinline__ void q8_block_amax(float m, unsigned* st) {
+  m = wave_max(m);
+  __shared__ float red[16];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r = fmaxf(r, red[w]);
+    atomicMax(st + 16, __float_as_uint(r));
+  }
+}

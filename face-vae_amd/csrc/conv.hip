@@ -4342,12 +4342,6 @@ namespace {
 
 constexpr int FP8_NPART = 1024;   // amax partials (blocks of the amax pass)
 
-__device__ __forceinline__ float pow2_scale_of(float amax) {
-  // largest power of two s with amax * s <= 448
-  if (!(amax > 0.f) || !isfinite(amax)) return 1.f;
-  return exp2f(floorf(log2f(448.f / amax)));
-}
-
 template <typename T>
 __global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, long n, float* part) {
   float m = 0.f;
@@ -4379,12 +4373,6 @@ __device__ __forceinline__ float amax_of_parts(const float* part, int np, float*
   float r = 0.f;
   for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r = fmaxf(r, sh[w]);
   return r;
-}
-
-__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
-  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
-  return (uint32_t)v;
 }
 
 template <typename T>
@@ -4419,13 +4407,6 @@ __global__ void __launch_bounds__(256) quantize_fp8_kernel(const T* __restrict__
 // conv consuming the operand moves that amax into the history (fp8_site_roll, block 0 at its
 // start: every quantize block has finished by then and only dq is read concurrently).  The
 // site's first call quantizes exactly (amax pass + quantize pass) and fills the history.
-constexpr int FP8_SITE = 32, FP8_HIST = 16;
-__device__ __forceinline__ float site_hist_max(const unsigned* st) {
-  float m = 0.f;
-#pragma unroll
-  for (int i = 0; i < FP8_HIST; ++i) m = fmaxf(m, __uint_as_float(st[i]));
-  return m;
-}
 __device__ __forceinline__ void fp8_site_roll(unsigned* st) {
   const unsigned p = st[17] % FP8_HIST;
   st[p] = st[16];

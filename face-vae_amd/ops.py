@@ -324,7 +324,8 @@ def stats_geometry(cs: ConvState):
     return query("fv_conv2d_stats_blocks", d), query("fv_conv2d_stats_block_pixels", d)
 
 
-def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False):
+def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False, x8=None):
+    """x8: (e4m3 copy of x, dq) already written by x's producer (bn_act_forward_q8), fp8 mode."""
     d = cs.d
     part = None
     if stats:
@@ -333,7 +334,7 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
     psc, psh = (pro if pro is not None else (None, None))
     if cs.fp8:
         site = fp8_site(cs.conv, "x", x.device)
-        x8, xdq = quantize_fp8_site(x, site)
+        x8, xdq = x8 if x8 is not None else quantize_fp8_site(x, site)
         _timed("fwd", d, lambda: call("fv_conv2d_fwd_fp8_site", ctypes.byref(d), ptr(x8), ptr(site[0]), ptr(cs.wk),
                                       ptr(cs.wdq), ptr(bias), ptr(res), ptr(y), ptr(part), stream()))
         if CHECK is not None:
@@ -462,15 +463,16 @@ def _sn_defer(cs: ConvState) -> bool:
     return True
 
 
-def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=True, bnred=None, want_recs=False):
+def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=True, bnred=None, want_recs=False,
+                  dy8=None):
     """-> (dx at the conv input resolution (upsample folded back), dW (param layout), db
-    [, BNRecords or None when want_recs])."""
+    [, BNRecords or None when want_recs]).  dy8: (e4m3 copy of dy, dq) from dy's producer."""
     dw, db = _wgrad(cs, x, dy, ldd, pro, need_db)
-    dx, recs = _dgrad(cs, dy, ldd, need_dx, bnred)
+    dx, recs = _dgrad(cs, dy, ldd, need_dx, bnred, dy8)
     return (dx, dw, db, recs) if want_recs else (dx, dw, db)
 
 
-def _dgrad(cs: ConvState, dy, ldd, need_dx, bnred):
+def _dgrad(cs: ConvState, dy, ldd, need_dx, bnred, dy8=None):
     """Data gradient of cs -> (dx or None, BNRecords or None)."""
     d = cs.d
     dev = dy.device
@@ -478,7 +480,7 @@ def _dgrad(cs: ConvState, dy, ldd, need_dx, bnred):
         return None, None
     if cs.fp8:
         site = fp8_site(cs.conv, "dy", dy.device)
-        dy8, dydq = quantize_fp8_site(dy, site)
+        dy8, dydq = dy8 if dy8 is not None else quantize_fp8_site(dy, site)
         dx = torch.empty((d.n, d.cin, d.h, d.w), dtype=dy.dtype, device=dev, memory_format=CL)
         _timed("dgrad", d, lambda: call("fv_conv2d_bwd_data_fp8_site", ctypes.byref(d), ptr(dy8), ptr(site[0]),
                                         ptr(cs.wt), ptr(cs.wdq), ptr(dx), stream()))
@@ -609,6 +611,29 @@ def bn_act_forward(y, r: BNResult, slope, pool, bn=None):
     return out
 
 
+def _q8_ok(site, y, pool, bn=None):
+    """The fused fp8 copy applies: a seeded site (the exact first call stays a separate pass),
+    bf16 storage, no pooling, affine BN."""
+    return (site is not None and site[1] and not pool and y.dtype == torch.bfloat16
+            and (bn is None or (bn.weight is not None and bn.bias is not None)))
+
+
+def bn_act_forward_q8(y, r: BNResult, slope, bn, site):
+    """bn_act_forward for an fp8 consumer: -> (out, (e4m3 copy, dq) or None).  With a seeded
+    delayed-scaling site the pass writes the consumer's fp8 operand beside `out`
+    (fv_bn_act_fwd_q8), so the conv needs no quantize pass of its own."""
+    if not _q8_ok(site, y, False):
+        return bn_act_forward(y, r, slope, False, bn), None
+    N, C, H, W = y.shape
+    out = torch.empty((N, C, H, W), dtype=y.dtype, device=y.device, memory_format=CL)
+    out8 = _empty(out.numel(), torch.uint8, y.device)
+    call("fv_bn_act_fwd_q8", L.dtype_code(y.dtype), ptr(y), N, H, W, C, ptr(r.scale), ptr(r.shift), float(slope),
+         ptr(out), ptr(out8), ptr(site[0]), stream())
+    if CHECK is not None:
+        CHECK("bn_fwd", bn, y=y, r=r, slope=slope, pool=False, out=out)
+    return out, (out8, site[0][18:19].view(F32))
+
+
 def bn_backward_is_local(r: BNResult, comm) -> bool:
     """True when this BN's backward needs no collective: no communicator, or eval-mode
     statistics (running mean / var, count 0, no all-reduced record) -- the normalisation is
@@ -618,9 +643,11 @@ def bn_backward_is_local(r: BNResult, comm) -> bool:
     return comm is None or (r.count == 0 and r.stats is None)
 
 
-def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True, recs=None):
+def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True, recs=None, q8=None):
     """-> (dx of the BN input, dgamma, dbeta).  recs: the BN-backward sums already reduced by
-    the dgrad that produced dout (BNRecords), replacing the reduce pass."""
+    the dgrad that produced dout (BNRecords), replacing the reduce pass.  q8: the delayed-scaling
+    site of an fp8 data gradient consuming dx -> (dx, dgamma, dbeta, (e4m3 copy of dx, dq) or
+    None), the copy written by the apply pass itself (fv_bn_act_bwd_apply_q8)."""
     N, C, H, W = y.shape
     dev = y.device
     dc = L.dtype_code(y.dtype)
@@ -663,14 +690,21 @@ def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, ne
         if need_dx:
             _sync(red, comm)
             call("fv_bn_bwd_finalize_dev", ptr(red), C, ptr(r.stats), None, None, ptr(k), stream())
-    dx = None
+    dx = q = None
     if need_dx:
         dx = torch.empty((N, C, H, W), dtype=y.dtype, device=dev, memory_format=CL)
-        call("fv_bn_act_bwd_apply", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
-             ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), ptr(k), ptr(addend), ptr(dx), stream())
+        if _q8_ok(q8, y, pool, bn):
+            dx8 = _empty(dx.numel(), torch.uint8, dev)
+            call("fv_bn_act_bwd_apply_q8", dc, ptr(dout), ptr(y), N, H, W, C, ptr(r.mean), ptr(r.invstd),
+                 ptr(bn.weight), ptr(bn.bias), float(slope), ptr(k), ptr(addend), ptr(dx), ptr(dx8), ptr(q8[0]),
+                 stream())
+            q = (dx8, q8[0][18:19].view(F32))
+        else:
+            call("fv_bn_act_bwd_apply", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
+                 ptr(bn.weight), ptr(bn.bias), float(slope), int(pool), ptr(k), ptr(addend), ptr(dx), stream())
     if CHECK is not None and comm is None:
         CHECK("bn_bwd", bn, dout=dout, y=y, r=r, slope=slope, pool=pool, addend=addend, dx=dx, dg=dg, dbt=dbt)
-    return dx, dg, dbt
+    return (dx, dg, dbt, q) if q8 is not None else (dx, dg, dbt)
 
 
 def grad_in(g: torch.Tensor, dtype) -> torch.Tensor:
@@ -766,15 +800,16 @@ class ResBlockFn(torch.autograd.Function):
             r1 = bn_from_records(blk.bn1, rec[0], rec[1], rec[2], N * H * W, C, True, comm)
         else:
             r1 = bn_from_tensor(blk.bn1, xb, training, comm)
-        a1 = bn_act_forward(xb, r1, 0.0, False, blk.bn1)
         d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size)
         cs1 = ConvState(c1, d1, dtype, x.device, training, True, fp8=mode == FP8)
+        # fp8 convs: the BN pass writes the conv's e4m3 operand beside its bf16 output
+        a1, q1 = bn_act_forward_q8(xb, r1, 0.0, blk.bn1, fp8_site(c1, "x", x.device) if cs1.fp8 else None)
         t1 = torch.empty_like(xb)
-        part = conv_forward(cs1, a1, b1, y=t1, stats=training)
+        part = conv_forward(cs1, a1, b1, y=t1, stats=training, x8=q1)
         r2 = bn_from_partials(blk.bn2, part, cs1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
-        a2 = bn_act_forward(t1, r2, 0.0, False, blk.bn2)
         d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size)
         cs2 = ConvState(c2, d2, dtype, x.device, training, True, fp8=mode == FP8)
+        a2, q2 = bn_act_forward_q8(t1, r2, 0.0, blk.bn2, fp8_site(c2, "x", x.device) if cs2.fp8 else None)
         out = torch.empty_like(xb)
         geo = sr_records(d2, False) if training and not cs2.fp8 else None
         if geo is not None:
@@ -789,7 +824,7 @@ class ResBlockFn(torch.autograd.Function):
                 CHECK("fwd", cs2, x=a2, bias=b2, pro=None, res=xb, y=out)
             blk._fv_out_rec = (part, geo[0], geo[1])
         else:
-            conv_forward(cs2, a2, b2, res=xb, y=out)
+            conv_forward(cs2, a2, b2, res=xb, y=out, x8=q2)
             blk._fv_out_rec = None
         cs1.release()
         cs2.release()
@@ -807,8 +842,9 @@ class ResBlockFn(torch.autograd.Function):
         # store pass they cost that kernel +29 us per launch against the pass's 27 us,
         # profiles/r2b_*)
         da2, dw2, db2 = conv_backward(cs2, a2, dout, C)
-        dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm)
-        da1, dw1, db1 = conv_backward(cs1, a1, dt1, C)
+        site1 = fp8_site(cs1.conv, "dy", xb.device) if cs1.fp8 else None
+        dt1, dg2, dbe2, *q = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, q8=site1)
+        da1, dw1, db1 = conv_backward(cs1, a1, dt1, C, dy8=q[0] if q else None)
         dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout)
         dx = from_nhwc(dxb, x)
         return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None

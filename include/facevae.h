@@ -410,6 +410,17 @@ int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h
                         int ldc, const float* mean, const float* invstd, const float* gamma,
                         const float* beta, float slope, int pool, const float* k,
                         const void* addend, void* dx, void* stream);
+/* the same two passes (no pool, ldc == c) also writing an e4m3 copy of their output for an fp8
+ * conv that consumes it: out8 / dx8 [n][h][w][c] bytes = the bf16 output quantized with the
+ * delayed scale of `site` (the consumer's fv_fp8_site_bytes site, already seeded), bit-identical
+ * to fv_quantize_fp8_site over the output; the site's in-flight amax and dq are updated the
+ * same way.  Replaces the separate quantize pass (one read of the output) */
+int fv_bn_act_fwd_q8(int dtype, const void* y, int n, int h, int w, int c, const float* scale,
+                     const float* shift, float slope, void* out, void* out8, void* site, void* stream);
+int fv_bn_act_bwd_apply_q8(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
+                           const float* mean, const float* invstd, const float* gamma,
+                           const float* beta, float slope, const float* k, const void* addend,
+                           void* dx, void* dx8, void* site, void* stream);
 
 /* ------------------------------------------------------ elementwise / layout ---- */
 int fv_nchw_to_nhwc(int dtype_out, const float* x, int n, int c, int hw, int ldc, void* out,

@@ -149,3 +149,49 @@ def test_delayed_scaling_site():
     e3, edq3 = quant(x2)
     torch.cuda.synchronize()
     assert dq3.item() == edq3.item() and torch.equal(q3, e3)
+
+
+@pytest.mark.parametrize("addend", [False, True])
+def test_bn_passes_write_the_fp8_operand(addend):
+    """fv_bn_act_fwd_q8 / fv_bn_act_bwd_apply_q8: the bf16 output equals the plain BN pass, and
+    the e4m3 copy, dq and the site's in-flight amax equal fv_quantize_fp8_site over that output
+    on an identical copy of the site (delayed scale: the history is seeded with a smaller amax,
+    so part of the output saturates)."""
+    g = torch.Generator().manual_seed(21)
+    N, C, H, W = 2, 256, 8, 64
+    y = (torch.randn(N, C, H, W, generator=g) * 2).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+    dout = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=CL)
+    add = torch.randn(N, C, H, W, generator=g).to(torch.bfloat16).cuda().contiguous(memory_format=CL) if addend \
+        else None
+    bn = torch.nn.BatchNorm2d(C).cuda()                    # affine parameter holder
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    r = ops._bn_result(C, y.device, N * H * W)
+    r.mean.copy_(torch.randn(C, generator=g).cuda() * 0.1)
+    r.invstd.copy_(torch.rand(C, generator=g).cuda() + 0.5)
+    r.scale.copy_(bn.weight.detach() * r.invstd)
+    r.shift.copy_(bn.bias.detach() - r.mean * r.scale)
+
+    def seeded_site():
+        s = [torch.zeros(L.query("fv_fp8_site_bytes") // 4, dtype=torch.int32, device="cuda"), True]
+        s[0][:16] = torch.tensor([1.5], dtype=torch.float32).view(torch.int32).item()
+        return s
+
+    # forward pass
+    sa, sb = seeded_site(), seeded_site()
+    out, q = ops.bn_act_forward_q8(y, r, 0.0, bn, sa)
+    ref = ops.bn_act_forward(y, r, 0.0, False, bn)
+    rq, rdq = ops.quantize_fp8_site(ref, sb)
+    torch.cuda.synchronize()
+    assert q is not None and torch.equal(out, ref)
+    assert torch.equal(q[0], rq) and q[1].item() == rdq.item() and torch.equal(sa[0], sb[0])
+    # backward apply
+    sa, sb = seeded_site(), seeded_site()
+    dx, _, _, q = ops.bn_act_backward(dout, y, bn, r, 0.0, False, None, addend=add, q8=sa)
+    # the same BN backward (same reduce, same k) without the site, then the separate quantize
+    dx2, _, _ = ops.bn_act_backward(dout, y, bn, r, 0.0, False, None, addend=add)
+    rq, rdq = ops.quantize_fp8_site(dx2, sb)
+    torch.cuda.synchronize()
+    assert q is not None and torch.equal(dx, dx2)
+    assert torch.equal(q[0], rq) and q[1].item() == rdq.item() and torch.equal(sa[0], sb[0])
