@@ -3326,6 +3326,8 @@ int wg2_cfg(const fv_conv_desc* d, int K) {
   if (bc == 16) return 5;
   if (bc == 64) return (K % 384 == 0 && d->w % 64 == 0) ? 7 : 4;
   const bool k256 = fv_cdiv(K, 256) * 256 <= fv_cdiv(K, 128) * 128;
+  // (r3, alternating convbench runs on one box, res wgrad at B=32: cfg 0 150-153 us, cfg 6
+  // (32-pixel stages, 3 in flight) 168, cfg 1 (128 x 256 tiles, 3 stages) 202-207)
   if (bc == 256) return K % 256 == 0 ? 0 : (d->ksize == 3 && d->w % 32 == 0 ? 6 : 1);
   return k256 ? 2 : 3;
 }
