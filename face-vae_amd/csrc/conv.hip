@@ -1537,6 +1537,173 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
 }
 
 // ----------------------------------------------------------------------------------------
+// 3x3 conv with 64 input channels at full resolution (AFE.down1 forward, 64 -> 128 at 256^2),
+// as a sliding band with the weights in registers.  A block of 8 waves owns 64 output channels
+// of one 64-column strip of one image and walks a band of rows, 4 output rows per iteration:
+// wave (rw, cg) computes output row h0 + rw x 64 pixels for the 32 channels cg of the block's
+// 64, with its 2 x 18 A fragments (32 co x K = 576 = 9 taps x 64 ci) held in registers for the
+// whole band (two waves per SIMD fit: ~240 registers each) -- the only LDS traffic is the input,
+// 4 B fragments per 8 MFMAs.  Input rows (66 px incl. the halo columns) stream through a 10-row
+// LDS ring by LDS-DMA (44 pieces per iteration spread over the waves and over the first k-steps)
+// and are waited for one iteration later (counted vmcnt: the output stores issued after them
+// stay in flight).  A halo pixel takes 160 B (128 B of channels + 32 B zero-filled by
+// out-of-range DMA slots): 16 consecutive pixels read by ds_read_b128 are conflict-free from any
+// start.  The two 64-channel halves of a strip are neighbours on one XCD, so the input is
+// fetched from HBM about once.  Epilogue per iteration: bias, BN (sum, sum of squares) per lane
+// over 8 iterations = one record of 512 pixels per (wave row, 8 iterations), 16-B bf16 stores
+// (v_permlane16_swap pairs the two 16-channel fragments).  Replaces conv_fwd_v2's per-tap DMA.
+// ----------------------------------------------------------------------------------------
+constexpr int C64_PXB = 160, C64_ROWB = 11 * 1024, C64_NR = 10, C64_G = 8;
+__global__ void __launch_bounds__(512, 1)
+conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
+  __shared__ __attribute__((aligned(1024))) char smem[C64_NR * C64_ROWB];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cg = wave & 1, rw = wave >> 1;
+  const int lr = lane & 15, lh = lane >> 4;
+  // XCD-aware order: consecutive local ids (the co groups of one strip) share an XCD
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int nco = a.Cout >> 6, strips = a.W >> 6;
+  const int cgrp = lid % nco, rest = lid / nco;
+  const int band = rest % nbands, strip = (rest / nbands) % strips, n = rest / (nbands * strips);
+  const int BAND = a.H / nbands, hb = band * BAND, w0 = strip * 64;
+  const int cw = cgrp * 64 + cg * 32;                       // this wave's first output channel
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+  // DMA slots of a row: 16-B chunk k = piece * 64 + lane -> halo pixel k / 10, chunk k % 10
+  unsigned poff[11];
+#pragma unroll
+  for (int p = 0; p < 11; ++p) {
+    const int k = p * 64 + lane, px = k / 10, ch = k - (k / 10) * 10;
+    const int iw = w0 - 1 + px;
+    poff[p] = (px < 66 && ch < 8 && iw >= 0 && iw < a.W) ? (unsigned)((iw * 64 + ch * 8) * 2) : 0x80000000u;
+  }
+  auto row_slot = [&](int y) { return (y - hb + 1) % C64_NR; };
+  // piece q (0 .. 11 * rows - 1) of the rows starting at y0: row y0 + q / 11, piece q % 11
+  auto issue_piece = [&](int y0, int q) {                  // rows outside the image -> zeros
+    const int y = y0 + q / 11, p = q % 11;
+    const bool rok = y >= 0 && y < a.H;
+    unsigned v = 0x80000000u;
+#pragma unroll
+    for (int j = 0; j < 11; ++j)
+      if (j == p) v = poff[j];
+    dma16s(xr, sbase + row_slot(y) * C64_ROWB + p * 1024, rok ? v : 0x80000000u,
+           rok ? (unsigned)((n * a.H + y) * a.W) * 128u : 0u);
+  };
+
+  // the wave's weights: A fragment (cf, ks) = 16 channels x 32 k, k = tap * 64 + ci
+  bf16x8 wf[2][18];
+  const bf16* wk = reinterpret_cast<const bf16*>(a.w);
+#pragma unroll
+  for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks)
+      wf[cf][ks] = *reinterpret_cast<const bf16x8*>(wk + (long)(cw + cf * 16 + lr) * a.Kpad + ks * 32 + lh * 8);
+  float bv[2][4];
+#pragma unroll
+  for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[cf][i] = a.bias ? a.bias[cw + cf * 16 + lh * 4 + i] : 0.f;
+
+  // prologue: input rows hb - 1 .. hb + 4 (66 pieces)
+  for (int q = wave; q < 66; q += 8) issue_piece(hb - 1, q);
+
+  float st[2][4], sq[2][4];
+#pragma unroll
+  for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[cf][i] = sq[cf][i] = 0.f;
+  const int niter = BAND >> 2, ng = niter / C64_G;
+  const int rec0 = ((n * strips + strip) * nbands + band) * (4 * ng);
+  const int loff = lr * C64_PXB + lh * 16;
+  auto pk = [](float lo, float hi) {
+    const bf16 t[2] = {(bf16)lo, (bf16)hi};
+    return *reinterpret_cast<const unsigned*>(t);
+  };
+
+  for (int it = 0; it < niter; ++it) {
+    const int h0 = hb + 4 * it;
+    // this iteration's rows landed; younger than them are at most the previous iteration's 4
+    // output stores (+ 2 record stores), which stay in flight
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bool more = it + 1 < niter;
+    const int orow = h0 + rw;
+    unsigned sb[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) sb[q] = (unsigned)(row_slot(orow - 1 + q) * C64_ROWB + loff);
+
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int pf = 0; pf < 4; ++pf)
+#pragma unroll
+      for (int cf = 0; cf < 2; ++cf) acc[pf][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int tap = ks >> 1, r = tap / 3, s = tap - (tap / 3) * 3, ch = ks & 1;
+      bf16x8 fb[4];
+#pragma unroll
+      for (int pf = 0; pf < 4; ++pf)
+        fb[pf] = *reinterpret_cast<const bf16x8*>(smem + sb[r] + (pf * 16 + s) * C64_PXB + ch * 64);
+      // the next iteration's rows h0 + 5 .. h0 + 8: pieces wave, wave + 8, ... < 44
+      if (ks < 6 && more && wave + 8 * ks < 44) issue_piece(h0 + 5, wave + 8 * ks);
+#pragma unroll
+      for (int pf = 0; pf < 4; ++pf)
+#pragma unroll
+        for (int cf = 0; cf < 2; ++cf)
+          acc[pf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cf][ks], fb[pf], acc[pf][cf], 0, 0, 0);
+    }
+
+    // epilogue: bias, BN partials, 16-B stores: lane (lr, lh) holds channels cf * 16 + lh * 4
+    // .. + 3 of pixel lr; one v_permlane16_swap per dword pair leaves lane lh with the 8
+    // contiguous channels (lh & 1) * 16 + (lh >> 1) * 8 .. + 7
+    bf16* yp = reinterpret_cast<bf16*>(a.y) + ((long)(n * a.H + orow) * a.W + w0 + lr) * a.ldy + cw +
+               (lh & 1) * 16 + (lh >> 1) * 8;
+#pragma unroll
+    for (int pf = 0; pf < 4; ++pf) {
+      float v[2][4];
+#pragma unroll
+      for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[cf][i] = acc[pf][cf][i] + bv[cf][i];
+          st[cf][i] += v[cf][i];
+          sq[cf][i] += v[cf][i] * v[cf][i];
+        }
+      const auto s0 = __builtin_amdgcn_permlane16_swap(pk(v[0][0], v[0][1]), pk(v[1][0], v[1][1]), false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(pk(v[0][2], v[0][3]), pk(v[1][2], v[1][3]), false, false);
+      *reinterpret_cast<uint4*>(yp + (long)pf * 16 * a.ldy) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+    if (a.stats && (it % C64_G) == C64_G - 1) {
+      // record (block, 8-iteration group, wave row): lanes 0-3 of a 16-lane row store the 4
+      // channel sums, lanes 4-7 the squares (conv_epilogue's record layout)
+      const int rec = rec0 + (it / C64_G) * 4 + rw;
+#pragma unroll
+      for (int cf = 0; cf < 2; ++cf) {
+        float sv[4], qv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sv[i] = row16_sum(st[cf][i]);
+          qv[i] = row16_sum(sq[cf][i]);
+          st[cf][i] = sq[cf][i] = 0.f;
+        }
+        const int cb = cw + cf * 16 + lh * 4, ii = lr & 3;
+        const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
+        const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
+        const float val = lr < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
+        if (lr < 8) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // 7x7 conv with a 64-channel input and <= 4 output channels (Generator.out_conv 64 -> 3,
 // models.py:1099 + sigmoid 1110), "column taps in N": for every input pixel w' of a row the
 // block computes D[h][w'][(co, s)] = sum_{r, ci} x[h + r - 3][w'][ci] * W[co][ci][r][s]
@@ -3562,6 +3729,21 @@ static bool use_c74(const fv_conv_desc* fd) {
   return halo_tr(fd) == 4 && fd->cin == 8 && fd->cin_valid <= 4 && fd->cout == 64 && fd->ldy == 64 &&
          !fd->epi_sigmoid && !fd->out_nchw_f32;
 }
+// the launch of forward-conv descriptor fd runs conv3c64_fwd (64 input channels, sliding band,
+// weights in registers; plain [co][Kpad] weights)
+static bool use_c64(const fv_conv_desc* fd) {
+  return fd->dtype == FV_BF16 && fd->ksize == 3 && !fd->upsample && !fd->pro_act && fd->cin == 64 &&
+         fd->cin_valid == 64 && fd->cout % 64 == 0 && fd->ldy % 8 == 0 && !fd->epi_sigmoid && !fd->out_nchw_f32 &&
+         fd->w % 64 == 0 && fd->h % 32 == 0 && (long)fd->n * fd->h * fd->w * 64 * 2 < (1L << 31) &&
+         (long)fd->n * fd->h * fd->w * fd->ldy * 2 < (1L << 31);
+}
+// bands per (image, strip, 64-channel group): about one block per CU, bands of 32k rows
+static int c64_bands(const fv_conv_desc* d) {
+  const long base = (long)d->n * (d->w / 64) * (d->cout / 64);
+  int nb = 1;
+  while (base * nb < 256 && d->h % (nb * 64) == 0) nb *= 2;
+  return nb;
+}
 static FwdTile plan_tile(const fv_conv_desc* d) {
   const int tr = halo_tr(d);
   if (tr) return {d->cout <= 16 ? 16 : 64, tr * 64};
@@ -3572,6 +3754,7 @@ static FwdTile plan_tile(const fv_conv_desc* d) {
 static int stats_record_pixels(const fv_conv_desc* d) {
   if (use_c7n(d)) return 64;                                  // one 64-pixel row segment
   if (use_c74(d)) return C74_TR * 64;                         // one record per tile
+  if (use_c64(d)) return C64_G * 64;                          // 8 iterations x one wave's row
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
   const FwdTile t = plan_tile(d);
   if (const int bn = halo3_bn(d)) return bn == 256 ? 128 : 64;   // RM * 16 pixels per wave row
@@ -3598,7 +3781,7 @@ static fv_conv_desc dgrad_desc(const fv_conv_desc* d);
 // conv3_halo_fwd3 / fwd2), whose weights are prepared stage-major (weight_prep_body smaj) with
 // wk_rows(fd) rows per tap unit
 static bool h3s_layout(const fv_conv_desc* fd) {
-  return !use_c7n(fd) && !halo_tr(fd) && !use_subpix(fd) && halo3_bn(fd) != 0;
+  return !use_c7n(fd) && !halo_tr(fd) && !use_subpix(fd) && !use_c64(fd) && halo3_bn(fd) != 0;
 }
 static int wk_rows(const fv_conv_desc* fd) {
   const FwdTile t = fwd_tile(fd->cout);
@@ -3740,7 +3923,7 @@ int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* con
 // record, 0 when that path has none.  The halo-staged 3x3 kernels only: 256-pixel tiles of 8
 // waves (co tiles of 256 / 128) or 4 waves (co tiles of 64), one record per (tile, wave).
 static int sr_geometry(const fv_conv_desc* d, int* bp) {
-  if (d->dtype != FV_BF16 || use_c7n(d) || halo_tr(d) || use_subpix(d)) return 0;
+  if (d->dtype != FV_BF16 || use_c7n(d) || halo_tr(d) || use_subpix(d) || use_c64(d)) return 0;
   const int bn = halo3_bn(d);
   const long P = (long)d->n * d->h * d->w;
   if (!bn || d->cout % bn || P % 256) return 0;
@@ -3784,6 +3967,14 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     const int nblk = d->n * (d->h / band) * (d->w / 64);
     hipLaunchKernelGGL(conv7_n3_fwd2, dim3(nblk), dim3(512), 0, s, a, xb, band);
     return fv_check_launch("conv2d_fwd_c7n2");
+  }
+  if (use_c64(d)) {
+    FV_REQUIRE(!res && !a.spm, "64-channel band conv: no residual / store-pass records");
+    const int nb = c64_bands(d);
+    const int nblk = d->n * (d->w / 64) * (d->cout / 64) * nb;
+    const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
+    hipLaunchKernelGGL(conv3c64_fwd, dim3(nblk), dim3(512), 0, s, a, xb, nb);
+    return fv_check_launch("conv2d_fwd_c64");
   }
   if (use_c74(d)) {
     FV_REQUIRE(!res, "packed 7x7 conv: no residual");
