@@ -211,6 +211,10 @@ class ResBlock2D(_Block):
         if rec is not None:
             out._fv_bnrec = rec + (out._version,)     # the next ResBlock's bn1 statistics
             self._fv_out_rec = None
+        q8 = getattr(self, "_fv_q8_consumer", None)
+        if q8 is not None:
+            out._fv_q8_consumer = q8                  # fp8: the conv consuming out's gradient
+            self._fv_q8_consumer = None
         return out
 
 

@@ -828,6 +828,12 @@ class ResBlockFn(torch.autograd.Function):
             blk._fv_out_rec = None
         cs1.release()
         cs2.release()
+        # fp8: the gradient of out is the next ResBlock's bn1-backward output; that pass writes
+        # its e4m3 copy for this conv2's data gradient (`_fv_q8_consumer`, ResBlock2D.forward
+        # tags out with it), and this block does the same for the block before it
+        blk._fv_q8_consumer = (c2, fp8_site(c2, "dy", x.device)) if cs2.fp8 else None
+        prev = getattr(x, "_fv_q8_consumer", None)
+        ctx.q8_prev = prev if cs1.fp8 and xb is x else None
         ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm = blk, cs1, cs2, r1, r2, comm
         ctx.save_for_backward(x, xb, t1, a1, a2)
         return out
@@ -841,11 +847,18 @@ class ResBlockFn(torch.autograd.Function):
         # (the BN-backward sums stay a separate pass here: fused into the 256-channel dgrad's
         # store pass they cost that kernel +29 us per launch against the pass's 27 us,
         # profiles/r2b_*)
-        da2, dw2, db2 = conv_backward(cs2, a2, dout, C)
+        # the e4m3 copy of dout, if the next block's bn1 backward wrote one for exactly this tensor
+        pend = cs2.conv.__dict__.pop("_fv_fp8_pending", None) if cs2.fp8 else None
+        dy8 = pend[1] if pend is not None and pend[0] == dout.data_ptr() else None
+        da2, dw2, db2 = conv_backward(cs2, a2, dout, C, dy8=dy8)
         site1 = fp8_site(cs1.conv, "dy", xb.device) if cs1.fp8 else None
         dt1, dg2, dbe2, *q = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, q8=site1)
         da1, dw1, db1 = conv_backward(cs1, a1, dt1, C, dy8=q[0] if q else None)
-        dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout)
+        prev = ctx.q8_prev
+        dxb, dg1, dbe1, *q = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout,
+                                             q8=prev[1] if prev is not None else None)
+        if prev is not None and q and q[0] is not None:
+            prev[0].__dict__["_fv_fp8_pending"] = (dxb.data_ptr(), q[0])
         dx = from_nhwc(dxb, x)
         return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None
 

@@ -259,6 +259,16 @@ class LaunchChecker:
         w = eff_weight(cs, self.dtype)
         bf = self.dtype == torch.bfloat16
         with torch.no_grad():
+            if kind in ("fwd", "dgrad") and t.get("q8") is not None:
+                # the e4m3 operand (quantized by the conv's own pass, or written by its producer:
+                # a BN pass, the next ResBlock's bn1 backward) is exactly its bf16 tensor x the
+                # delayed scale, saturated
+                q8, dq = t["q8"]
+                src = t["x"] if kind == "fwd" else t["dy"]
+                ref8 = (src.float() * (1.0 / dq.item())).clamp(-448, 448).to(torch.float8_e4m3fn)
+                ref8 = ref8.permute(0, 2, 3, 1).reshape(-1).view(torch.uint8)
+                bad = int((q8.reshape(-1) != ref8).sum().item())
+                assert bad == 0, f"{name} {kind}: fp8 operand differs from its bf16 tensor in {bad} bytes"
             if kind == "fwd" and t.get("q8") is not None:        # fp8 kernel: dequantized operands
                 x8, xdq = t["q8"]
                 N, Cp, H, W = t["x"].shape
