@@ -54,6 +54,28 @@ def test_descriptor_queries(lib_built):
     assert b"power of two" in _lib.load().fv_last_error()
 
 
+@pytest.mark.parametrize("shape", [
+    (32, 256, 256, 64, 128),    # AFE.down1 forward: the sliding-band kernel (conv3c64_fwd)
+    (8, 512, 512, 64, 128),     # the same at 512^2
+    (32, 128, 128, 128, 256),   # AFE.down2
+    (32, 64, 64, 256, 256),     # ResBlock
+    (32, 256, 256, 8, 64),      # AFE.in_conv (7x7, packed)
+])
+def test_bn_record_geometry_covers_every_pixel(lib_built, shape):
+    """BN-statistics records of a forward launch: blocks x pixels per block == N*H*W for every
+    kernel family (the host sizes the partials buffer and the fold from these two queries)."""
+    import ctypes
+    import fvamd  # noqa: F401
+    from facevae_amd import _lib, ops
+    n, h, w, cin, cout = shape
+    d = ops.desc(torch.bfloat16, n, h, w, cin, min(cin, 3) if cin == 8 else cin, cout, cout, 7 if cin == 8 else 3)
+    bp = _lib.query("fv_conv2d_stats_block_pixels", ctypes.byref(d))
+    nb = _lib.query("fv_conv2d_stats_blocks", ctypes.byref(d))
+    assert bp > 0 and nb * bp == n * h * w
+    if cin == 64:
+        assert bp == 512        # one record per (band block, 8 iterations, wave row)
+
+
 def test_state_dict_and_init_match_reference():
     import fvamd  # noqa: F401
     import facevae_amd as fv
