@@ -218,6 +218,44 @@ sum_finalize_kernel(const double* ws, int nsplit, int C, const float* gamma, con
   }
 }
 
+// single-process form for few records (<= REC_DIRECT): fold the conv's fp32 (sum, sum of
+// squares) records straight into fp64 and finalize -- partials_kernel + sum_finalize_kernel in
+// one launch (the res convs' 1024 records x 256 channels: 2 MB, read by 16 blocks).  Same
+// mapping as sum_finalize_kernel: block = 16 channels x 64 record phases.
+constexpr int REC_DIRECT = 1024;
+__global__ void __launch_bounds__(SUMT)
+rec_finalize_kernel(const float* __restrict__ part, int nrec, int bpix, long P, int C, const float* gamma,
+                    const float* beta, float eps, float mom, float* rm, float* rv, long long* nbt, float* save_mean,
+                    float* save_invstd, float* scale, float* shift) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ch = lane & 15, ph = w * 4 + (lane >> 4);
+  const int c = blockIdx.x * SUMCH + ch;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  double n = 0, S = 0, Q = 0;
+  if (c < C) {
+#pragma unroll 4
+    for (int r = ph; r < nrec; r += SUMPH) {
+      n += (double)min((long)bpix, P - (long)r * bpix);
+      S += part[(long)(2 * r) * C + c];
+      Q += part[(long)(2 * r + 1) * C + c];
+    }
+  }
+  __shared__ double red[3][SUMPH][SUMCH];
+  red[0][ph][ch] = n;
+  red[1][ph][ch] = S;
+  red[2][ph][ch] = Q;
+  __syncthreads();
+  if (threadIdx.x < SUMCH && c < C) {
+    n = S = Q = 0;
+    for (int k = 0; k < SUMPH; ++k) {
+      n += red[0][k][ch];
+      S += red[1][k][ch];
+      Q += red[2][k][ch];
+    }
+    bn_finalize_one(c, C, n, S, Q, gamma, beta, eps, mom, 1, rm, rv, save_mean, save_invstd, scale, shift);
+  }
+}
+
 // out = [pool](act(y*scale+shift)).  grid.y = output row (n*Ho + i), grid.x covers the row's
 // (pixel, 8-channel chunk) pairs: 32-bit shift/mask indexing only.
 template <typename T>
@@ -731,6 +769,12 @@ int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_
   FV_REQUIRE(partials && ws, "null pointer");
   FV_REQUIRE(nblocks > 0 && c > 0, "bad sizes");
   hipStream_t s = (hipStream_t)stream;
+  if (nblocks <= REC_DIRECT) {
+    hipLaunchKernelGGL(rec_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, partials, nblocks, block_pixels,
+                       total_pixels, c, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked,
+                       save_mean, save_invstd, scale, shift);
+    return fv_check_launch("bn_rec_finalize");
+  }
   const int ns = partial_splits(nblocks, c);
   hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), ns), dim3(NTH), 0, s, partials, nblocks,
                      block_pixels, total_pixels, c, (double*)ws);

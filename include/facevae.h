@@ -373,7 +373,8 @@ int fv_bn_finalize(const double* stats, int c, const float* gamma, const float* 
                    long long* num_batches_tracked, float* save_mean, float* save_invstd, float* scale,
                    float* shift, void* stream);
 /* single-process training forms (no SyncBN exchange between the statistics and finalize):
- * statistics + finalize (+ num_batches_tracked += 1) in two launches */
+ * statistics + finalize (+ num_batches_tracked += 1) in two launches (one when the conv wrote
+ * <= 1024 records) */
 int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_pixels, long total_pixels,
                                   int c, const float* gamma, const float* beta, float eps, float momentum,
                                   float* running_mean, float* running_var, long long* num_batches_tracked,
