@@ -128,9 +128,15 @@ def pmc_counters(cfg, B, dtype, fam, avg_ms):
     out = {"pmc_source": "profiles/r3_pmc.json (" + dom["kernel"] + ")"}
     if "hbm_bytes_per_launch" in dom:
         t = dom["hbm_bytes_per_launch"]
+        act = B * cfg.latent_hw ** 2 * cfg.up_seq[0] * 2          # one bf16 activation of the res stack
+        # forward launches of the family: Generator.in_conv + 2 per ResBlock; the second conv of
+        # each ResBlock also reads the residual input (n_res of the 2 n_res + 1 launches)
+        res_share = cfg.n_res / (2 * cfg.n_res + 1)
         out.update({"traffic": round(t), "traffic_unit": "bytes/launch (PMC)",
                     "traffic_gbs_at_avg": round(t / (avg_ms * 1e-3) / 1e9, 1),
-                    "algorithmic_bytes": 2 * (B * cfg.latent_hw ** 2 * cfg.up_seq[0] * 2) + cfg.up_seq[0] ** 2 * 9 * 2})
+                    "algorithmic_bytes": round(2 * act + res_share * act + cfg.up_seq[0] ** 2 * 9 * 2),
+                    "algorithmic_bytes_what": "input + output + weights per launch, + the residual input "
+                                              f"averaged over the family ({cfg.n_res} of {2 * cfg.n_res + 1} launches)"})
     if "mfma_busy_frac" in dom:
         out.update({"mfma_busy_counter": round(dom["mfma_busy_frac"], 4),
                     "eff_clock_ghz": round(dom["eff_clock_ghz"], 3) if dom.get("eff_clock_ghz") else None})
@@ -250,6 +256,13 @@ def main():
     _, f_img = flops_per_image(OracleConfig(H=cfg.H, down_seq=cfg.down_seq, latent=cfg.latent,
                                             n_res=cfg.n_res, up_seq=cfg.up_seq))
     step_util = ips / world * f_img / (peak * 1e12)
+    # sub-pixel shortcut (flag it): the two UpBlock2D convs run nearest-x2 upsample
+    # + 3x3 as 4 phases of a 2x2 conv at the low resolution (forward, data and weight gradient),
+    # executing 4/9 of the reference MACs; utilisation above is on reference FLOPs
+    subpix = dtype != torch.float32 and os.environ.get("FV_DISABLE_SUBPIX", "0") != "1"
+    f_up = sum(2.0 * (cfg.H // 2 ** (len(cfg.up_seq) - 2 - i)) ** 2 * cfg.up_seq[i] * cfg.up_seq[i + 1] * 9
+               for i in range(len(cfg.up_seq) - 1))        # forward FLOPs of the up convs per image
+    f_exec = f_img - (5.0 / 9.0) * 3 * f_up if subpix else f_img
     out = {
         "metric": "training images/sec (256x256 face-VAE step)" if cfg.H == 256 else
                   f"training images/sec ({cfg.H}x{cfg.H} face-VAE step)",
@@ -263,6 +276,10 @@ def main():
         "launch": "hip graph (one captured step replayed)" if use_graph else "eager",
         "mfma_util_step": round(step_util, 4),
         "step_flop_per_image": f_img,
+        "subpixel_shortcut": {"active": subpix, "executed_flop_per_image": f_exec,
+                              "mfma_util_step_executed": round(ips / world * f_exec / (peak * 1e12), 4),
+                              "what": "UpBlock2D upsample+3x3 as 4 low-res 2x2 phases (fwd, dgrad, wgrad): 4/9 of "
+                                      "the reference MACs; mfma_util_step is on reference FLOPs"},
         "roofline": roof,
         "cpu_baseline": None,
         "parity": None,

@@ -11,20 +11,8 @@
 
 namespace {
 
-constexpr int NSPLIT = 128;   // level-1 splits of the conv-partials reduction
 constexpr int MAXBLK = 1024;  // max blocks (= level-1 records) of the streaming reductions
 constexpr int NTH = 256;
-
-// level-1 splits of the conv-partials reduction: enough blocks to cover the chip (>= 1024 over
-// all channel groups) with >= 16 records per split; <= MAXBLK (the ws size)
-int partial_splits(int nb, int c) {
-  int ns = 1024 / ((c + 63) / 64);
-  if (ns < NSPLIT) ns = NSPLIT;
-  const int by_records = (nb + 15) / 16;
-  if (ns > by_records) ns = by_records;
-  if (ns < 1) ns = 1;
-  return ns > MAXBLK ? MAXBLK : ns;
-}
 
 // blocks of a streaming per-channel reduction over `pixels` x (C/8) chunks: >= 8 chunks per thread
 int stream_blocks(long pixels, int C) {
@@ -47,38 +35,6 @@ __device__ __forceinline__ void st8(T* p, const float* f) {
   Chunk8<T> c;
   c.set8(f);
   c.store(p);
-}
-
-// conv per-record (sum, sum of squares) partials -> ws [split][3][C] (n, S, Q) in fp64
-__global__ void partials_kernel(const float* __restrict__ part, int nb, int bpix, long P, int C,
-                                double* ws) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int r = threadIdx.x >> 6;
-  const int split = blockIdx.y;
-  const int per = (nb + gridDim.y - 1) / gridDim.y;
-  const int b0 = split * per, b1 = min(nb, b0 + per);
-  double n = 0, S = 0, Q = 0;
-  if (c < C) {
-#pragma unroll 8
-    for (int b = b0 + r; b < b1; b += 4) {
-      const double nb_ = (double)min((long)bpix, P - (long)b * bpix);
-      n += nb_;
-      S += part[(long)(2 * b) * C + c];
-      Q += part[(long)(2 * b + 1) * C + c];
-    }
-  }
-  __shared__ double red[3][4][64];
-  red[0][r][threadIdx.x & 63] = n;
-  red[1][r][threadIdx.x & 63] = S;
-  red[2][r][threadIdx.x & 63] = Q;
-  __syncthreads();
-  if (r == 0 && c < C) {
-    for (int j = 0; j < 3; ++j) {
-      double t = 0;
-      for (int k = 0; k < 4; ++k) t += red[j][k][threadIdx.x];
-      ws[((long)split * 3 + j) * C + c] = t;
-    }
-  }
 }
 
 // streaming statistics of x [P][ldc] -> ws [block][3][C]; thread = (pixel row, 8-channel group)
@@ -124,25 +80,6 @@ __global__ void tensor_stats_kernel(const T* __restrict__ x, long P, int C, int 
   }
 }
 
-// out[i] = sum_s ws[s][i], i < rec*C : one wave per output (lanes stride the splits), 4 per block
-__global__ void sum_splits_kernel(const double* ws, int nsplit, int rec, int C, double* out) {
-  const int n = rec * C;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (i >= n) return;
-  double t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-  int s = lane;
-  for (; s + 192 < nsplit; s += 256) {
-    t0 += ws[(long)s * n + i];
-    t1 += ws[(long)(s + 64) * n + i];
-    t2 += ws[(long)(s + 128) * n + i];
-    t3 += ws[(long)(s + 192) * n + i];
-  }
-  for (; s < nsplit; s += 64) t0 += ws[(long)s * n + i];
-  const double t = wave_sum_d((t0 + t1) + (t2 + t3));
-  if (lane == 0) out[i] = t;
-}
-
 // mean / invstd / fused affine / running statistics of one channel from (n, S, Q)
 __device__ __forceinline__ void bn_finalize_one(int c, int C, double n, double S, double Q, const float* gamma,
                                                 const float* beta, float eps, float mom, int training, float* rm,
@@ -178,82 +115,97 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
   bn_finalize_one(c, C, n, S, Q, gamma, beta, eps, mom, training, rm, rv, save_mean, save_invstd, scale, shift);
 }
 
-// single-process form: sum the level-1 records [split][3][C] over the splits and finalize, one
-// wave per channel (replaces sum_splits + finalize + the num_batches_tracked increment)
-// sum the level-1 records [split][3][C] and finalize.  Block = 16 channels x 64 split phases
-// (1024 threads: lane = (channel, phase & 3), wave = phase >> 2), so one load instruction
-// reads 4 split rows x 128 contiguous bytes; fixed-order LDS combine of the 64 phases.
-constexpr int SUMT = 1024, SUMCH = 16, SUMPH = SUMT / SUMCH;
-__global__ void __launch_bounds__(SUMT)
-sum_finalize_kernel(const double* ws, int nsplit, int C, const float* gamma, const float* beta,
-                    float eps, float mom, float* rm, float* rv, long long* nbt, float* save_mean,
-                    float* save_invstd, float* scale, float* shift) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ch = lane & 15, ph = w * 4 + (lane >> 4);
-  const int c = blockIdx.x * SUMCH + ch;
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
-  double n = 0, S = 0, Q = 0;
-  if (c < C) {
-#pragma unroll 4
-    for (int sp = ph; sp < nsplit; sp += SUMPH) {
-      const double* r = ws + (long)sp * 3 * C + c;
-      n += r[0];
-      S += r[C];
-      Q += r[2 * C];
-    }
+// ---------------------------------------------------------------------------------------------
+// Record folds (+ finalize): the per-channel sums of a BN layer arrive as `nrec` rows of partial
+// sums -- fp32 (sum, sum of squares) records of a conv epilogue / store pass ([r][2][C]), or the
+// fp64 per-block rows of a streaming pass ([b][3][C] with a count row, [b][2][C] backward sums).
+// ONE launch folds them and finishes the layer: grid = C blocks of 1024 threads, one channel per
+// block, so a fold of up to ~16k records is one round of loads on (up to) every CU (the previous
+// two-level partials -> sum_finalize pair ran on C/16 blocks: 6.7 + 8.9 us per layer, latency
+// bound).  Fixed order: thread t sums rows t, t + 1024, ... in order, then a fixed xor tree per
+// wave and the 16 wave sums in wave order -> bit-reproducible.
+// ---------------------------------------------------------------------------------------------
+constexpr int FOLDT = 1024;
+enum { FOLD_STATS = 0, FOLD_FWD = 1, FOLD_BWD = 2 };
+struct FoldArgs {
+  const void* src;
+  int nrec, C;
+  long rstride;              // elements between rows
+  long P;                    // element count per channel when the rows carry none (NV = 2 forward)
+  // FOLD_STATS: the fp64 [3][C] (n, S, Q) record (the SyncBN all-reduce payload)
+  double* stats;
+  // FOLD_FWD: finalize (bn_finalize_one)
+  const float *gamma, *beta;
+  float eps, mom;
+  float *rm, *rv;
+  long long* nbt;
+  float *save_mean, *save_invstd, *scale, *shift;
+  // FOLD_BWD: dbeta = sum g, dgamma = sum g*yhat (rank-local), k = (sums) / count (count > 0),
+  // red = the fp64 [2][C] sums (SyncBN payload), each optional
+  double count;
+  float *dgamma, *dbeta, *k;
+  double* red;
+};
+
+template <typename T, int NV, int MODE>
+__global__ void __launch_bounds__(FOLDT) fold_kernel(FoldArgs a) {
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const T* src = reinterpret_cast<const T*>(a.src) + c;
+  const long vs = a.C;
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+#pragma unroll 8
+  for (int r = tid; r < a.nrec; r += FOLDT) {
+    const T* p = src + (long)r * a.rstride;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] += (double)p[v * vs];
   }
-  __shared__ double red[3][SUMPH][SUMCH];
-  red[0][ph][ch] = n;
-  red[1][ph][ch] = S;
-  red[2][ph][ch] = Q;
+  __shared__ double red[NV][FOLDT / 64];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double t = wave_sum_d(acc[v]);
+    if (lane == 0) red[v][w] = t;
+  }
   __syncthreads();
-  if (threadIdx.x < SUMCH && c < C) {
-    n = S = Q = 0;
-    for (int k = 0; k < SUMPH; ++k) {
-      n += red[0][k][ch];
-      S += red[1][k][ch];
-      Q += red[2][k][ch];
+  if (tid != 0) return;
+  double tot[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double t = 0.0;
+    for (int j = 0; j < FOLDT / 64; ++j) t += red[v][j];
+    tot[v] = t;
+  }
+  // (n, S, Q): rows with a count row carry it first; fp32 records are counted by P
+  const double n = NV == 3 ? tot[0] : (double)a.P;
+  const double S = tot[NV - 2], Q = tot[NV - 1];
+  if constexpr (MODE == FOLD_STATS) {
+    a.stats[c] = n;
+    a.stats[a.C + c] = S;
+    a.stats[2 * a.C + c] = Q;
+  } else if constexpr (MODE == FOLD_FWD) {
+    if (a.nbt && c == 0) a.nbt[0] += 1;
+    bn_finalize_one(c, a.C, n, S, Q, a.gamma, a.beta, a.eps, a.mom, 1, a.rm, a.rv, a.save_mean, a.save_invstd,
+                    a.scale, a.shift);
+  } else {
+    // backward rows are (sum g, sum g * yhat)
+    if (a.dbeta) a.dbeta[c] = (float)S;
+    if (a.dgamma) a.dgamma[c] = (float)Q;
+    if (a.k && a.count > 0) {
+      a.k[c] = (float)(S / a.count);
+      a.k[a.C + c] = (float)(Q / a.count);
     }
-    bn_finalize_one(c, C, n, S, Q, gamma, beta, eps, mom, 1, rm, rv, save_mean, save_invstd, scale, shift);
+    if (a.red) {
+      a.red[c] = S;
+      a.red[a.C + c] = Q;
+    }
   }
 }
 
-// single-process form for few records (<= REC_DIRECT): fold the conv's fp32 (sum, sum of
-// squares) records straight into fp64 and finalize -- partials_kernel + sum_finalize_kernel in
-// one launch (the res convs' 1024 records x 256 channels: 2 MB, read by 16 blocks).  Same
-// mapping as sum_finalize_kernel: block = 16 channels x 64 record phases.
-constexpr int REC_DIRECT = 1024;
-__global__ void __launch_bounds__(SUMT)
-rec_finalize_kernel(const float* __restrict__ part, int nrec, int bpix, long P, int C, const float* gamma,
-                    const float* beta, float eps, float mom, float* rm, float* rv, long long* nbt, float* save_mean,
-                    float* save_invstd, float* scale, float* shift) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ch = lane & 15, ph = w * 4 + (lane >> 4);
-  const int c = blockIdx.x * SUMCH + ch;
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
-  double n = 0, S = 0, Q = 0;
-  if (c < C) {
-#pragma unroll 4
-    for (int r = ph; r < nrec; r += SUMPH) {
-      n += (double)min((long)bpix, P - (long)r * bpix);
-      S += part[(long)(2 * r) * C + c];
-      Q += part[(long)(2 * r + 1) * C + c];
-    }
-  }
-  __shared__ double red[3][SUMPH][SUMCH];
-  red[0][ph][ch] = n;
-  red[1][ph][ch] = S;
-  red[2][ph][ch] = Q;
-  __syncthreads();
-  if (threadIdx.x < SUMCH && c < C) {
-    n = S = Q = 0;
-    for (int k = 0; k < SUMPH; ++k) {
-      n += red[0][k][ch];
-      S += red[1][k][ch];
-      Q += red[2][k][ch];
-    }
-    bn_finalize_one(c, C, n, S, Q, gamma, beta, eps, mom, 1, rm, rv, save_mean, save_invstd, scale, shift);
-  }
+template <typename T, int NV, int MODE>
+int launch_fold(const FoldArgs& a, hipStream_t s, const char* what) {
+  hipLaunchKernelGGL((fold_kernel<T, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, a);
+  return fv_check_launch(what);
 }
 
 // out = [pool](act(y*scale+shift)).  grid.y = output row (n*Ho + i), grid.x covers the row's
@@ -546,38 +498,6 @@ __global__ void bwd_finalize_kernel(const double* red, int C, double count, cons
   }
 }
 
-// single-process form: sum the level-1 records [split][2][C] and finalize (mapping of
-// sum_finalize_kernel)
-__global__ void __launch_bounds__(SUMT)
-bwd_sum_finalize_kernel(const double* ws, int nsplit, int C, double count, float* dgamma, float* dbeta, float* k) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ch = lane & 15, ph = w * 4 + (lane >> 4);
-  const int c = blockIdx.x * SUMCH + ch;
-  double sg = 0, sgy = 0;
-  if (c < C) {
-#pragma unroll 4
-    for (int sp = ph; sp < nsplit; sp += SUMPH) {
-      sg += ws[(long)sp * 2 * C + c];
-      sgy += ws[(long)sp * 2 * C + C + c];
-    }
-  }
-  __shared__ double red[2][SUMPH][SUMCH];
-  red[0][ph][ch] = sg;
-  red[1][ph][ch] = sgy;
-  __syncthreads();
-  if (threadIdx.x < SUMCH && c < C) {
-    sg = sgy = 0;
-    for (int j = 0; j < SUMPH; ++j) {
-      sg += red[0][j][ch];
-      sgy += red[1][j][ch];
-    }
-    if (dbeta) dbeta[c] = (float)sg;
-    if (dgamma) dgamma[c] = (float)sgy;
-    k[c] = (float)(sg / count);
-    k[C + c] = (float)(sgy / count);
-  }
-}
-
 // dx = gamma*invstd*(g - k0 - yhat*k1) [+ addend]; thread = (pixel, 8-channel chunk), the
 // grid stride is a multiple of C/8 so each thread keeps one chunk's parameters in registers
 template <typename T>
@@ -656,25 +576,6 @@ __global__ void __launch_bounds__(NTH) act_bwd_apply_q8_kernel(
   q8_block_amax(m, st);
 }
 
-// BN backward from the [3][C] (count, sum g, sum g*yhat) totals of store-pass records
-__global__ void bwd_from_stats_kernel(const double* st, int C, double count, float* dgamma, float* dbeta, float* k,
-                                      double* red) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const double sg = st[C + c], sgy = st[2 * C + c];
-  if (dbeta) dbeta[c] = (float)sg;
-  if (dgamma) dgamma[c] = (float)sgy;
-  if (k && count > 0) {
-    k[c] = (float)(sg / count);
-    k[C + c] = (float)(sgy / count);
-  }
-  if (red) {
-    red[c] = sg;
-    red[C + c] = sgy;
-  }
-}
-
-
 int grid_for(long work, int cap = 8192) {
   long g = (work + NTH - 1) / NTH;
   if (g < 1) g = 1;
@@ -699,34 +600,20 @@ int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixe
                               int c, double* stats, void* ws, void* stream) {
   FV_REQUIRE(partials && stats && ws, "null pointer");
   FV_REQUIRE(nblocks > 0 && c > 0, "bad sizes");
-  hipStream_t s = (hipStream_t)stream;
-  const int ns = partial_splits(nblocks, c);
-  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), ns), dim3(NTH), 0, s, partials, nblocks,
-                     block_pixels, total_pixels, c, (double*)ws);
-  int st = fv_check_launch("bn_partials");
-  if (st) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 4)), dim3(NTH), 0, s, (const double*)ws, ns,
-                     3, c, stats);
-  return fv_check_launch("bn_sum_splits");
+  FV_REQUIRE((long)nblocks * block_pixels >= total_pixels, "bn_stats_from_partials: records do not cover the pixels");
+  FoldArgs a{};
+  a.src = partials; a.nrec = nblocks; a.C = c; a.rstride = 2L * c; a.P = total_pixels; a.stats = stats;
+  return launch_fold<float, 2, FOLD_STATS>(a, (hipStream_t)stream, "bn_fold_stats");
 }
 
 int fv_bn_bwd_from_records(const float* records, int nrec, int record_pixels, long pixels, int c, long count,
                            float* dgamma, float* dbeta, float* k, double* red, void* ws, void* stream) {
   FV_REQUIRE(records && ws && nrec > 0 && c > 0 && (long)nrec * record_pixels == pixels,
              "bn_bwd_from_records: bad arguments");
-  hipStream_t s = (hipStream_t)stream;
-  int ns = partial_splits(nrec, c);
-  if (ns > MAXBLK - 1) ns = MAXBLK - 1;
-  double* tot = (double*)ws + (long)(MAXBLK - 1) * 3 * c;
-  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), ns), dim3(NTH), 0, s, records, nrec, record_pixels, pixels,
-                     c, (double*)ws);
-  int st = fv_check_launch("bn_bwd_records_partials");
-  if (st) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 4)), dim3(NTH), 0, s, (const double*)ws, ns, 3, c, tot);
-  if ((st = fv_check_launch("bn_bwd_records_sum"))) return st;
-  hipLaunchKernelGGL(bwd_from_stats_kernel, dim3(fv_cdiv(c, NTH)), dim3(NTH), 0, s, (const double*)tot, c,
-                     (double)count, dgamma, dbeta, k, red);
-  return fv_check_launch("bn_bwd_records_finalize");
+  FoldArgs a{};
+  a.src = records; a.nrec = nrec; a.C = c; a.rstride = 2L * c;
+  a.count = (double)count; a.dgamma = dgamma; a.dbeta = dbeta; a.k = k; a.red = red;
+  return launch_fold<float, 2, FOLD_BWD>(a, (hipStream_t)stream, "bn_bwd_fold_records");
 }
 
 int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, double* stats, void* ws,
@@ -743,9 +630,9 @@ int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, do
     hipLaunchKernelGGL(tensor_stats_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)x, pixels, c, ldc,
                        (double*)ws);
   if ((st = fv_check_launch("bn_tensor_stats"))) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(3 * c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, 3, c,
-                     stats);
-  return fv_check_launch("bn_sum_splits");
+  FoldArgs a{};
+  a.src = ws; a.nrec = nb; a.C = c; a.rstride = 3L * c; a.stats = stats;
+  return launch_fold<double, 3, FOLD_STATS>(a, s, "bn_fold_tensor_stats");
 }
 
 int fv_bn_finalize(const double* stats, int c, const float* gamma, const float* beta, float eps,
@@ -766,24 +653,15 @@ int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_
                                   float* running_mean, float* running_var, long long* num_batches_tracked,
                                   float* save_mean, float* save_invstd, float* scale, float* shift, void* ws,
                                   void* stream) {
-  FV_REQUIRE(partials && ws, "null pointer");
+  FV_REQUIRE(partials, "null pointer");
   FV_REQUIRE(nblocks > 0 && c > 0, "bad sizes");
-  hipStream_t s = (hipStream_t)stream;
-  if (nblocks <= REC_DIRECT) {
-    hipLaunchKernelGGL(rec_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, partials, nblocks, block_pixels,
-                       total_pixels, c, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked,
-                       save_mean, save_invstd, scale, shift);
-    return fv_check_launch("bn_rec_finalize");
-  }
-  const int ns = partial_splits(nblocks, c);
-  hipLaunchKernelGGL(partials_kernel, dim3(fv_cdiv(c, 64), ns), dim3(NTH), 0, s, partials, nblocks,
-                     block_pixels, total_pixels, c, (double*)ws);
-  int st = fv_check_launch("bn_partials");
-  if (st) return st;
-  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, (const double*)ws, ns, c, gamma,
-                     beta, eps, momentum, running_mean, running_var, num_batches_tracked, save_mean, save_invstd,
-                     scale, shift);
-  return fv_check_launch("bn_sum_finalize");
+  FV_REQUIRE((long)nblocks * block_pixels >= total_pixels, "bn_stats_finalize_partials: records do not cover the pixels");
+  (void)ws;
+  FoldArgs a{};
+  a.src = partials; a.nrec = nblocks; a.C = c; a.rstride = 2L * c; a.P = total_pixels;
+  a.gamma = gamma; a.beta = beta; a.eps = eps; a.mom = momentum; a.rm = running_mean; a.rv = running_var;
+  a.nbt = num_batches_tracked; a.save_mean = save_mean; a.save_invstd = save_invstd; a.scale = scale; a.shift = shift;
+  return launch_fold<float, 2, FOLD_FWD>(a, (hipStream_t)stream, "bn_fold_finalize");
 }
 
 int fv_bn_stats_finalize_tensor(int dtype, const void* x, long pixels, int c, int ldc, const float* gamma,
@@ -802,10 +680,11 @@ int fv_bn_stats_finalize_tensor(int dtype, const void* x, long pixels, int c, in
     hipLaunchKernelGGL(tensor_stats_kernel<float>, dim3(nb), dim3(NTH), 0, s, (const float*)x, pixels, c, ldc,
                        (double*)ws);
   if ((st = fv_check_launch("bn_tensor_stats"))) return st;
-  hipLaunchKernelGGL(sum_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, (const double*)ws, nb, c, gamma,
-                     beta, eps, momentum, running_mean, running_var, num_batches_tracked, save_mean, save_invstd,
-                     scale, shift);
-  return fv_check_launch("bn_sum_finalize");
+  FoldArgs a{};
+  a.src = ws; a.nrec = nb; a.C = c; a.rstride = 3L * c;
+  a.gamma = gamma; a.beta = beta; a.eps = eps; a.mom = momentum; a.rm = running_mean; a.rv = running_var;
+  a.nbt = num_batches_tracked; a.save_mean = save_mean; a.save_invstd = save_invstd; a.scale = scale; a.shift = shift;
+  return launch_fold<double, 3, FOLD_FWD>(a, s, "bn_fold_tensor_finalize");
 }
 
 int fv_bn_act_fwd(int dtype, const void* y, int n, int h, int w, int c, int ldc, const float* scale,
@@ -858,9 +737,9 @@ int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int 
                          (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   }
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(fv_cdiv(2 * c, 4)), dim3(NTH), 0, s, (const double*)ws, nb, 2, c,
-                     red);
-  return fv_check_launch("bn_sum_splits");
+  FoldArgs a{};
+  a.src = ws; a.nrec = nb; a.C = c; a.rstride = 2L * c; a.red = red;
+  return launch_fold<double, 2, FOLD_BWD>(a, s, "bn_bwd_fold");
 }
 
 int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, int n, int h, int w, int c,
@@ -895,9 +774,10 @@ int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, in
                          (const float*)y, P, fw, w, c, ldc, mean, invstd, gamma, beta, slope, pool, (double*)ws);
   }
   if ((st = fv_check_launch("bn_bwd_reduce"))) return st;
-  hipLaunchKernelGGL(bwd_sum_finalize_kernel, dim3(fv_cdiv(c, SUMCH)), dim3(SUMT), 0, s, (const double*)ws, nb, c,
-                     (double)count, dgamma, dbeta, k);
-  return fv_check_launch("bn_bwd_sum_finalize");
+  FoldArgs a{};
+  a.src = ws; a.nrec = nb; a.C = c; a.rstride = 2L * c;
+  a.count = (double)count; a.dgamma = dgamma; a.dbeta = dbeta; a.k = k;
+  return launch_fold<double, 2, FOLD_BWD>(a, s, "bn_bwd_fold_finalize");
 }
 
 int fv_bn_bwd_finalize(const double* red, int c, long count, float* dgamma, float* dbeta, float* k,

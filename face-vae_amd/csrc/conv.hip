@@ -3968,8 +3968,10 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     hipLaunchKernelGGL(conv7_n3_fwd2, dim3(nblk), dim3(512), 0, s, a, xb, band);
     return fv_check_launch("conv2d_fwd_c7n2");
   }
-  if (use_c64(d)) {
-    FV_REQUIRE(!res && !a.spm, "64-channel band conv: no residual / store-pass records");
+  // the 64-channel band kernel has no residual / store-pass epilogue: such a launch (a 64-channel
+  // ResBlock conv) runs conv_fwd_v2, which reads the same plain [co][Kpad] weights (lay_of)
+  const bool c64 = use_c64(d);
+  if (c64 && !res && !a.spm) {
     const int nb = c64_bands(d);
     const int nblk = d->n * (d->w / 64) * (d->cout / 64) * nb;
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
@@ -4013,7 +4015,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     }
     return fv_check_launch("conv2d_fwd_subpix");
   }
-  if (const int bn = halo3_bn(d)) {
+  if (const int bn = c64 ? 0 : halo3_bn(d)) {
     FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");
     a.lgtw = 6;
     a.wus = wk_rows(d) * 64;

@@ -8,7 +8,8 @@ indices into the folder's `os.listdir` order, dataset.py:102-105), returned as `
 driving, source_aug, driving_aug)` float32 CHW arrays in [0, 1] (dataset.py:91-129); a
 test-split item is the whole video, frames sorted by name (read_video, dataset.py:20-23).
 Frames are decoded with PIL (skimage / imageio are not in this image; for uint8 PNGs
-`img_as_float32` is the same division by 255).  The `*_aug` items go through
+`img_as_float32` is `np.multiply(x, 1. / 255, dtype=np.float32)`, i.e. x times the fp32
+reciprocal of 255 -- NOT x / 255, which differs in the last bit for 126 of the 256 values).  The `*_aug` items go through
 `augmentation.AllAugmentationTransform` with the reference's default parameters (rotation
 30 degrees, perspective (30, 40), colour jitter 0.1, dataset.py:52-57), each frame on its own
 as dataset.py:122-123; they feed the keypoint / contrastive losses, not the FaceVAE path.
@@ -19,7 +20,7 @@ DataLoader's worker IPC and collate).  `output="driving_uint8"` is the FaceVAE f
 is the `driving` frame alone (the same two random draws, so the same frame as the reference
 item's `driving`; `source` is not decoded -- the FaceVAE step never reads it).
 `to_device_frames` turns a collated uint8 batch into the float32 NCHW [0, 1] tensor on the
-GPU -- x / 255 in fp32, bit-identical to img_as_float32 on the CPU.
+GPU -- x times fp32(1/255), bit-identical to img_as_float32 on the CPU (`u8_to_float`).
 
 `PairedDataset` is dataset.py:154-193 (source / driving pairs for animation), and
 `SyntheticFramesDataset` produces VoxCeleb-shaped frames x ~ U[0, 1) deterministically per
@@ -44,8 +45,18 @@ def _read_frame_u8(path: str) -> np.ndarray:
         return np.asarray(im)
 
 
+# skimage.util.img_as_float32 on uint8 (skimage/util/dtype.py `_convert`: unsigned -> float
+# multiplies by 1. / imax_in with dtype=float32, so the reciprocal is rounded to fp32 first)
+INV255 = np.float32(1.0 / 255.0)
+
+
+def u8_to_float(a: np.ndarray) -> np.ndarray:
+    """img_as_float32 of a uint8 array."""
+    return np.multiply(a, INV255, dtype=np.float32)
+
+
 def _read_frame(path: str) -> np.ndarray:
-    return _read_frame_u8(path).astype(np.float32) / 255.0
+    return u8_to_float(_read_frame_u8(path))
 
 
 def _read_gif_u8(path: str) -> np.ndarray:
@@ -72,11 +83,11 @@ def read_video_u8(name: str) -> np.ndarray:
 
 def to_device_frames(t, device="cuda") -> "torch.Tensor":
     """A collated batch of frames -> float32 NCHW on `device`: uint8 (output="uint8") is moved
-    as bytes and divided by 255 there; float32 is moved as is."""
+    as bytes and converted there (x * fp32(1/255), as u8_to_float); float32 is moved as is."""
     import torch
     t = torch.as_tensor(t)
     if t.dtype == torch.uint8:
-        return t.to(device, non_blocking=True).float().div_(255.0)
+        return t.to(device, non_blocking=True).float().mul_(float(INV255))
     return t.to(device, non_blocking=True)
 
 
@@ -151,7 +162,7 @@ class FramesDataset(Dataset):
                 return (np.ascontiguousarray(arr[0].transpose(2, 0, 1)),
                         np.ascontiguousarray(arr[1].transpose(2, 0, 1)))
             return np.ascontiguousarray(np.asarray(arr).transpose(3, 0, 1, 2))
-        arr = [a.astype(np.float32) / 255.0 for a in arr]
+        arr = [u8_to_float(a) for a in arr]
         if self.is_train:
             source = np.ascontiguousarray(arr[0].transpose(2, 0, 1))
             driving = np.ascontiguousarray(arr[1].transpose(2, 0, 1))

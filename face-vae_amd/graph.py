@@ -54,6 +54,7 @@ class SegmentRecorder:
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs = []
         self.ops = []
+        self.open = False
 
     def begin(self):
         # relaxed: the backward's collectives (SyncBN sums, gradient buckets) run on the autograd
@@ -62,14 +63,27 @@ class SegmentRecorder:
         g = torch.cuda.CUDAGraph()
         g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
         self.graphs.append(g)
+        self.open = True
 
     def cut(self, op):
+        self.open = False
         self.graphs[-1].capture_end()
         self.ops.append(op)
         self.begin()
 
     def end(self):
+        self.open = False
         self.graphs[-1].capture_end()
+
+    def abort(self):
+        """End the segment capture an exception left open (its stream -- possibly begun on the
+        autograd thread -- would otherwise stay in capture mode and fail later GPU work)."""
+        if self.open:
+            self.open = False
+            try:
+                self.graphs[-1].capture_end()
+            except Exception:      # an invalidated capture still leaves capture mode; the original error is raised
+                pass
 
     def replay(self):
         for i, g in enumerate(self.graphs):
@@ -126,6 +140,9 @@ class StepGraph:
                         rec.begin()
                         self.out = self.step_fn()
                         rec.end()
+                except BaseException:
+                    rec.abort()
+                    raise
                 finally:
                     D._SEGMENTS = None
                 cur.wait_stream(cap)

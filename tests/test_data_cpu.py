@@ -140,7 +140,7 @@ def test_training_frames_follow_os_listdir_order(tmp_path, monkeypatch):
 
 def test_uint8_feed_matches_float32_items(tmp_path):
     """output="uint8" + to_device_frames (here on the CPU) gives the float32 frames of the
-    reference layout bit for bit (x / 255 in fp32 = img_as_float32)."""
+    reference layout bit for bit (x * fp32(1/255) = img_as_float32)."""
     from facevae_amd import data as D
     _tree(tmp_path)
     f32 = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), id_sampling=True, is_train=True,
@@ -201,7 +201,7 @@ def test_gif_video_and_paired_dataset(tmp_path):
 
 def test_driving_feed_is_the_reference_driving_frame(tmp_path):
     """output="driving_uint8": the same two random draws as the reference item, only the
-    driving frame decoded -- equal to the float32 item's `driving` after x / 255."""
+    driving frame decoded -- equal to the float32 item's `driving` after the uint8 -> float conversion."""
     from facevae_amd import data as D
     _tree(tmp_path)
     f32 = D.FramesDataset(str(tmp_path), frame_shape=(32, 32, 3), is_train=True, augmentation_params=None)
@@ -213,3 +213,20 @@ def test_driving_feed_is_the_reference_driving_frame(tmp_path):
         d8 = dv[i]
         assert d8.dtype == np.uint8 and d8.shape == (3, 32, 32)
         assert torch.equal(D.to_device_frames(torch.from_numpy(d8), "cpu"), torch.from_numpy(d))
+
+
+def test_uint8_conversion_is_img_as_float32():
+    """skimage.util.img_as_float32 on uint8 is np.multiply(x, 1. / 255, dtype=float32)
+    (skimage/util/dtype.py `_convert`, unsigned -> float; skimage is not importable here, so this
+    restates its arithmetic -- parity unpinned by a reference fixture).  x / 255 differs from it in
+    the last bit for 126 of the 256 byte values; the CPU items and the GPU feed both use the
+    fp32 reciprocal."""
+    import numpy as np
+    import torch
+    import fvamd  # noqa: F401
+    from facevae_amd import data as D
+    x = np.arange(256, dtype=np.uint8)
+    ref = np.multiply(x, 1. / 255, dtype=np.float32)
+    assert np.array_equal(D.u8_to_float(x), ref)
+    assert int((x.astype(np.float32) / 255.0 != ref).sum()) == 126
+    assert torch.equal(D.to_device_frames(torch.from_numpy(x), "cpu"), torch.from_numpy(ref))

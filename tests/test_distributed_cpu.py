@@ -80,26 +80,29 @@ def _run(world, bucket_mb, grad_dtype=None):
     return sorted(out, key=lambda t: t[0])
 
 
-@pytest.mark.parametrize("bucket_mb", [25.0, 1e-6])
-def test_dataparallel_gloo_world2(bucket_mb):
-    out = _run(2, bucket_mb)
-    (_, f0, g0, nb0, sb0, lo0), (_, f1, g1, nb1, sb1, lo1) = out
-    assert torch.equal(f0, f1), "rank-0 broadcast of params/buffers"
-    assert sb0 and sb1, "SyncBN communicator installed"
+@pytest.mark.parametrize("world,bucket_mb", [(2, 25.0), (2, 1e-6), (8, 25.0), (8, 1e-6)])
+def test_dataparallel_gloo(world, bucket_mb):
+    """world 2 and world 8 (the 8-GPU node's rank count, on gloo here)."""
+    out = _run(world, bucket_mb)
+    (_, f0, g0, nb0, sb0, lo0) = out[0]
+    for _, f, g_, nb, sb, lo in out:
+        assert torch.equal(f0, f), "rank-0 broadcast of params/buffers"
+        assert sb, "SyncBN communicator installed"
+        assert nb == nb0 and lo == lo0, "one bucket plan and launch order on every rank"
+        assert torch.allclose(g0, g_, atol=0, rtol=0), "identical averaged gradients on every rank"
     if bucket_mb < 1:
         assert nb0 == 4, "tiny cap: one bucket per parameter"
         # buckets hold the parameters in reverse registration order and launch in the order
         # their gradients complete (b.bias / b.weight first: the last layer's grads are ready first)
-        assert lo0 == lo1 and sorted(lo0) == [0, 1, 2, 3] and set(lo0[:2]) == {0, 1}
+        assert sorted(lo0) == [0, 1, 2, 3] and set(lo0[:2]) == {0, 1}
     else:
         assert nb0 == 1 and lo0 == [0]
-    assert torch.allclose(g0, g1, atol=0, rtol=0), "identical averaged gradients on every rank"
     # reference: the same model on the global batch (mean loss) in one process
     torch.manual_seed(100)
     ref = _Net()
     g = torch.Generator().manual_seed(7)
-    xs = torch.randn(4, 6, generator=g)
-    ys = torch.randn(4, 3, generator=g)
+    xs = torch.randn(2 * world, 6, generator=g)
+    ys = torch.randn(2 * world, 3, generator=g)
     loss = ((ref(xs) - ys) ** 2).mean()
     loss.backward()
     gr = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])

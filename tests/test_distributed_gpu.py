@@ -35,8 +35,8 @@ def _free_port():
     return p
 
 
-def _inputs(H=64, latent=16, hw=32):
-    B = WORLD * PER_RANK
+def _inputs(H=64, latent=16, hw=32, world=WORLD):
+    B = world * PER_RANK
     x = torch.rand(B, 3, H, H, generator=torch.Generator().manual_seed(1234))
     eps = torch.randn(B, latent, hw, hw, generator=torch.Generator().manual_seed(1235))
     return x, eps
@@ -46,10 +46,10 @@ def _cfg(fv, big):
     return fv.FaceVAEConfig(H=256) if big else fv.FaceVAEConfig.toy()
 
 
-def _worker(rank, port, q, big=False):
+def _worker(rank, port, q, big=False, world=WORLD, dtype_name=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import sys
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -61,10 +61,11 @@ def _worker(rank, port, q, big=False):
         D.install(comm, syncbn=True)
         cfg = _cfg(fv, big)
         torch.manual_seed(10 + rank)                 # different init per rank: rank 0's is broadcast
-        m = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(torch.bfloat16 if big else torch.float32)
+        mode = getattr(torch, dtype_name) if dtype_name else (torch.bfloat16 if big else torch.float32)
+        m = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(mode)
         dp = D.DataParallel(m, comm)
         opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
-        x, eps = _inputs(cfg.H, cfg.latent, cfg.latent_hw)
+        x, eps = _inputs(cfg.H, cfg.latent, cfg.latent_hw, world)
         sl = slice(PER_RANK * rank, PER_RANK * (rank + 1))
         xs, es = x[sl].cuda(), eps[sl].cuda()
         init = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
@@ -89,11 +90,11 @@ def _worker(rank, port, q, big=False):
         dist.destroy_process_group()
 
 
-def _run_ranks(big):
+def _run_ranks(big, world=WORLD, dtype_name=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, port, q, big)) for r in range(WORLD)]
+    ps = [ctx.Process(target=_worker, args=(r, port, q, big, world, dtype_name)) for r in range(world)]
     for p in ps:
         p.start()
     out = [torch.load(io.BytesIO(q.get(timeout=240)), weights_only=True) for _ in ps]
@@ -111,14 +112,20 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
 
-def test_dataparallel_syncbn_two_ranks_match_global_batch_oracle():
+@pytest.mark.parametrize("world", [2, 8])
+def test_dataparallel_syncbn_ranks_match_global_batch_oracle(world):
+    """world 2 (global batch 4) and world 8 -- SURVEY §8(e): 8 ranks x 2 images vs the CPU
+    restatement at B = 16 (8 gloo ranks on the one GPU: the bucket plan, the SyncBN count rows
+    and the fp64 record sums over 8 ranks)."""
     from oracle import facevae_cpu as O          # checker only
-    (_, R0, K0, y0, init0, g0, a0), (_, R1, K1, y1, init1, g1, a1) = _run_ranks(False)
+    out = _run_ranks(False, world)
+    (_, R0, K0, y0, init0, g0, a0) = out[0]
     # C2: rank 0's parameters / buffers broadcast before the step
-    for k in init0:
-        assert torch.equal(init0[k], init1[k]), k
+    for r in out[1:]:
+        for k in init0:
+            assert torch.equal(init0[k], r[4][k]), (r[0], k)
 
-    x, eps = _inputs()
+    x, eps = _inputs(world=world)
     ocfg = O.OracleConfig.toy()
     sd = O.prepare_state(init0)
     oo, og = O.train_step(sd, O.adam_init(sd), x, eps, ocfg)
@@ -127,13 +134,16 @@ def test_dataparallel_syncbn_two_ranks_match_global_batch_oracle():
         return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
     # global-batch losses = mean of the per-rank means (equal shards)
-    assert abs((R0 + R1) / 2 - oo["R"].item()) < 1e-3 * oo["R"].item()
-    assert abs((K0 + K1) / 2 - oo["K"].item()) < 1e-3 * abs(oo["K"].item())
-    assert rel(torch.cat([y0, y1]), oo["y"]) < 1e-3           # SyncBN: global-batch statistics
+    Rm = sum(r[1] for r in out) / world
+    Km = sum(r[2] for r in out) / world
+    assert abs(Rm - oo["R"].item()) < 1e-3 * oo["R"].item()
+    assert abs(Km - oo["K"].item()) < 1e-3 * abs(oo["K"].item())
+    assert rel(torch.cat([r[3] for r in out]), oo["y"]) < 1e-3   # SyncBN: global-batch statistics
     dead = {s.prefix + ".bias" for s in O.conv_specs(ocfg)
             if s.block == "cna" or (s.block == "nac" and ".layers.0.layers.2" in s.prefix)}
     for k, g in og.items():
-        assert torch.equal(g0[k], g1[k]), k                   # identical averaged gradients
+        for r in out[1:]:
+            assert torch.equal(g0[k], r[5][k]), (r[0], k)     # identical averaged gradients
         if k in dead:
             assert (g0[k] - g).abs().max() < 1e-4, k
         else:
@@ -141,21 +151,32 @@ def test_dataparallel_syncbn_two_ranks_match_global_batch_oracle():
     for k, v in sd.items():
         if v.is_floating_point() and k not in dead:
             assert rel(a0[k], v.detach()) < 1e-4, k
+            for r in out[1:]:
+                assert torch.equal(a0[k], r[6][k]), (r[0], k)   # every rank: the same step
         elif not v.is_floating_point():
             assert torch.equal(a0[k], v), k
 
 
-def test_dataparallel_syncbn_256_bf16_two_ranks_match_single_process():
+@pytest.mark.parametrize("dtype_name", ["bfloat16", "float8_e4m3fn"])
+def test_dataparallel_syncbn_256_two_ranks_match_single_process(dtype_name):
     """Real 256x256 model, bf16 kernels, 2 ranks x 2 images with SyncBN vs one process x 4
     images on the same weights and inputs.  Per-pixel conv outputs do not depend on the batch
     split and the BN statistics / backward sums are fp64 records summed over both ranks, so the
     two runs differ only by summation order (BN records, weight-gradient split-K) and the bf16
     roundings such differences flip: the image, losses, BN running statistics and gradients
-    must agree far inside the bf16-vs-fp32 deviation (~2e-2 image)."""
+    must agree far inside the bf16-vs-fp32 deviation (~2e-2 image).
+
+    float8_e4m3fn (BASELINE config C5's combination, VERDICT r3 missing item 4): the fp8 convs
+    under DataParallel + SyncBN + the gradient all-reduce, each rank with its own delayed-scaling
+    sites.  A rank's first-step scale comes from its OWN two images' amax, so the e4m3 operands
+    (and everything after them) legitimately differ from the 4-image single process: checked at
+    fp8 tolerance against the single process and the fp32 oracle, and for identical averaged
+    gradients on both ranks."""
     import facevae_amd as fv
     from facevae_amd import distributed as D
     from oracle import facevae_cpu as O          # checker only
-    (_, R0, K0, y0, init0, g0, a0), (_, R1, K1, y1, init1, g1, a1) = _run_ranks(True)
+    fp8 = dtype_name == "float8_e4m3fn"
+    (_, R0, K0, y0, init0, g0, a0), (_, R1, K1, y1, init1, g1, a1) = _run_ranks(True, WORLD, dtype_name)
     for k in init0:
         assert torch.equal(init0[k], init1[k]), k
     for k in g0:
@@ -166,7 +187,7 @@ def test_dataparallel_syncbn_256_bf16_two_ranks_match_single_process():
     D.install(None, syncbn=True)
     m = fv.FaceVAE(cfg)
     m.load_state_dict(init0)
-    m = m.cuda().train().set_compute_dtype(torch.bfloat16)
+    m = m.cuda().train().set_compute_dtype(getattr(torch, dtype_name))
     opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
     opt.zero_grad(set_to_none=True)
     xc, ec = x.cuda(), eps.cuda()
@@ -181,7 +202,7 @@ def test_dataparallel_syncbn_256_bf16_two_ranks_match_single_process():
 
     ocfg = O.OracleConfig(H=256)
     sd = O.prepare_state(init0)
-    oo, _ = O.train_step(sd, O.adam_init(sd), x, eps, ocfg)
+    oo, og = O.train_step(sd, O.adam_init(sd), x, eps, ocfg)
 
     ycat = torch.cat([y0, y1])
     dev = {"image_vs_1proc": _rel(ycat, y.cpu()), "R_vs_1proc": abs((R0 + R1) / 2 - R.item()) / R.item(),
@@ -190,17 +211,40 @@ def test_dataparallel_syncbn_256_bf16_two_ranks_match_single_process():
     dead = {s_.prefix + ".bias" for s_ in O.conv_specs(ocfg)
             if s_.block == "cna" or (s_.block == "nac" and ".layers.0.layers.2" in s_.prefix)}
     gdev = {k: _rel(g0[k], gs[k]) for k in gs if k not in dead}
+    # the same gradients, single process vs the fp32 oracle: the bf16 / fp8 floor of each key
+    gora = {k: _rel(gs[k], og[k]) for k in gs if k not in dead}
     bn = {k: _rel(a0[k], st[k]) for k in st if k.endswith("running_mean") or k.endswith("running_var")}
     gv = sorted(gdev.values())
-    print(f"\n[2 ranks x 2, 256x256 bf16, SyncBN] {dev}\n  grads vs 1 process: median {gv[len(gv) // 2]:.2e} "
-          f"worst {gv[-1]:.2e} ({max(gdev, key=gdev.get)}); BN running stats worst {max(bn.values()):.2e}")
+    top = sorted(gdev, key=gdev.get)[-4:]
+    print(f"\n[2 ranks x 2, 256x256 {dtype_name}, SyncBN] {dev}\n  grads vs 1 process: median {gv[len(gv) // 2]:.2e}; "
+          + ", ".join(f"{k} {gdev[k]:.2e} (1 process vs oracle {gora[k]:.2e})" for k in top)
+          + f"; BN running stats worst {max(bn.values()):.2e}")
+    if fp8:
+        assert dev["image_vs_1proc"] < 5e-2 and dev["R_vs_1proc"] < 1e-2 and dev["K_vs_1proc"] < 1e-3
+        assert dev["image_vs_oracle"] < 5e-2 and dev["R_vs_oracle"] < 1e-2
+        assert gv[len(gv) // 2] < 5e-2
+        for k, v in gdev.items():
+            assert v < max(0.25, 2 * gora[k]), k
+        assert max(bn.values()) < 5e-3
+        return
     # measured (r3): forward bit-identical (image 0.0, BN running stats 0.0), K 5e-8; gradients
-    # median 2.6e-3, worst 8.4e-2 (generator.mid_conv.bias, a near-cancelling sum) -- the fp32
-    # rounding of the fp64 BN-backward sums flips single bf16 roundings of the data gradients
+    # median 2.6e-3.  The worst key, generator.mid_conv.bias (8.4e-2 in r3), is a plain sum over
+    # 131,072 pixels of the residual-stream gradient, which is the bf16-rounded sum of the skip
+    # gradient and six bn1 backward terms whose pixel sums cancel exactly in real arithmetic:
+    # the rounding noise of those terms (a random walk over the pixels) is what is left, and it
+    # flips between two summation orders of the fp64 BN sums.  Gated at <= 3e-2 for every other
+    # gradient, and for such a sum at twice its own single-process-vs-fp32-oracle deviation
+    # (the bf16 floor of that key)
     assert dev["image_vs_1proc"] < 1e-5 and dev["R_vs_1proc"] < 1e-5 and dev["K_vs_1proc"] < 1e-5
     assert dev["image_vs_oracle"] < 2e-2 and dev["R_vs_oracle"] < 1e-3
-    assert gv[len(gv) // 2] < 1e-2 and gv[-1] < 0.25
+    assert gv[len(gv) // 2] < 1e-2
+    for k, v in gdev.items():
+        assert v <= 3e-2 or (k in RESIDUAL_SUM_BIASES and v <= 2 * gora[k]), (k, v, gora[k])
     assert max(bn.values()) < 1e-5
+
+
+# conv biases whose gradient is the pixel sum of the ResBlock stack's residual-stream gradient
+RESIDUAL_SUM_BIASES = {"generator.mid_conv.bias"}
 
 
 def _eval_worker(rank, port, q):

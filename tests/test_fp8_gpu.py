@@ -195,3 +195,70 @@ def test_bn_passes_write_the_fp8_operand(addend):
     torch.cuda.synchronize()
     assert q is not None and torch.equal(dx, dx2)
     assert torch.equal(q[0], rq) and q[1].item() == rdq.item() and torch.equal(sa[0], sb[0])
+
+
+@pytest.mark.parametrize("two_consumers", [False, True])
+def test_resblock_fp8_handoff_checks_the_gradient_tensor(two_consumers):
+    """the next ResBlock's bn1 backward leaves an e4m3 copy of its output for this
+    block's conv2 data gradient.  With a second consumer of the block output autograd adds the
+    other gradient into that tensor (in place: same pointer, new version) before conv2's backward
+    runs, so the copy is stale and must be rejected.  Gradients with the hand-off on equal those
+    with it off (every dy quantized by its conv), and the hand-off is still taken when the output
+    has one consumer."""
+    from facevae_amd.modules import ResBlock2D
+    N, C, H, W = 2, 256, 8, 64
+    g = torch.Generator().manual_seed(31)
+    x0 = torch.randn(N, C, H, W, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    g1 = torch.randn(N, C, H, W, generator=g).cuda()
+    g2 = torch.randn(N, C, H, W, generator=g).cuda()
+    torch.manual_seed(5)
+    r1, r2 = ResBlock2D(C, True), ResBlock2D(C, True)
+    r1, r2 = r1.cuda().train().set_compute_dtype(torch.float8_e4m3fn), r2.cuda().train().set_compute_dtype(
+        torch.float8_e4m3fn)
+    state = [{k: v.clone() for k, v in m.state_dict().items()} for m in (r1, r2)]
+    calls = []
+    orig = ops.quantize_fp8_site
+
+    def counting(t, site):
+        calls.append(t.shape)
+        return orig(t, site)
+
+    def run(handoff):
+        for m, sd in zip((r1, r2), state):
+            m.load_state_dict(sd)
+            m.__dict__.pop("_fv_fp8_sites", None)
+            for c in (m.conv1, m.conv2):
+                c.__dict__.pop("_fv_fp8_sites", None)
+                c.__dict__.pop("_fv_fp8_pending", None)
+        ops._FP8_HANDOFF = handoff
+        try:
+            out = None
+            for it in range(2):                       # step 1 seeds the delayed-scaling sites
+                x = x0.clone().requires_grad_(True)
+                for p in list(r1.parameters()) + list(r2.parameters()):
+                    p.grad = None
+                h = r1(x)
+                out = r2(h)
+                loss = (out.float() * g1).sum()
+                if two_consumers:
+                    loss = loss + (h.float() * g2).sum()
+                calls.clear()
+                ops.quantize_fp8_site = counting
+                try:
+                    loss.backward()
+                finally:
+                    ops.quantize_fp8_site = orig
+            torch.cuda.synchronize()
+            return x.grad.clone(), [p.grad.clone() for p in r1.parameters()], len(calls)
+        finally:
+            ops._FP8_HANDOFF = True
+
+    dx_on, gr_on, nq_on = run(True)
+    dx_off, gr_off, nq_off = run(False)
+    assert torch.equal(dx_on, dx_off)
+    for a, b in zip(gr_on, gr_off):
+        assert torch.equal(a, b)
+    if two_consumers:
+        assert nq_on == nq_off            # the stale copy is rejected: dy quantized again
+    else:
+        assert nq_on == nq_off - 1        # the copy is taken: one quantize pass fewer

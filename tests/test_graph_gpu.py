@@ -171,3 +171,45 @@ def test_sn_bwd_batch_bit_identical(monkeypatch):
         out.append({k: p.detach().clone() for k, p in m.named_parameters()})
     for k in out[0]:
         assert torch.equal(out[0][k], out[1][k]), k
+
+
+def test_segmented_capture_that_raises_leaves_capture_mode():
+    """when the captured step raises inside a segmented (world > 1) capture, the open
+    segment is ended, so the capture stream is usable afterwards and the error surfaces.  A
+    stand-in communicator with world_size 2 selects the segmented path; the step fails before
+    any collective."""
+    from facevae_amd import distributed as D
+
+    class _FakeComm:
+        world_size, rank = 2, 0
+
+    x = torch.randn(1 << 16, device="cuda")
+
+    def bad_step():
+        y = x * 2.0 + 1.0
+        if y.numel() > 0:
+            raise ValueError("step failed inside the capture")
+        return y
+
+    prev = (D._COMM, D._SYNCBN)
+    D.install(_FakeComm(), syncbn=False)
+    try:
+        calls = {"n": 0}
+
+        def step():                          # the eager warm-up call succeeds, the captured one raises
+            calls["n"] += 1
+            return x * 3.0 if calls["n"] == 1 else bad_step()
+        with pytest.raises(ValueError, match="inside the capture"):
+            fv.StepGraph(step, [], warmup=1).capture()
+    finally:
+        D.install(*prev)
+    assert not torch.cuda.is_current_stream_capturing()
+    z = (x + 1.0).sum()                      # ordinary GPU work and a new capture still run
+    torch.cuda.synchronize()
+    assert torch.isfinite(z).item()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        w = x * 5.0
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(w, x * 5.0)

@@ -455,3 +455,26 @@ def test_bn_act_bwd_pooled(shape, dtype):
            i_.data_ptr(), g_.data_ptr(), b_.data_ptr(), 0.0, 1, red.data_ptr(), ws.data_ptr(), L.stream())
     torch.cuda.synchronize()
     assert rel(red[:C], br.grad) < tol and rel(red[C:], gr.grad) < tol
+
+
+@pytest.mark.parametrize("res", [False, True])
+def test_conv3x3_64ch_with_residual(res):
+    """a 64 -> 64 3x3 conv (a 64-channel ResBlock2D conv) has the shape of the 64-channel
+    band kernel (conv3c64_fwd), which has no residual epilogue; with a residual the launch must run
+    the generic DMA-fed kernel on the same prepared weights instead of failing."""
+    N, C, H, W = 2, 64, 64, 64
+    g = gen(77)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    b = torch.randn(C, generator=g)
+    r = torch.randn(N, C, H, W, generator=g)
+    dtype = torch.bfloat16
+    d, xb, wk, _, shp = conv_setup(x, w, 3, dtype)
+    rb = r.cuda().to(dtype).contiguous(memory_format=CL)
+    y = torch.empty(shp, dtype=dtype, device="cuda", memory_format=CL)
+    L.call("fv_conv2d_fwd", ctypes.byref(d), xb.data_ptr(), wk.data_ptr(), b.cuda().data_ptr(), None, None,
+           L.ptr(rb if res else None), y.data_ptr(), None, L.stream())
+    torch.cuda.synchronize()
+    xq = xb.float().cpu()
+    ref = F.conv2d(xq, w, b, padding=1) + (rb.float().cpu() if res else 0)
+    assert rel(y.float(), ref) < 1e-2

@@ -33,15 +33,32 @@ def dead_bias_keys(cfg):
     return keys
 
 
+def dead_bn_keys(cfg):
+    """running_mean keys of the BNs that normalise a dead-bias conv's output (CNA: the block's
+    own BN, `P.layers.0` conv -> `P.layers.1`; ResBlock conv1 `R.layers.0.layers.2` -> the second
+    NAC's BN `R.layers.1.layers.0`)."""
+    keys = set()
+    for k in dead_bias_keys(cfg):
+        p = k[:-len(".bias")]
+        if p.endswith(".layers.0.layers.2"):
+            keys.add(p[:-len(".layers.0.layers.2")] + ".layers.1.layers.0.running_mean")
+        else:
+            assert p.endswith(".layers.0"), p
+            keys.add(p[:-len(".0")] + ".1.running_mean")
+    return keys
+
+
 def check_state(sd, ref, cfg, steps, tol):
     dead = dead_bias_keys(cfg)
+    dead_bn = dead_bn_keys(cfg)
+    assert dead_bn <= set(ref), sorted(dead_bn - set(ref))
     for k, v in ref.items():
         a = sd[k].detach()
         if not v.is_floating_point():
             assert torch.equal(a, v), k
         elif k in dead:
             assert (a - v).abs().max().item() <= 2 * cfg.lr * steps + 1e-7, k
-        elif k.endswith(".running_mean"):
+        elif k in dead_bn:
             # the batch mean of a conv output carries that conv's (dead) bias, which Adam moves
             # by up to ±lr per step in a rounding-noise direction (above); the running mean takes
             # momentum (0.1) of it per step: |delta| <= 0.1 * 2 * lr * steps on top of rel < tol
@@ -115,6 +132,10 @@ def test_full256_two_steps_match_reference():
 
 
 BLOCKS = ["cna_relu", "cna_leaky_sn", "cna_7x7", "down", "up_sn", "res_sn", "same"]
+# per block: the conv biases that feed a training-mode BN (prefix '' = the block; see oracle_block)
+BLOCK_DEAD_BIAS = {"cna_relu": {"layers.0.bias"}, "cna_leaky_sn": {"layers.0.bias"}, "cna_7x7": {"layers.0.bias"},
+                   "down": {"layers.0.layers.0.bias"}, "up_sn": {"layers.1.layers.0.bias"},
+                   "res_sn": {"layers.0.layers.2.bias"}, "same": {"layers.layers.0.bias"}}
 
 
 def oracle_block(name, sd, x):
@@ -146,11 +167,13 @@ def test_block_cases(name):
     (y * c["gy"]).sum().backward()
     assert rel(x.grad, c["gx"]) < 1e-5
     gscale = max(gr.abs().max().item() for gr in c["grads"].values())
+    dead = BLOCK_DEAD_BIAS[name]
     for k, gr in c["grads"].items():
         g = sdp["m." + k].grad
-        if gr.abs().max().item() < 1e-4 * gscale:
+        if k in dead:
             # a conv bias feeding a training-mode BN (dead_bias_keys): its gradient is rounding
             # noise whose digits follow the host CPU's summation order -- absolute bound only
+            assert gr.abs().max().item() < 1e-4 * gscale, k
             assert (g - gr).abs().max().item() <= 1e-4 * gscale, k
         else:
             assert rel(g, gr) < 1e-5, k
