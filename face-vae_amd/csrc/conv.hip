@@ -2452,6 +2452,7 @@ struct H3Wg2Args {
   float* slab;
   float* bslab;
   int H, W, Cout, ldd, nseg, rows, nct;
+  int ldx, nci;          // x channel stride (= Cin) and 64-channel input tiles (Cin / 64)
   unsigned xbytes, dybytes;
 };
 
@@ -2473,11 +2474,16 @@ conv3_halo_wgrad2(H3Wg2Args a) {
   const int wc = wave & 1, wk = wave >> 1;
   const int li = lane & 15, g = lane >> 4;
   const int strips = a.W >> 6;
-  const int blk = blockIdx.x;
-  const int tc = blk % a.nct;
-  const int rest = blk / a.nct;
-  const int seg = rest % a.nseg, strip = (rest / a.nseg) % strips, n = rest / (a.nseg * strips);
-  const int co0 = tc * BC, w0 = strip * 64;
+  // XCD-aware order (bijective remap, speed only): the nct x nci tiles of one (image, strip,
+  // segment) -- the same dy and x rows -- are consecutive lids, dealt to one XCD's L2
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int ntile = a.nct * a.nci;
+  const int tile = blk % ntile, tc = tile % a.nct, tci = tile / a.nct;
+  const int split = blk / ntile;
+  const int seg = split % a.nseg, strip = (split / a.nseg) % strips, n = split / (a.nseg * strips);
+  const int co0 = tc * BC, w0 = strip * 64, ci0 = tci * 64;
   const int h0 = seg * a.rows, h1 = min(a.H, h0 + a.rows);
   const int nrow = h1 - h0;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
@@ -2503,7 +2509,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       const int px = o >> 7, b = o & 127;
       const int ci = ((((b >> 5) ^ tswz<64>(px)) << 4) | (((b >> 4) & 1) << 3));
       const int iw = w0 - 1 + px;
-      poff[j] = (px < 66 && iw >= 0 && iw < a.W) ? (unsigned)((iw * 64 + ci) * 2) : 0x80000000u;
+      poff[j] = (px < 66 && iw >= 0 && iw < a.W) ? (unsigned)((iw * a.ldx + ci0 + ci) * 2) : 0x80000000u;
     } else {
       poff[j] = 0x80000000u;
     }
@@ -2514,7 +2520,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
     const int q = wave + 8 * j - 16;
     const bool rok = y >= 0 && y < a.H;               // wave-uniform (the column test is in poff)
     dma16s(xr, sbase + NSD * DYB + slot * XB + q * 1024, rok ? poff[j] : 0x80000000u,
-           rok ? (unsigned)(((n * a.H + y) * a.W) * 64 * 2) : 0u);
+           rok ? (unsigned)(((n * a.H + y) * a.W) * a.ldx * 2) : 0u);
   };
   auto issue_group = [&](int i) {             // dy row h0 + i, x row h0 + i + 1
     const int h = h0 + i;
@@ -2555,7 +2561,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
     f32x4 accb[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) accb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bool do_bias = BIAS_W && a.bslab;
+    const bool do_bias = BIAS_W && a.bslab && tci == 0;
     bf16x8 ones;
 #pragma unroll
     for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
@@ -2599,23 +2605,24 @@ conv3_halo_wgrad2(H3Wg2Args a) {
         __builtin_amdgcn_s_setprio(0);
       }
     }
-    // slab[blk][co][tap * 64 + ci]: lane holds D[co = 4g + jj][k-col = li]
-    float* sl = a.slab + (long)blk / a.nct * a.Cout * 576;
+    // slab[split][co][tap * Cin + ci]: lane holds D[co = 4g + jj][k-col = li]
+    const long KW = 9L * a.ldx;
+    float* sl = a.slab + (long)split * a.Cout * KW;
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       const int kt = 9 * WK + j, tap = kt >> 2;
-      const int kcol = tap * 64 + (kt & 3) * 16 + li;
+      const int kcol = tap * a.ldx + ci0 + (kt & 3) * 16 + li;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) sl[(long)(co0 + wc * 64 + q * 16 + 4 * g + jj) * 576 + kcol] = acc[q][j][jj];
+        for (int jj = 0; jj < 4; ++jj) sl[(long)(co0 + wc * 64 + q * 16 + 4 * g + jj) * KW + kcol] = acc[q][j][jj];
     }
     if (do_bias && li == 0) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj)
-          a.bslab[(long)(blk / a.nct) * a.Cout + co0 + wc * 64 + q * 16 + 4 * g + jj] = accb[q][jj];
+          a.bslab[(long)split * a.Cout + co0 + wc * 64 + q * 16 + 4 * g + jj] = accb[q][jj];
     }
   });
 }
@@ -3421,12 +3428,18 @@ static int c7n_band(const fv_conv_desc* d) {
 // 3x3 weight gradient with the halo-staged input, rows sliding down a segment
 // (conv3_halo_wgrad2; its tile-per-row-segment predecessor ran 518 us against 262 us for
 // AFE.down1)
+static int g_h3w_all = -1;
 bool use_h3w(const fv_conv_desc* d) {
   // measured against conv_wgrad_v2 (tools/convbench.py): 12 % faster on AFE.down1 (64 -> 128,
-  // whose v2 tile is 128 x 128), slower where v2 runs 256 x 256 tiles (LDS fill per MAC of
-  // the two is then within 20 %), so only cin == 64 takes it
-  return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && !d->pro_act &&
-         d->cin == 64 && d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
+  // whose v2 tile is 128 x 128).  Wider inputs run it as 64-channel input tiles (r4: the res /
+  // down2 weight gradients; FV_H3W_ALL=0 keeps them on conv_wgrad_v2 for A/B)
+  if (g_h3w_all < 0) {
+    const char* e = getenv("FV_H3W_ALL");
+    g_h3w_all = (e && e[0] == '0') ? 0 : 1;
+  }
+  const bool cin_ok = d->cin == 64 || (g_h3w_all && d->cin % 64 == 0);
+  return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && !d->pro_act && cin_ok &&
+         d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
 }
 
 // out_conv weight gradient as "row taps in N" (conv7_n3_wgrad)
@@ -3529,8 +3542,8 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
     const int strips = d->w / 64;
     p.v2 = 5;
     p.ntc = d->cout / 128;
-    p.ntk = 1;
-    int nseg = (256 / p.ntc + d->n * strips / 2) / (d->n * strips);
+    p.ntk = d->cin / 64;               // 64-channel input tiles
+    int nseg = (256 / (p.ntc * p.ntk) + d->n * strips / 2) / (d->n * strips);
     if (nseg < 1) nseg = 1;
     if (nseg > d->h / 4) nseg = d->h / 4 > 0 ? d->h / 4 : 1;
     p.sps = fv_cdiv(d->h, nseg);                  // rows per segment
@@ -4210,9 +4223,10 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
     a.H = d->h; a.W = d->w; a.Cout = d->cout; a.ldd = ldy_dy;
     a.nseg = t.nsteps; a.rows = t.sps; a.nct = t.ntc;
+    a.ldx = d->cin; a.nci = t.ntk;
     a.xbytes = (unsigned)(P * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
-    hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
     return fv_check_launch("conv2d_bwd_weight_halo3s");
   }
   if (t.v2 == 3) {
