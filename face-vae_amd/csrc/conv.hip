@@ -1055,7 +1055,16 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
 // address of pixel hp shifted by a tap is linear: a tap adds one wave-uniform offset to a
 // per-lane base and the fragments of the step are immediate offsets from it (measured in the
 // asm: 4 non-MFMA VALU per 64-MFMA step against 88).  LDS: [NSB weight stages][2 halo buffers].
-template <int WN, int WM, int RN, int RM, int NSB>
+//
+// PRO (NAC blocks: BN-apply + activation of the conv INPUT, modules.py:13,31-39,119-125): the
+// halo is staged pre-BN and transformed IN LDS, once per 32-channel chunk, by the waves that
+// DMA'd it: slot -> bf16(act(fma(v, scale[c], shift[c]))), the exact arithmetic of the separate
+// act_fwd pass (bn.hip), which this removes together with its output tensor.  Out-of-image
+// slots (the zero padding of the ACTIVATED input) are skipped, so they stay 0.  Chunks 0 / 1
+// are transformed after the prologue barrier (+1 barrier); chunk c >= 2 lands by the barrier of
+// the step after its issue, is transformed at the end of that step and published by the next
+// barrier, >= 2 steps before its first fragment read ("BN-apply in the staging").
+template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
@@ -1067,7 +1076,8 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   constexpr int QB = BN / 16, JB = QB / NW;
   static_assert(QB % NW == 0, "weight pieces per wave");
   constexpr int BST = BN * 64, STG = 2 * BST, WOFF = NSB * STG;
-  constexpr int MAIN = WOFF + 2 * HALO, EPI = BM * BN * 2;
+  constexpr int PROB = PRO ? 2 * 256 * 4 : 0;              // scale / shift of <= 256 input channels
+  constexpr int MAIN = WOFF + 2 * HALO + PROB, EPI = BM * BN * 2;
   static_assert(MAIN <= 163840, "LDS");
   static_assert(STG * (NSB - 1) + BST + (BN - 16) * 64 < 65536, "weight fragment immediates");
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
@@ -1092,6 +1102,8 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
 
   // halo slots of this wave: slot k = 16-B chunk k % 6 of halo pixel k / 6 (chunks 4, 5 pad)
   unsigned hoff[JH];
+  unsigned hval = 0;             // PRO: bit j = slot j holds image data (a transform target)
+  int hcb[PRO ? JH : 1];         // PRO: the slot's channel offset in a 32-channel chunk
 #pragma unroll
   for (int j = 0; j < JH; ++j) {
     const int k = (wave + j * NW) * 64 + lane;
@@ -1100,7 +1112,38 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
     const bool ok = hp < HP && ch < 4 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
     hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
+    if constexpr (PRO) {
+      hval |= ok ? 1u << j : 0u;
+      hcb[j] = ch * 8;
+    }
   }
+  float* const sst = reinterpret_cast<float*>(smem + WOFF + 2 * HALO);    // PRO: [scale 256][shift 256]
+  if constexpr (PRO) {
+    for (int i = tid; i < a.Cin; i += NW * 64) {
+      sst[i] = a.psc[i];
+      sst[256 + i] = a.psh[i];
+    }
+  }
+  // PRO: transform this wave's slots of halo chunk c in place (they landed: see above)
+  auto xform = [&](int c) {
+    if constexpr (PRO) {
+      char* const Hs = smem + WOFF + (c & 1) * HALO;
+#pragma unroll
+      for (int j = 0; j < JH; ++j) {
+        if ((hval >> j) & 1u) {
+          uint4* const p = reinterpret_cast<uint4*>(Hs + (wave + j * NW) * 1024 + lane * 16);
+          const float* const sc = sst + c * 32 + hcb[j];
+          Chunk8<bf16> v;
+          v.raw = *p;
+          float f[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = fv_act(fmaf(v.get(q), sc[q], sc[256 + q]), a.slope);
+          v.set8(f);
+          *p = v.raw;
+        }
+      }
+    }
+  };
   // Weights are stage-major (weight_prep_body smaj): tap unit u = c * 9 + t is a [Cout][32]
   // block, so the 16 rows of a DMA piece are one contiguous KB (8 whole 128-B lines; the
   // [co][Kpad] rows made every piece 16 separate 64-B segments).  Piece jb of unit u starts at
@@ -1166,6 +1209,11 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     if (i < nsteps) issue_b(i, i);
   wait_vm<0>();
   __syncthreads();
+  if constexpr (PRO) {
+    xform(0);
+    xform(1);
+    __syncthreads();
+  }
   FV_DIAG_PROLOGUE();
   int pend = 0;
   if (NSB - 1 < nsteps) {
@@ -1174,6 +1222,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   }
   load_frags(fa0, fb0, 0, 0);
   int hn = 2, hstep = (9 * 2 - 10) / 2;
+  int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
   int bj = 0;
   for (int j = 0; j < nsteps; ++j) {
     load_frags(fa1, fb1, 2 * j + 1, bj);
@@ -1190,6 +1239,10 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       FV_DIAG_WAIT_END();
       if (hn < nch && j == hstep) {
         issue_halo(hn);
+        if constexpr (PRO) {
+          xc = hn;
+          xstep = j + 1;             // landed by the next step's barrier
+        }
         ++hn;
         hstep = (9 * hn - 10) / 2;
       }
@@ -1202,6 +1255,9 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       FV_DIAG_ISSUE_END();
     }
     mfma_all(fa1, fb1);
+    if constexpr (PRO) {
+      if (j == xstep) xform(xc);     // published by the next step's barrier
+    }
     bj = bn1;
   }
   FV_DIAG_LOOP_END();
@@ -2445,6 +2501,11 @@ conv_wgrad_v2(Wg2Args a) {
 //   8 waves = 2 (64 co) x 4 (9 of the 36 k-tiles of 16 = (tap, 16 ci)).
 // Output: slab [block][cout][576] (k = tap * 64 + ci: wgrad_reduce_kernel's layout) and the
 // bias slab [block][cout] (sum of dy by an all-ones MFMA operand, k-wave 0).
+// PRO (NAC blocks): x is the PRE-BN tensor; each x row is transformed in LDS after it lands,
+// v -> bf16(act(fma(v, scale, shift))) (act_fwd's arithmetic), out-of-image slots left 0.  The
+// x rows then travel one group earlier (group i = {dy row h0+i, x row h0+i+2}, ring one slot
+// deeper): row h0+i+2 lands by step i's barrier, is transformed in step i and published by
+// step i+1's barrier, where it is first read.
 // ----------------------------------------------------------------------------------------
 struct H3Wg2Args {
   const void* x;
@@ -2454,19 +2515,24 @@ struct H3Wg2Args {
   int H, W, Cout, ldd, nseg, rows, nct;
   int ldx, nci;          // x channel stride (= Cin) and 64-channel input tiles (Cin / 64)
   unsigned xbytes, dybytes;
+  const float* psc;      // PRO: BN scale / shift of the x channels, act slope
+  const float* psh;
+  float slope;
 };
 
-template <int AHEAD>
+template <int AHEAD, bool PRO = false>
 __global__ void __launch_bounds__(512, 1)
 conv3_halo_wgrad2(H3Wg2Args a) {
   // AHEAD groups in flight: group i + AHEAD is issued in row step i (HBM latency under load
-  // is several row steps of MFMA work); rings: dy AHEAD + 1 deep, x AHEAD + 3 deep
-  constexpr int BC = 128, NSD = AHEAD + 1, NSX = AHEAD + 3;
+  // is several row steps of MFMA work); rings: dy AHEAD + 1 deep, x AHEAD + 2 + XA deep
+  constexpr int XA = PRO ? 2 : 1;                     // group i carries x row h0 + i + XA
+  constexpr int BC = 128, NSD = AHEAD + 1, NSX = AHEAD + 2 + XA;
   constexpr int DYB = 64 * BC * 2;                    // 16 KB, 16 pieces
   constexpr int XQ = (66 * 128 + 1023) / 1024;        // 9 pieces per x row (66 px x 64 ci)
   constexpr int XB = XQ * 1024;
   constexpr int NPC = 16 + XQ;                        // pieces per group (25)
-  __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB];
+  constexpr int SSB = PRO ? 2 * 64 * 4 : 0;           // scale / shift of the block's 64 channels
+  __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB + SSB];
   char* dyr = smem;
   char* xr_ = smem + NSD * DYB;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2495,6 +2561,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
   const int npw = wave == 0 ? 4 : 3;                  // pieces of a group this wave issues
   unsigned poff[4];
   int pisx[4];
+  int pci[PRO ? 4 : 1];                               // PRO: the x lane's channel in the tile
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int q = wave + 8 * j;
@@ -2510,6 +2577,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       const int ci = ((((b >> 5) ^ tswz<64>(px)) << 4) | (((b >> 4) & 1) << 3));
       const int iw = w0 - 1 + px;
       poff[j] = (px < 66 && iw >= 0 && iw < a.W) ? (unsigned)((iw * a.ldx + ci0 + ci) * 2) : 0x80000000u;
+      if constexpr (PRO) pci[j] = ci;
     } else {
       poff[j] = 0x80000000u;
     }
@@ -2522,7 +2590,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
     dma16s(xr, sbase + NSD * DYB + slot * XB + q * 1024, rok ? poff[j] : 0x80000000u,
            rok ? (unsigned)(((n * a.H + y) * a.W) * a.ldx * 2) : 0u);
   };
-  auto issue_group = [&](int i) {             // dy row h0 + i, x row h0 + i + 1
+  auto issue_group = [&](int i) {             // dy row h0 + i, x row h0 + i + XA
     const int h = h0 + i;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -2532,22 +2600,56 @@ conv3_halo_wgrad2(H3Wg2Args a) {
           dma16s(dr, sbase + (i % NSD) * DYB + q * 1024, poff[j],
                  (unsigned)((((n * a.H + h) * a.W + w0) * a.ldd) * 2));
         } else {
-          issue_x(h + 1, j);
+          issue_x(h + XA, j);
         }
       }
     }
   };
-  auto issue_xonly = [&](int y) {             // prologue rows h0 - 1, h0
+  auto issue_xonly = [&](int y) {             // prologue rows h0 - 1 .. h0 + XA - 1
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (j < npw && pisx[j]) issue_x(y, j);
   };
+  float* const sst = reinterpret_cast<float*>(smem + NSD * DYB + NSX * XB);   // PRO: [scale 64][shift 64]
+  // PRO: transform this wave's slots of x row y (its own DMAs: landed once its vmcnt says so)
+  auto xform_row = [&](int y) {
+    if constexpr (PRO) {
+      if (y < 0 || y >= a.H) return;                  // wave-uniform: an all-zero padding row
+      char* const xs = xr_ + ((y - h0 + 1) % NSX) * XB;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (j < npw && pisx[j] && poff[j] != 0x80000000u) {
+          uint4* const p = reinterpret_cast<uint4*>(xs + (wave + 8 * j - 16) * 1024 + lane * 16);
+          Chunk8<bf16> v;
+          v.raw = *p;
+          float f[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) f[q] = fv_act(fmaf(v.get(q), sst[pci[j] + q], sst[64 + pci[j] + q]), a.slope);
+          v.set8(f);
+          *p = v.raw;
+        }
+      }
+    }
+  };
+  if constexpr (PRO) {
+    if (tid < 64) {
+      sst[tid] = a.psc[ci0 + tid];
+      sst[64 + tid] = a.psh[ci0 + tid];
+    }
+    __syncthreads();
+  }
 
-  issue_xonly(h0 - 1);
-  issue_xonly(h0);
+#pragma unroll
+  for (int y = -1; y < XA; ++y) issue_xonly(h0 + y);
 #pragma unroll
   for (int i = 0; i < AHEAD; ++i)
     if (i < nrow) issue_group(i);
+  if constexpr (PRO) {
+    // the prologue rows are this wave's oldest DMAs; transformed here, published by step 0's barrier
+    wait_vm_dyn(min(AHEAD, nrow) * npw);
+#pragma unroll
+    for (int y = -1; y < XA; ++y) xform_row(h0 + y);
+  }
   // the wave's k-wave index as a compile-time constant (its 9 k-tiles, and the bias MFMAs of
   // k-wave 0, then need no registers)
   with_const<0, 4>(wk, [&](auto wkc) {
@@ -2573,6 +2675,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (i + AHEAD < nrow) issue_group(i + AHEAD);
+      if constexpr (PRO) xform_row(h0 + i + XA);      // landed with group i; read from step i + 1
       const char* dys = dyr + (i % NSD) * DYB;
       const char* xrow[3];
 #pragma unroll
@@ -3283,8 +3386,29 @@ bool use_v2(const fv_conv_desc* d) {
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
 
+// BN-apply + activation prologue in the halo staging (conv3_halo_fwd3<..., PRO>): the NAC
+// ResBlock convs (256-channel co tiles, <= 256 input channels).  FV_NAC_STAGED=0 turns it off
+// (the model then materialises act(BN(x)) with a separate pass, for A/B)
+static int g_nac_staged = -1;
+bool nac_staged_enabled() {
+  if (g_nac_staged < 0) {
+    const char* e = getenv("FV_NAC_STAGED");
+    g_nac_staged = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_nac_staged != 0;
+}
+static bool pro3_ok(const fv_conv_desc* d) {
+  if (!nac_staged_enabled()) return false;
+  if (d->dtype != FV_BF16 || d->ksize != 3 || d->upsample || !d->pro_act) return false;
+  if (d->out_nchw_f32 || d->epi_sigmoid || d->ldy % 8 || d->cout % 256) return false;
+  if (d->cin % 64 || d->cin > 256 || d->cin_valid != d->cin || d->w % 64 || d->h % 4) return false;
+  const long P = (long)d->n * d->h * d->w;
+  return P * d->cin * 2 < (1L << 31) && P * d->ldy * 2 < (1L << 31);
+}
+
 // 3x3 halo path (conv3_halo_fwd2 / fwd3): co per block (256 / 128 / 64), 0 when not eligible
 int halo3_bn(const fv_conv_desc* d) {
+  if (d->pro_act) return pro3_ok(d) ? 256 : 0;
   if (!use_v2(d) || d->ksize != 3 || d->upsample || d->w % 64 || d->h % 4) return 0;
   if ((long)d->n * d->h * d->w * d->ldy * 2 >= (1L << 31)) return 0;
   // co % 256: the pipelined pair-of-taps kernel (3 % over conv_fwd_v2's 256 x 256 tile on
@@ -3438,7 +3562,8 @@ bool use_h3w(const fv_conv_desc* d) {
     g_h3w_all = (e && e[0] == '0') ? 0 : 1;
   }
   const bool cin_ok = d->cin == 64 || (g_h3w_all && d->cin % 64 == 0);
-  return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && !d->pro_act && cin_ok &&
+  if (d->pro_act && !pro3_ok(d)) return false;      // the staged BN prologue: NAC convs only
+  return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && cin_ok &&
          d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
 }
 
@@ -3518,8 +3643,9 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   const long hin = d->upsample ? d->h / 2 : d->h, win = d->upsample ? d->w / 2 : d->w;
   // 32-bit buffer offsets: x and dy (channel stride = cout padded to a power of two >= 8, as
   // every caller passes; fv_conv2d_bwd_weight re-checks the real stride) must stay < 2 GB
-  p.v2 = d->dtype == FV_BF16 && !d->pro_act && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
-         P * pad_pow2_8(d->cout) * 2 < (1L << 31);
+  const bool fits = d->dtype == FV_BF16 && (long)d->n * hin * win * d->cin * 2 < (1L << 31) &&
+                   P * pad_pow2_8(d->cout) * 2 < (1L << 31);
+  p.v2 = fits && !d->pro_act;
   // out_conv 7x7 64 -> <= 4 (v2 == 3): blocks = (image, 64-column strip, row segment), about
   // 4 per CU; slab [block][32 (r, co)][448 (s, ci)]
   if (p.v2 && use_c7w(d)) {
@@ -3538,7 +3664,7 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   }
   // 3x3 sliding-row wgrad (v2 == 5, conv3_halo_wgrad2): blocks = (image, 64-column strip,
   // row segment) x co tiles of 128, ~1 block per CU; splits = image x strip x segment
-  if (p.v2 && use_h3w(d)) {
+  if (fits && use_h3w(d)) {             // (with the staged BN prologue too)
     const int strips = d->w / 64;
     p.v2 = 5;
     p.ntc = d->cout / 128;
@@ -3717,6 +3843,11 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   const size_t rows = (size_t)fv_cdiv(d->cin, t.bn) * t.bn;
   if (use_dgrad_lowres(d)) return rows * 16 * cin_t;
   return rows * kpad_of(d->ksize, cin_t);
+}
+
+int fv_conv2d_pro_staged(const fv_conv_desc* d) {
+  if (check_desc(d) != FV_OK) return 0;
+  return pro3_ok(d) ? 1 : 0;
 }
 
 int fv_conv2d_dgrad_lowres(const fv_conv_desc* d) {
@@ -4053,7 +4184,10 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // fwd / dgrad 127 / 121.5 -> 122 / 117 us, down2 dgrad 317 -> 301 us (kept).  The weights
     // off the LDS-DMA path -- each wave's A fragments loaded to registers two / one taps ahead,
     // the halo register-staged, one barrier per 32-channel chunk: 126 -> 134 us (not kept).)
-    if (bn >= 128 && a.Cin % 64 == 0) {
+    if (d->pro_act) {
+      FV_REQUIRE(bn == 256 && psc && psh, "staged BN prologue: bad arguments");
+      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb);
+    } else if (bn >= 128 && a.Cin % 64 == 0) {
       if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 256) {
@@ -4149,6 +4283,17 @@ int fv_conv2d_fwd_sr(const fv_conv_desc* d, const void* x, const void* wk, const
   return conv_run(d, x, wk, bias, nullptr, nullptr, res, y, nullptr, (hipStream_t)stream, sr);
 }
 
+int fv_conv2d_fwd_pro_sr(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
+                         const float* pro_scale, const float* pro_shift, const void* res, void* y,
+                         const fv_store_reduce* sr, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(x && wk && y && sr && sr->mode == 1, "fwd_pro_sr: null pointer or mode != 1");
+  FV_REQUIRE(!d->pro_act || (pro_scale && pro_shift), "prologue needs scale/shift");
+  FV_REQUIRE(!d->out_nchw_f32 && d->ldy == d->cout, "fwd_pro_sr: plain NHWC output only");
+  return conv_run(d, x, wk, bias, pro_scale, pro_shift, res, y, nullptr, (hipStream_t)stream, sr);
+}
+
 int fv_conv2d_bwd_data_sr(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,
                           const fv_store_reduce* sr, void* stream) {
   int st = check_desc(d);
@@ -4226,7 +4371,11 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.ldx = d->cin; a.nci = t.ntk;
     a.xbytes = (unsigned)(P * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
-    hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    a.psc = pro_scale; a.psh = pro_shift; a.slope = d->pro_slope;
+    if (d->pro_act)
+      hipLaunchKernelGGL((conv3_halo_wgrad2<4, true>), dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
     return fv_check_launch("conv2d_bwd_weight_halo3s");
   }
   if (t.v2 == 3) {
