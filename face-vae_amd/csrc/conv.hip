@@ -1062,8 +1062,11 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
 // act_fwd pass (bn.hip), which this removes together with its output tensor.  Out-of-image
 // slots (the zero padding of the ACTIVATED input) are skipped, so they stay 0.  Chunks 0 / 1
 // are transformed after the prologue barrier (+1 barrier); chunk c >= 2 lands by the barrier of
-// the step after its issue, is transformed at the end of that step and published by the next
-// barrier, >= 2 steps before its first fragment read ("BN-apply in the staging").
+// the step after its issue and is transformed at the end of that step by waves 0-3 and of the
+// next by waves 4-7 (the SIMD partners of 0-3: one wave of a SIMD transforms while the other
+// runs MFMAs), published by the following barrier, before its first fragment read (the first
+// read needs it published by barrier floor(9c / 2) - 1 (c even) / (9c - 3) / 2 (c odd), the
+// later half publishes at barrier 9c / 2 - 2 / (9c - 5) / 2).
 template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
@@ -1241,7 +1244,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
         issue_halo(hn);
         if constexpr (PRO) {
           xc = hn;
-          xstep = j + 1;             // landed by the next step's barrier
+          xstep = j + 1 + (wave >= 4 ? 1 : 0);   // landed by the next step's barrier
         }
         ++hn;
         hstep = (9 * hn - 10) / 2;

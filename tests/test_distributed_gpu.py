@@ -127,8 +127,16 @@ def test_dataparallel_syncbn_ranks_match_global_batch_oracle(world):
 
     x, eps = _inputs(world=world)
     ocfg = O.OracleConfig.toy()
-    sd = O.prepare_state(init0)
-    oo, og = O.train_step(sd, O.adam_init(sd), x, eps, ocfg)
+
+    def oracle(dt):
+        sd = O.prepare_state(init0)
+        sd = {k: (v.detach().to(dt).requires_grad_(v.requires_grad) if v.is_floating_point() else v.clone())
+              for k, v in sd.items()}
+        oo, og = O.train_step(sd, O.adam_init(sd), x.to(dt), eps.to(dt), ocfg)
+        return sd, oo, og
+
+    sd, oo, og = oracle(torch.float32)
+    _, oo64, og64 = oracle(torch.float64)
 
     def rel(a, b):
         return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
@@ -147,7 +155,11 @@ def test_dataparallel_syncbn_ranks_match_global_batch_oracle(world):
         if k in dead:
             assert (g0[k] - g).abs().max() < 1e-4, k
         else:
-            assert rel(g0[k], g) < 1e-3, k
+            # vs the float64 oracle: 1e-3, or -- at B = 16 the reference's own fp32 arithmetic is
+            # already 3e-3 off float64 on the Generator's first layers (BN-backward cancellation;
+            # 1e-6 at B = 4) -- twice the fp32 oracle's own deviation
+            e_ref = rel(g, og64[k])
+            assert rel(g0[k], og64[k]) < max(1e-3, 2 * e_ref + 1e-4), (k, rel(g0[k], og64[k]), e_ref)
     for k, v in sd.items():
         if v.is_floating_point() and k not in dead:
             assert rel(a0[k], v.detach()) < 1e-4, k

@@ -96,6 +96,9 @@ def main():
                     help="load the diagnostic library (build.py --diag) and print the in-kernel clock stamps "
                          "of the halo 3x3 forward after each layer's forward timing")
     ap.add_argument("--lib", default="", help="another build of libfacevae.so (A/B of two builds on one box)")
+    ap.add_argument("--pro", action="store_true",
+                    help="BN-apply + ReLU prologue (pre-BN input) on the layers whose fast kernels stage it "
+                         "(fv_conv2d_pro_staged: the NAC ResBlock convs), fwd and wgrad")
     a = ap.parse_args()
     if a.diag:
         L.LIB_PATH = os.path.join(ROOT, "face-vae_amd", "csrc", "build_diag", "libfacevae_diag.so")
@@ -114,6 +117,13 @@ def main():
         cp = ops.pad_pow2(cin)
         x = torch.randn(B, cp, Hi, Hi, device="cuda").to(dtype).contiguous(memory_format=CL)
         d = ops.desc(dtype, B, H, H, cp, cin, cout, cout, k, ups)
+        psc = psh = None
+        if a.pro:
+            dp = ops.desc(dtype, B, H, H, cp, cin, cout, cout, k, ups, pro=1)
+            if L.query("fv_conv2d_pro_staged", ctypes.byref(dp)):
+                d = dp
+                psc = (torch.rand(cp, device="cuda") + 0.5).contiguous()
+                psh = (torch.randn(cp, device="cuda") * 0.1).contiguous()
         w = (torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).contiguous()
         wk = torch.empty(L.query("fv_conv_wk_elems", ctypes.byref(d)), dtype=dtype, device="cuda")
         wt = torch.empty(L.query("fv_conv_wt_elems", ctypes.byref(d)), dtype=dtype, device="cuda")
@@ -128,7 +138,8 @@ def main():
         nb = L.query("fv_conv2d_stats_blocks", ctypes.byref(d))
         part = torch.empty(nb * 2 * cout, device="cuda")
         flop = 2.0 * B * H * H * cout * cin * k * k
-        row = {"layer": name, "k": k, "cin": cin, "cout": cout, "H": H, "ups": ups, "gflop": flop / 1e9}
+        row = {"layer": name, "k": k, "cin": cin, "cout": cout, "H": H, "ups": ups, "gflop": flop / 1e9,
+               "pro": psc is not None}
         if fp8 and L.query("fv_conv2d_fp8_supported", ctypes.byref(d)):
             # fp8 operands (quantized once, outside the timed region) for fwd and dgrad
             ws = torch.empty(L.query("fv_fp8_ws_bytes") // 4, device="cuda")
@@ -160,14 +171,14 @@ def main():
         if "fwd" in kinds:
             if a.diag:
                 L.load().fv_diag_clear()
-            us = timeit(lambda: L.call("fv_conv2d_fwd", ctypes.byref(d), x.data_ptr(), wk.data_ptr(), None, None,
-                                       None, None, y.data_ptr(), None if nchw else part.data_ptr(), L.stream()),
+            us = timeit(lambda: L.call("fv_conv2d_fwd", ctypes.byref(d), x.data_ptr(), wk.data_ptr(), None, L.ptr(psc),
+                                       L.ptr(psh), None, y.data_ptr(), None if nchw else part.data_ptr(), L.stream()),
                         a.iters)
             row["fwd_us"], row["fwd_tf"] = round(us, 1), round(flop / us / 1e6, 1)
             if a.diag:
                 row["diag_fwd"] = diag_summary()
         dy = (torch.randn(B, ldd, H, H, device="cuda") * 0.1).to(dtype).contiguous(memory_format=CL)
-        if "dgrad" in kinds and name != "in7":
+        if "dgrad" in kinds and name != "in7" and psc is None:
             dx = torch.empty(B, cp, H, H, dtype=dtype, device="cuda", memory_format=CL)
             if a.diag:
                 L.load().fv_diag_clear()
@@ -181,7 +192,7 @@ def main():
             bslab = torch.empty(L.query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), device="cuda")
             dw = torch.empty_like(w)
             db = torch.empty(cout, device="cuda")
-            us = timeit(lambda: L.call("fv_conv2d_bwd_weight", ctypes.byref(d), x.data_ptr(), None, None,
+            us = timeit(lambda: L.call("fv_conv2d_bwd_weight", ctypes.byref(d), x.data_ptr(), L.ptr(psc), L.ptr(psh),
                                        dy.data_ptr(), ldd, slab.data_ptr(), bslab.data_ptr(), L.stream()), a.iters)
             us2 = timeit(lambda: L.call("fv_conv2d_wgrad_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(),
                                         dw.data_ptr(), db.data_ptr(), L.stream()), a.iters)
