@@ -102,6 +102,7 @@ _SIGS = {
     "fv_conv2d_fp8_stats_blocks": (c_int, [D]),
     "fv_conv2d_fp8_stats_block_pixels": (c_int, [D]),
     "fv_fp8_mfma_probe": (c_int, [P, P, P, P]),
+    "fv_tr8_probe": (c_int, [P, P, P]),
     "fv_conv3d_wk_bytes": (c_size_t, [D3]),
     "fv_conv3d_weight_prep": (c_int, [D3, P, P, P, P]),
     "fv_conv3d_stats_blocks": (c_int, [D3]),

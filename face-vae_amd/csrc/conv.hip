@@ -4879,6 +4879,18 @@ __global__ void fp8_mfma_probe_kernel(const uint8_t* a, const uint8_t* b, float*
   for (int i = 0; i < 4; ++i) c[(4 * g + i) * 16 + r] = acc[i];
 }
 
+// ds_read_b64_tr_b8 probe (tests/test_fp8_gpu.py pins its lane mapping before any kernel relies
+// on it): LDS byte i = i & 255 over 4 KB, lane l reads 8 transposed bytes at lane_addr[l]
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+__global__ void tr8_probe_kernel(const int* lane_addr, int* out) {
+  __shared__ __attribute__((aligned(16))) unsigned char sm[4096];
+  for (int i = threadIdx.x; i < 4096; i += 64) sm[i] = (unsigned char)(i & 255);
+  __syncthreads();
+  const v2i_t v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((FV_LDS v2i_t*)(sm + lane_addr[threadIdx.x]));
+  out[2 * threadIdx.x] = v[0];
+  out[2 * threadIdx.x + 1] = v[1];
+}
+
 // fp8 3x3 conv, halo-staged input (the structure of conv3_halo_fwd with a 128-channel k step):
 //   k step ks = (128-channel chunk c = ks / 9, tap t = ks % 9);
 //   weights stage [BN rows][128 B] (one tap x 128 ci), 16-B chunks XOR swz8(row): fragment
@@ -5178,6 +5190,12 @@ int fv_conv2d_fp8_stats_block_pixels(const fv_conv_desc* d) {
 int fv_conv2d_fp8_stats_blocks(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK || !fp8_ok(d)) return 0;
   return fv_cdiv((long)d->n * d->h * d->w, 64);
+}
+
+int fv_tr8_probe(const int* lane_addr, int* out, void* stream) {
+  FV_REQUIRE(lane_addr && out, "tr8_probe: null pointer");
+  hipLaunchKernelGGL(tr8_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, lane_addr, out);
+  return fv_check_launch("tr8_probe");
 }
 
 int fv_fp8_mfma_probe(const uint8_t* a, const uint8_t* b, float* c, void* stream) {

@@ -250,6 +250,9 @@ int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void*
                                 const float* wt_dq, void* dx, void* stream);
 /* layout probe: c[16][16] = a[16][128] . b[16][128]^T through one scaled fp8 MFMA tile */
 int fv_fp8_mfma_probe(const uint8_t* a, const uint8_t* b, float* c, void* stream);
+/* test probe: 64 lanes each read 8 bytes by ds_read_b64_tr_b8 at LDS byte offset lane_addr[lane]
+ * (< 4088, 8-aligned) of a 4 KB LDS image holding byte i = i & 255; out [64][2] ints */
+int fv_tr8_probe(const int* lane_addr, int* out, void* stream);
 
 /* ------------------------------------------------ 3x3x3 conv (AFE ResBlock3D) ---- */
 /* nn.Conv3d(cin, cout, 3, 1, 1) of ConvBlock3D / ResBlock3D (modules.py:52-56, 133-135) in the

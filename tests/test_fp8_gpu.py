@@ -262,3 +262,26 @@ def test_resblock_fp8_handoff_checks_the_gradient_tensor(two_consumers):
         assert nq_on == nq_off            # the stale copy is rejected: dy quantized again
     else:
         assert nq_on == nq_off - 1        # the copy is taken: one quantize pass fewer
+
+
+def test_tr8_transposed_read_lane_mapping():
+    """ds_read_b64_tr_b8 (gfx950): within each 16-lane group, lane li supplies the address of an
+    8-byte segment -- row li >> 1, columns 8 (li & 1) .. +7 -- of an 8 x 16 byte block, and lane li
+    receives COLUMN li of the block (its 8 rows, row 0 in the lowest byte): the 8-bit form of the
+    ds_read_b64_tr_b16 transpose the bf16 weight gradients use.  Pinned here before the fp8
+    weight gradient relies on it."""
+    ROWB = 16
+    lanes = torch.arange(64)
+    li, g = lanes & 15, lanes >> 4
+    addr = (g * 256 + (li >> 1) * ROWB + (li & 1) * 8).to(torch.int32).cuda()
+    out = torch.empty(128, dtype=torch.int32, device="cuda")
+    L.call("fv_tr8_probe", addr.data_ptr(), out.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    got = out.cpu().view(64, 2).contiguous().view(torch.uint8).view(64, 8)
+    exp = torch.empty(64, 8, dtype=torch.uint8)
+    for lane in range(64):
+        for r in range(8):
+            exp[lane, r] = (int(g[lane]) * 256 + r * ROWB + int(li[lane])) & 255
+    print("\n[tr_b8] group 0 received (lane: bytes):\n" + "\n".join(
+        f"  {i:2d}: {got[i].tolist()}" for i in range(16)))
+    assert torch.equal(got, exp)
