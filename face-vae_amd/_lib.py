@@ -99,6 +99,8 @@ _SIGS = {
     "fv_quantize_fp8_site": (c_int, [c_int, P, c_long, P, P, c_int, P, P]),
     "fv_conv2d_fwd_fp8_site": (c_int, [D, P, P, P, P, P, P, P, P, P]),
     "fv_conv2d_bwd_data_fp8_site": (c_int, [D, P, P, P, P, P, P]),
+    "fv_conv2d_wgrad_fp8_supported": (c_int, [D]),
+    "fv_conv2d_bwd_weight_fp8": (c_int, [D, P, P, P, P, P, P, P]),
     "fv_conv2d_fp8_stats_blocks": (c_int, [D]),
     "fv_conv2d_fp8_stats_block_pixels": (c_int, [D]),
     "fv_fp8_mfma_probe": (c_int, [P, P, P, P]),

@@ -5029,6 +5029,206 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
 }
 
+// ----------------------------------------------------------------------------------------
+// fp8 (e4m3) weight gradient of the 3x3 convs (BASELINE config C5): the
+// sliding-row structure of conv3_halo_wgrad2 on v_mfma_scale_f32_16x16x128_f8f6f4, fed by the
+// e4m3 copies of x and dy the forward / data gradient already consumed (delayed scaling, dq =
+// site word 18).  A block owns 128 co x 9 taps x 64 ci and walks ROW PAIRS of one 64-column strip
+// (the MFMA K = 128 pixels = output rows h and h+1):
+//   D[co][(tap, ci)] += sum_{p in rows h, h+1} dy[p][co] * x[p + tap offset][ci]
+// A = dy^T (rows co, k = pixel), B = x^T (rows ci, k = pixel): both transposed reads of NHWC byte
+// images, ds_read_b64_tr_b8 (8 pixels x 16 channels per 16-lane group; tests/test_fp8_gpu.py
+// pins the lane mapping).  A fragment (lane r = l & 15, g = l >> 4: k 16g..16g+15 U 64+16g..+15)
+// = 4 such reads: pixels 16g + {0, 8} of row h, the same of row h + 1.  The 8-byte channel blocks
+// of a pixel row are XOR-swizzled by the pixel (swz8d / swz8x) so the 32 lanes of a read
+// (16 pixels x 2 blocks) hit 64 distinct banks; the swizzle is even, so a lane's 16-B DMA slot
+// is one contiguous 16-B source chunk.  Group i = {dy rows h0+2i, h0+2i+1; x rows h0+2i+1,
+// h0+2i+2} (26 pieces) travels AHEAD groups ahead; rings dy AHEAD+1 groups, x 2 AHEAD+4 rows.
+// 4 waves, one per SIMD (512 registers each: the 128 x 576 tile is 288 accumulators per wave,
+// which two waves per SIMD -- 256 registers each -- spill): wave (wc, wk) owns 64 co x 18 k-tiles.
+// Output: the slab layout of conv3_halo_wgrad2 (fv_conv2d_wgrad_reduce), scaled by dq_x dq_dy;
+// bias gradient = sum of the e4m3 dy (an all-ones B operand, ci tile 0; k-wave wk sums the co
+// tiles 2 wk, 2 wk + 1 of its four).
+// ----------------------------------------------------------------------------------------
+struct Wg8Args {
+  const uint8_t* x8;
+  const uint8_t* dy8;
+  const float* dqx;
+  const float* dqdy;
+  float* slab;
+  float* bslab;
+  int H, W, Cin, Cout, nseg, rows, nct, nci;
+  unsigned xbytes, dybytes;
+};
+
+__device__ __forceinline__ int swz8x(int px) { return (((px >> 2) & 1) | (((px >> 4) & 1) << 1)) << 1; }   // 64-B rows
+__device__ __forceinline__ int swz8d(int px) { return (((px >> 1) & 3) | (((px >> 4) & 1) << 2)) << 1; }   // 128-B rows
+
+__device__ __forceinline__ v2i_t tr8(const char* p) {
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((FV_LDS v2i_t*)(FV_LDS char*)(p));
+}
+
+template <int AHEAD>
+__global__ void __launch_bounds__(256, 1)
+conv3_wgrad_fp8(Wg8Args a) {
+  constexpr int BC = 128, NSD = AHEAD + 1, NSX = 2 * AHEAD + 4;
+  constexpr int DYR = 64 * BC, DYB = 2 * DYR;         // 8 KB per dy row, 16 KB per group
+  constexpr int XQ = 5, XB = XQ * 1024;               // x row: 66 px x 64 B = 4224 B -> 5 pieces
+  constexpr int NPC = 16 + 2 * XQ;                    // pieces per group (26)
+  __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB];
+  char* const dyr = smem;
+  char* const xr_ = smem + NSD * DYB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave & 1, wk = wave >> 1;
+  const int li = lane & 15, g = lane >> 4;
+  const int strips = a.W >> 6;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int ntile = a.nct * a.nci;
+  const int tile = blk % ntile, tc = tile % a.nct, tci = tile / a.nct;
+  const int split = blk / ntile;
+  const int seg = split % a.nseg, strip = (split / a.nseg) % strips, n = split / (a.nseg * strips);
+  const int co0 = tc * BC, w0 = strip * 64, ci0 = tci * 64;
+  const int h0 = seg * a.rows, h1 = min(a.H, h0 + a.rows);
+  const int nstep = (h1 - h0) >> 1;                   // row pairs (the host keeps segments even)
+  constexpr int NWV = 4, JP = (NPC + NWV - 1) / NWV;  // 4 waves; <= 7 pieces per wave and group
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.x8), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.dy8), 0, (int)a.dybytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+
+  // this wave's pieces of a group: q = wave + 4 j < 26 (q < 16: dy row q >> 3, piece q & 7; else
+  // x row (q - 16) / 5, piece (q - 16) % 5); source offsets relative to the row start
+  const int npw = (NPC - wave + NWV - 1) / NWV;
+  unsigned poff[JP];
+#pragma unroll
+  for (int j = 0; j < JP; ++j) {
+    const int q = wave + NWV * j;
+    poff[j] = 0x80000000u;
+    if (q < 16) {
+      const int o = (q & 7) * 1024 + lane * 16;
+      const int px = o >> 7, kk = (o >> 4) & 7;
+      poff[j] = (unsigned)(px * a.Cout + co0 + ((kk ^ (swz8d(px) >> 1)) << 4));
+    } else if (q < NPC) {
+      const int o = ((q - 16) % XQ) * 1024 + lane * 16;
+      const int px = o >> 6, kk = (o >> 4) & 3;
+      const int iw = w0 - 1 + px;
+      if (px < 66 && iw >= 0 && iw < a.W) poff[j] = (unsigned)(iw * a.Cin + ci0 + ((kk ^ (swz8x(px) >> 1)) << 4));
+    }
+  }
+  auto xslot = [&](int y) { return (y - h0 + 1) % NSX; };
+  auto issue_x = [&](int y, int j, int q) {             // x piece (q - 16) % 5 of row y
+    const bool rok = y >= 0 && y < a.H;
+    dma16s(xr, sbase + NSD * DYB + xslot(y) * XB + ((q - 16) % XQ) * 1024, rok ? poff[j] : 0x80000000u,
+           rok ? (unsigned)(((n * a.H + y) * a.W) * a.Cin) : 0u);
+  };
+  auto issue_group = [&](int i) {
+    const int h = h0 + 2 * i;
+#pragma unroll
+    for (int j = 0; j < JP; ++j) {
+      const int q = wave + NWV * j;
+      if (j < npw) {
+        if (q < 16) {
+          const int r = q >> 3;
+          dma16s(dr, sbase + (i % NSD) * DYB + r * DYR + (q & 7) * 1024, poff[j],
+                 (unsigned)(((n * a.H + h + r) * a.W + w0) * a.Cout));
+        } else {
+          issue_x(h + 1 + (q - 16) / XQ, j, q);
+        }
+      }
+    }
+  };
+  // prologue x rows h0 - 1 (as row 0 of a group) and h0 (as row 1)
+#pragma unroll
+  for (int j = 0; j < JP; ++j) {
+    const int q = wave + NWV * j;
+    if (j < npw && q >= 16) issue_x(h0 - 1 + (q - 16) / XQ, j, q);
+  }
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i)
+    if (i < nstep) issue_group(i);
+
+  with_const<0, 2>(wk, [&](auto wkc) {
+    constexpr int WK = decltype(wkc)::value, NK = 18;   // k-tiles NK WK .. NK WK + 17 of 36
+    f32x4 acc[4][NK];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < NK; ++j) acc[q][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // bias gradient: k-wave WK sums co tiles 2 WK, 2 WK + 1 of its four (an all-ones e4m3 B operand)
+    f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    const bool do_bias = a.bslab && tci == 0;
+    const int pl = 16 * g + (li >> 1);                  // this lane's pixel row of a tr_b8 block
+    for (int i = 0; i < nstep; ++i) {
+      const int younger = min(AHEAD - 1, nstep - 1 - i);
+      wait_vm_dyn(younger * npw);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (i + AHEAD < nstep) issue_group(i + AHEAD);
+      const char* d0 = dyr + (i % NSD) * DYB;
+      const char* d1 = d0 + DYR;
+      // the fragment offsets are recomputed every step (an opaque copy of the pixel row) instead
+      // of being hoisted out of the loop: 26 loop-invariant offsets would spill the accumulators
+      int plv = pl;
+      asm volatile("" : "+v"(plv));
+      v8i af[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cb = 2 * (wc * 4 + q) + (li & 1);     // 8-byte co block of the 128-co tile
+        const int o0 = plv * BC + ((cb ^ swz8d(plv)) << 3), o1 = (plv + 8) * BC + ((cb ^ swz8d(plv + 8)) << 3);
+        const v2i_t r0 = tr8(d0 + o0), r1 = tr8(d0 + o1), r2 = tr8(d1 + o0), r3 = tr8(d1 + o1);
+        af[q] = v8i{r0[0], r0[1], r1[0], r1[1], r2[0], r2[1], r3[0], r3[1]};
+      }
+      // x fragment of k-tile j: tap (r, s), 16-ci block u; rows h - 1 + r (k < 64) and h + r
+      auto xfrag = [&](int j) {
+        const int kt = NK * WK + j, tap = kt >> 2, u = kt & 3, r = tap / 3, s3 = tap - (tap / 3) * 3;
+        const char* xa = xr_ + ((2 * i + r) % NSX) * XB;
+        const char* xb = xr_ + ((2 * i + 1 + r) % NSX) * XB;
+        const int cb = 2 * u + (li & 1);
+        const int p0 = plv + s3, p1 = plv + 8 + s3;
+        const int o0 = p0 * 64 + ((cb ^ swz8x(p0)) << 3), o1 = p1 * 64 + ((cb ^ swz8x(p1)) << 3);
+        const v2i_t r0 = tr8(xa + o0), r1 = tr8(xa + o1), r2 = tr8(xb + o0), r3 = tr8(xb + o1);
+        return v8i{r0[0], r0[1], r1[0], r1[1], r2[0], r2[1], r3[0], r3[1]};
+      };
+      v8i bcur = xfrag(0);
+#pragma unroll
+      for (int j = 0; j < NK; ++j) {
+        v8i bnext = bcur;
+        if (j + 1 < NK) bnext = xfrag(j + 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q][j] = mma_f8(af[q], bcur, acc[q][j]);
+        bcur = bnext;
+      }
+      if (do_bias) {
+        const v8i ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838};
+        accb[0] = mma_f8(af[2 * WK], ones, accb[0]);
+        accb[1] = mma_f8(af[2 * WK + 1], ones, accb[1]);
+      }
+    }
+    const float dq = a.dqx[0] * a.dqdy[0], dqb = a.dqdy[0];
+    const long KW = 9L * a.Cin;
+    float* sl = a.slab + (long)split * a.Cout * KW;
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const int kt = NK * WK + j, tap = kt >> 2;
+      const int kcol = tap * a.Cin + ci0 + (kt & 3) * 16 + li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) sl[(long)(co0 + wc * 64 + q * 16 + 4 * g + jj) * KW + kcol] = acc[q][j][jj] * dq;
+    }
+    if (do_bias && li == 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          a.bslab[(long)split * a.Cout + co0 + wc * 64 + (2 * WK + t) * 16 + 4 * g + jj] = accb[t][jj] * dqb;
+    }
+  });
+}
+
 // fp8 conv eligibility: 3x3, stride 1, 'same', channel counts multiples of 128 (in and out),
 // W % 64 == 0, H % 4 == 0, bf16 NHWC output, operands < 2 GB
 bool fp8_ok(const fv_conv_desc* d) {
@@ -5178,6 +5378,35 @@ int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const floa
   FV_REQUIRE(fp8_ok(d), "fp8 conv: unsupported descriptor");
   FV_REQUIRE(dy8 && dy_dq && wt && wt_dq && dx, "null pointer");
   return conv_fp8_run(d, d->cout, d->cin, dy8, dy_dq, wt, wt_dq, nullptr, nullptr, dx, nullptr, (hipStream_t)stream);
+}
+
+int fv_conv2d_wgrad_fp8_supported(const fv_conv_desc* d) {
+  static int off = -1;          // FV_FP8_WGRAD=0: the bf16 weight gradient in fp8 mode (A/B)
+  if (off < 0) {
+    const char* e = getenv("FV_FP8_WGRAD");
+    off = (e && e[0] == '0') ? 1 : 0;
+  }
+  if (off || check_desc(d) != FV_OK || !fp8_ok(d) || d->cin % 64 || d->cout % 128) return 0;
+  const WgPlan t = plan_wgrad(d);
+  return t.v2 == 5 && t.ntk == d->cin / 64 && t.sps % 2 == 0 && d->h % t.sps == 0 ? 1 : 0;
+}
+
+int fv_conv2d_bwd_weight_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_dq, const uint8_t* dy8,
+                             const float* dy_dq, float* slab, float* bias_slab, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fv_conv2d_wgrad_fp8_supported(d), "fp8 weight gradient: unsupported descriptor");
+  FV_REQUIRE(x8 && x_dq && dy8 && dy_dq && slab, "null pointer");
+  const WgPlan t = plan_wgrad(d);
+  const long P = (long)d->n * d->h * d->w;
+  Wg8Args a{};
+  a.x8 = x8; a.dy8 = dy8; a.dqx = x_dq; a.dqdy = dy_dq; a.slab = slab; a.bslab = bias_slab;
+  a.H = d->h; a.W = d->w; a.Cin = d->cin; a.Cout = d->cout;
+  a.nseg = t.nsteps; a.rows = t.sps; a.nct = t.ntc; a.nci = t.ntk;
+  a.xbytes = (unsigned)(P * d->cin);
+  a.dybytes = (unsigned)(P * d->cout);
+  hipLaunchKernelGGL(conv3_wgrad_fp8<3>, dim3(t.ntc * t.ntk * t.nsplit), dim3(256), 0, (hipStream_t)stream, a);
+  return fv_check_launch("conv2d_bwd_weight_fp8");
 }
 
 // BN-statistics records of fv_conv2d_fwd_fp8: one per wave row of the 128 co x 256 px tile

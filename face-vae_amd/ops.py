@@ -339,6 +339,9 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
     if cs.fp8:
         site = fp8_site(cs.conv, "x", x.device)
         x8, xdq = x8 if x8 is not None else quantize_fp8_site(x, site)
+        # the e4m3 operand stays for the fp8 weight gradient (its dq is the site's word 18, which
+        # only this forward's quantization wrote until the next forward)
+        cs.x8 = (x8, xdq)
         _timed("fwd", d, lambda: call("fv_conv2d_fwd_fp8_site", ctypes.byref(d), ptr(x8), ptr(site[0]), ptr(cs.wk),
                                       ptr(cs.wdq), ptr(bias), ptr(res), ptr(y), ptr(part), stream()))
         if CHECK is not None:
@@ -399,14 +402,27 @@ def _wgrad(cs: ConvState, x, dy, ldd, pro, need_db):
     return _wgrad_finish(cs, x, dy, ldd, pro, need_db, slab, bslab)
 
 
-def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab):
+def _wgrad_fp8(cs: ConvState, x, dy, ldd, need_db, dy8):
+    d = cs.d
+    dev = dy.device
+    x8, xdq = cs.x8
+    dy8_, dydq = dy8
+    slab = _empty(query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), F32, dev)
+    bslab = _empty(query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), F32, dev) if need_db else None
+    _timed("wgrad", d, lambda: call("fv_conv2d_bwd_weight_fp8", ctypes.byref(d), ptr(x8), ptr(xdq), ptr(dy8_), ptr(dydq),
+                                    ptr(slab), ptr(bslab), stream()))
+    cs.x8 = None
+    return _wgrad_finish(cs, x, dy, ldd, None, need_db, slab, bslab, q8=(x8, xdq, dy8_, dydq))
+
+
+def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab, q8=None):
     d = cs.d
     dev = dy.device
     dw = torch.empty_like(cs.w)
     db = torch.empty(d.cout, dtype=F32, device=dev) if need_db else None
     call("fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(dw), ptr(db), stream())
     if CHECK is not None:
-        CHECK("wgrad", cs, x=x, dy=dy, ldd=ldd, dw=dw, db=db, pro=pro)
+        CHECK("wgrad", cs, x=x, dy=dy, ldd=ldd, dw=dw, db=db, pro=pro, q8=q8)
     if cs.conv.sn and not (_sn_defer_ok(cs) and _sn_defer(cs)):
         spectral_norm_bwd(cs.w, dw, cs.u, cs.v, cs.sigma)
     return dw, db
@@ -470,8 +486,15 @@ def _sn_defer(cs: ConvState) -> bool:
 def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=True, bnred=None, want_recs=False,
                   dy8=None):
     """-> (dx at the conv input resolution (upsample folded back), dW (param layout), db
-    [, BNRecords or None when want_recs]).  dy8: (e4m3 copy of dy, dq) from dy's producer."""
-    dw, db = _wgrad(cs, x, dy, ldd, pro, need_db)
+    [, BNRecords or None when want_recs]).  dy8: (e4m3 copy of dy, dq) from dy's producer.
+    fp8: the weight gradient runs on the e4m3 x (kept by the forward) and dy as well, when the
+    shape allows (fv_conv2d_wgrad_fp8_supported)."""
+    if cs.fp8 and getattr(cs, "x8", None) is not None and query("fv_conv2d_wgrad_fp8_supported", ctypes.byref(cs.d)):
+        site = fp8_site(cs.conv, "dy", dy.device)
+        dy8 = dy8 if dy8 is not None else quantize_fp8_site(dy, site)
+        dw, db = _wgrad_fp8(cs, x, dy, ldd, need_db, dy8)
+    else:
+        dw, db = _wgrad(cs, x, dy, ldd, pro, need_db)
     dx, recs = _dgrad(cs, dy, ldd, need_dx, bnred, dy8)
     return (dx, dw, db, recs) if want_recs else (dx, dw, db)
 

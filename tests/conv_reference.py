@@ -315,6 +315,18 @@ class LaunchChecker:
                 dx = t["dx"][:, :d.cin_valid].float()
                 rl2, worst = compare(dx, ref[:, :d.cin_valid], out_bf16=bf)
                 self._add(name, kind, d, rl2, worst)
+            elif t.get("q8") is not None:                 # fp8 weight gradient: dequantized operands
+                x8, xdq, dy8, dydq = t["q8"]
+                N, Cp, H, W = t["x"].shape
+                xq = x8.view(torch.float8_e4m3fn).float().view(N, H, W, Cp).permute(0, 3, 1, 2) * xdq
+                dyq = dy8.view(torch.float8_e4m3fn).float().view(N, H, W, d.cout).permute(0, 3, 1, 2) * dydq
+                rw, rb = conv_wgrad_ref(xq.contiguous(), dyq.contiguous(), k, ups)
+                aw, ab = conv_wgrad_ref(xq.abs().contiguous(), dyq.abs().contiguous(), k, ups)
+                rl2, worst = compare_sum(t["dw"], rw, aw)
+                self._add(name, "wgrad8", d, rl2, worst)
+                if t.get("db") is not None:
+                    rl2b, wb = compare_sum(t["db"], rb, ab)
+                    self._add(name, "bgrad8", d, rl2b, wb)
             else:
                 x = t["x"][:, :d.cin_valid].float()
                 x = pro_input(x, t.get("pro"), d.pro_slope, self.dtype)

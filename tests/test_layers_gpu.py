@@ -97,7 +97,7 @@ def _dead_biases(cfg):
 
 
 def _gate(gate, r, cfg):
-    if r["kind"] == "bgrad" and r["layer"] in _dead_biases(cfg):
+    if r["kind"] in ("bgrad", "bgrad8") and r["layer"] in _dead_biases(cfg):
         return float("inf")
     return gate[r["kind"]]
 
@@ -183,7 +183,11 @@ def _fp8_launch_check(B):
     print(f"\n[256x256 B={B} fp8] per-launch deviation\n" + chk.report())
     kinds = [r["kind"] for r in chk.rows]
     assert kinds.count("fwd8") == 14 and kinds.count("dgrad8") == 14       # + AFE.down2 (128 -> 256)
+    # the fp8 weight gradients: the same 14 convs, fp32 sums of exact e4m3
+    # products vs the float64 reference on the dequantized operands
+    assert kinds.count("wgrad8") == 14 and kinds.count("bgrad8") == 14
     gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 1e-4, "fwd8": 5e-3, "dgrad8": 5e-3,
+            "wgrad8": 1e-4, "bgrad8": 1e-4,
             "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
     cfg = fv.FaceVAEConfig()
     bad = [r for r in chk.rows if not (r["rel_l2"] <= _gate(gate, r, cfg) and r["worst"] <= 1.0)]

@@ -163,6 +163,13 @@ def main():
                 us = timeit(lambda: L.call("fv_quantize_fp8", L.dtype_code(dtype), x.data_ptr(), x.numel(),
                                            x8.data_ptr(), xdq.data_ptr(), ws.data_ptr(), L.stream()), a.iters)
                 row["fp8_quant_us"] = round(us, 1)
+            if "wgrad" in kinds and L.query("fv_conv2d_wgrad_fp8_supported", ctypes.byref(d)):
+                slab8 = torch.empty(L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), device="cuda")
+                bslab8 = torch.empty(L.query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), device="cuda")
+                us = timeit(lambda: L.call("fv_conv2d_bwd_weight_fp8", ctypes.byref(d), x8.data_ptr(), xdq.data_ptr(),
+                                           dy8.data_ptr(), dydq.data_ptr(), slab8.data_ptr(), bslab8.data_ptr(),
+                                           L.stream()), a.iters)
+                row["fp8_wgrad_us"], row["fp8_wgrad_tf"] = round(us, 1), round(flop / us / 1e6, 1)
             if "dgrad" in kinds:
                 dxf = torch.empty(B, cp, H, H, dtype=dtype, device="cuda", memory_format=CL)
                 us = timeit(lambda: L.call("fv_conv2d_bwd_data_fp8", ctypes.byref(d), dy8.data_ptr(), dydq.data_ptr(),
