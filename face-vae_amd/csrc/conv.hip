@@ -3389,14 +3389,16 @@ bool use_v2(const fv_conv_desc* d) {
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
 
-// BN-apply + activation prologue in the halo staging (conv3_halo_fwd3<..., PRO>): the NAC
-// ResBlock convs (256-channel co tiles, <= 256 input channels).  FV_NAC_STAGED=0 turns it off
-// (the model then materialises act(BN(x)) with a separate pass, for A/B)
+// BN-apply + activation prologue in the halo staging (conv3_halo_fwd3<..., PRO>, the sliding-row
+// weight gradient's PRO variant): the NAC ResBlock convs (256-channel co tiles, <= 256 input
+// channels).  Measured SLOWER than materialising act(BN(x)) with the separate pass (r4, one box,
+// B=32: res fwd 147-155 -> 170-172 us, wgrad 157-162 -> 169 us against the 21.5 us act_fwd pass
+// each saves; step 12.48 -> 12.70 ms), so it is off by default; FV_NAC_STAGED=1 turns it on.
 static int g_nac_staged = -1;
 bool nac_staged_enabled() {
   if (g_nac_staged < 0) {
     const char* e = getenv("FV_NAC_STAGED");
-    g_nac_staged = (e && e[0] == '0') ? 0 : 1;
+    g_nac_staged = (e && e[0] == '1') ? 1 : 0;
   }
   return g_nac_staged != 0;
 }

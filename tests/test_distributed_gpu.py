@@ -251,12 +251,18 @@ def test_dataparallel_syncbn_256_two_ranks_match_single_process(dtype_name):
     assert dev["image_vs_oracle"] < 2e-2 and dev["R_vs_oracle"] < 1e-3
     assert gv[len(gv) // 2] < 1e-2
     for k, v in gdev.items():
-        assert v <= 3e-2 or (k in RESIDUAL_SUM_BIASES and v <= 2 * gora[k]), (k, v, gora[k])
+        assert v <= 3e-2 or (residual_sum_bias(k) and v <= 2 * gora[k]), (k, v, gora[k])
     assert max(bn.values()) < 1e-5
 
 
-# conv biases whose gradient is the pixel sum of the ResBlock stack's residual-stream gradient
-RESIDUAL_SUM_BIASES = {"generator.mid_conv.bias"}
+def residual_sum_bias(k):
+    """Conv biases whose gradient is the pixel sum of the ResBlock stack's residual-stream
+    gradient: Generator.mid_conv (its output is the stack's input) and every ResBlock's second
+    conv (its output is added to the stream).  In bf16 that sum is dominated by the rounding
+    noise of the cancelling bn1-backward terms (measured r4: the single process is 8-17 % off
+    the fp32 oracle on them)."""
+    import re
+    return k == "generator.mid_conv.bias" or re.fullmatch(r"generator\.res\.\d+\.layers\.1\.layers\.2\.bias", k) is not None
 
 
 def _eval_worker(rank, port, q):
