@@ -4188,7 +4188,10 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // Stage-major weights (every DMA piece one contiguous KB, weight_prep_body smaj): res
     // fwd / dgrad 127 / 121.5 -> 122 / 117 us, down2 dgrad 317 -> 301 us (kept).  The weights
     // off the LDS-DMA path -- each wave's A fragments loaded to registers two / one taps ahead,
-    // the halo register-staged, one barrier per 32-channel chunk: 126 -> 134 us (not kept).)
+    // the halo register-staged, one barrier per 32-channel chunk: 126 -> 134 us (not kept).
+    // r4: the 256 x 256 tile on 4 waves of 128 co x 128 px (one wave per SIMD, 512 registers,
+    // a third fewer LDS fragment bytes per MFMA): res fwd / dgrad 133 / 127 -> 162 / 153 us,
+    // the SIMD partner's MFMAs no longer cover a wave's fragment reads and barrier waits.)
     if (d->pro_act) {
       FV_REQUIRE(bn == 256 && psc && psh, "staged BN prologue: bad arguments");
       hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb);

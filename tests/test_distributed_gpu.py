@@ -227,16 +227,23 @@ def test_dataparallel_syncbn_256_two_ranks_match_single_process(dtype_name):
     gora = {k: _rel(gs[k], og[k]) for k in gs if k not in dead}
     bn = {k: _rel(a0[k], st[k]) for k in st if k.endswith("running_mean") or k.endswith("running_var")}
     gv = sorted(gdev.values())
+    go = sorted(gora.values())
     top = sorted(gdev, key=gdev.get)[-4:]
-    print(f"\n[2 ranks x 2, 256x256 {dtype_name}, SyncBN] {dev}\n  grads vs 1 process: median {gv[len(gv) // 2]:.2e}; "
+    print(f"\n[2 ranks x 2, 256x256 {dtype_name}, SyncBN] {dev}\n  grads vs 1 process: median {gv[len(gv) // 2]:.2e} "
+          f"(1 process vs oracle: median {go[len(go) // 2]:.2e}); "
           + ", ".join(f"{k} {gdev[k]:.2e} (1 process vs oracle {gora[k]:.2e})" for k in top)
           + f"; BN running stats worst {max(bn.values()):.2e}")
     if fp8:
         assert dev["image_vs_1proc"] < 5e-2 and dev["R_vs_1proc"] < 1e-2 and dev["K_vs_1proc"] < 1e-3
         assert dev["image_vs_oracle"] < 5e-2 and dev["R_vs_oracle"] < 1e-2
-        assert gv[len(gv) // 2] < 5e-2
+        # measured (r4): median 0.42 against the single process, whose own median deviation from
+        # the fp32 oracle is of the same size -- on a first step from random init most gradients
+        # here (BN gamma / beta, the ResBlock convs behind a BN) are pixel sums that cancel to a
+        # few % of their terms, so the e4m3 rounding of dy / x (2^-4 relative) dominates them.
+        # Two scale choices are two independent draws of that noise: gated at twice its size
+        assert gv[len(gv) // 2] < 2 * go[len(go) // 2]
         for k, v in gdev.items():
-            assert v < max(0.25, 2 * gora[k]), k
+            assert v < max(0.25, 2 * gora[k]), (k, v, gora[k])
         assert max(bn.values()) < 5e-3
         return
     # measured (r3): forward bit-identical (image 0.0, BN running stats 0.0), K 5e-8; gradients
