@@ -61,6 +61,7 @@ class SegmentRecorder:
         # engine's device thread, so a segment is ended (and the next begun) on another thread
         # than the one that began the capture -- allowed only for relaxed-mode captures
         g = torch.cuda.CUDAGraph()
+        self.stream = torch.cuda.current_stream()
         g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
         self.graphs.append(g)
         self.open = True
@@ -81,7 +82,10 @@ class SegmentRecorder:
         if self.open:
             self.open = False
             try:
-                self.graphs[-1].capture_end()
+                # capture_end must run with the capture stream current (the caller's except
+                # clause is outside the capture's stream context)
+                with torch.cuda.stream(self.stream):
+                    self.graphs[-1].capture_end()
             except Exception:      # an invalidated capture still leaves capture mode; the original error is raised
                 pass
 
