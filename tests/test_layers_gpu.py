@@ -183,11 +183,15 @@ def _fp8_launch_check(B):
     print(f"\n[256x256 B={B} fp8] per-launch deviation\n" + chk.report())
     kinds = [r["kind"] for r in chk.rows]
     assert kinds.count("fwd8") == 14 and kinds.count("dgrad8") == 14       # + AFE.down2 (128 -> 256)
-    # the fp8 weight gradients: the same 14 convs, fp32 sums of exact e4m3
-    # products vs the float64 reference on the dequantized operands
+    # the fp8 weight gradients: the same 14 convs vs the float64 reference on
+    # the dequantized operands.  The scaled fp8 MFMA adds its products in groups of 8, truncated
+    # ~13 bits below the group's largest (test_fp8_gpu.py::test_fp8_mfma_accumulation_groups):
+    # elementwise <= 2^-10 of sum|terms| (conv_reference.compare_sum), and that truncation is
+    # biased, so on a ResBlock's conv1 -- whose dy is a BN backward output with ~7 % e4m3
+    # subnormals and whose weight-gradient sums cancel -- rel-L2 reaches 4e-3 (measured r4, B=64)
     assert kinds.count("wgrad8") == 14 and kinds.count("bgrad8") == 14
     gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 1e-4, "fwd8": 5e-3, "dgrad8": 5e-3,
-            "wgrad8": 1e-4, "bgrad8": 1e-4,
+            "wgrad8": 1e-2, "bgrad8": 1e-2,
             "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
     cfg = fv.FaceVAEConfig()
     bad = [r for r in chk.rows if not (r["rel_l2"] <= _gate(gate, r, cfg) and r["worst"] <= 1.0)]
