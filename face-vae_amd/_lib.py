@@ -12,7 +12,8 @@ from ctypes import POINTER, c_float, c_int, c_long, c_size_t, c_void_p
 import torch  # noqa: F401  (must be imported first: the HIP runtime is shared with torch)
 
 _HERE = os.path.dirname(os.path.realpath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfacevae.so")
+# FV_LIB_PATH: another build of the library (A/B of two builds on one box, tools/gpu.sh ab)
+LIB_PATH = os.environ.get("FV_LIB_PATH") or os.path.join(_HERE, "libfacevae.so")
 
 FV_F32, FV_BF16, FV_F64 = 0, 1, 2
 ADAM_CHUNK = 4096

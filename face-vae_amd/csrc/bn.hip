@@ -124,6 +124,10 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
 // two-level partials -> sum_finalize pair ran on C/16 blocks: 6.7 + 8.9 us per layer, latency
 // bound).  Fixed order: thread t sums rows t, t + 1024, ... in order, then a fixed xor tree per
 // wave and the 16 wave sums in wave order -> bit-reproducible.
+// (measured and not kept, r4: (C / 64 channel groups) x (record chunks) blocks with coalesced
+// 256-B row reads, each chunk's fp64 partial published by an agent-scope release + arrival
+// counter and the last block of a group adding them in chunk order -- the release writes back
+// the XCD's L2 per block: +6..8 us per fold, step 12.50 -> 12.86 ms.)
 // ---------------------------------------------------------------------------------------------
 constexpr int FOLDT = 1024;
 enum { FOLD_STATS = 0, FOLD_FWD = 1, FOLD_BWD = 2 };

@@ -1046,6 +1046,34 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   FV_DIAG_END();
 }
 
+// B fragments of tap (r, s) from those of tap (r, s - 1) in registers (conv3_halo_fwd3 DRV): the
+// fragment of output pixels 16m .. 16m + 15 at column shift s is the shift-(s-1) fragment moved
+// down one lane within each 16-lane row (DPP row_shl:1, the k-chunk rows stay put), lane 15
+// taking lane 0 of fragment m + 1 (row_shr:15) -- or, at the end of a 64-pixel image row, the
+// halo pixel 63 + s, read once per row as a broadcast.  Bit-identical to the LDS reads it
+// replaces.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+template <int CTRL>
+__device__ __forceinline__ v4i_t dpp4(const v4i_t& a) {
+  v4i_t o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = __builtin_amdgcn_update_dpp(0, a[k], CTRL, 0xf, 0xf, true);
+  return o;
+}
+__device__ __forceinline__ bf16x8 tap_shift(const bf16x8& cur, const bf16x8& next) {
+  const v4i_t a = dpp4<0x101>(__builtin_bit_cast(v4i_t, cur));      // row_shl:1
+  const v4i_t b = dpp4<0x11f>(__builtin_bit_cast(v4i_t, next));     // row_shr:15
+  return __builtin_bit_cast(bf16x8, a | b);
+}
+__device__ __forceinline__ bf16x8 tap_shift_end(const bf16x8& cur, const bf16x8& carry, bool l15) {
+  const v4i_t a = dpp4<0x101>(__builtin_bit_cast(v4i_t, cur));
+  const v4i_t c = __builtin_bit_cast(v4i_t, carry);
+  v4i_t o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = l15 ? c[k] : a[k];
+  return __builtin_bit_cast(bf16x8, o);
+}
+
 // Linear-halo variant of conv3_halo_fwd2: every LDS fragment address is a per-lane base
 // register plus an immediate.  In fwd2 the XOR swizzle of a 64-B halo pixel moves with the tap
 // shift, so each of the 16 fragment reads of a step costs ~5 VALU (88 non-MFMA VALU per 64
@@ -1067,7 +1095,10 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
 // runs MFMAs), published by the following barrier, before its first fragment read (the first
 // read needs it published by barrier floor(9c / 2) - 1 (c even) / (9c - 3) / 2 (c odd), the
 // later half publishes at barrier 9c / 2 - 2 / (9c - 5) / 2).
-template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false>
+//
+// DRV: the B fragments of taps with s > 0 come from the previous tap's in registers (tap_shift):
+// 2 broadcast LDS reads per tap instead of RM fragment reads.
+template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, bool DRV = false>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
@@ -1179,14 +1210,27 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   // adds one wave-uniform offset to each (2 VALU per tap); the fragments are immediates.
   const int va = (wn * RN * 16 + lr) * 64 + ((lh ^ rswz<bf16>(lr)) << 4);
   const int vb = WOFF + ((wm * RM / 4) * 66 + lr) * PXB + lh * 16;
-  auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], int u, int buf) {
+  // DRV: the lane's address of halo pixel 63 (+ the tap's row / column offset): the carry of a row
+  const int vx = WOFF + ((wm * RM / 4) * 66 + 63) * PXB + lh * 16;
+  const bool l15 = lr == 15;
+  auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], const Frag<bf16> (&pfb)[RM], int u, int buf) {
     const int c = u / 9, t = u - c * 9, r = t / 3, s3 = t - (t / 3) * 3;
     const int pa = va + (buf * STG + (u & 1) * BST);
-    const int pb = vb + ((c & 1) * HALO + (r * 66 + s3) * PXB);
 #pragma unroll
     for (int i = 0; i < RN; ++i) fa[i].lds(smem + pa + i * 1024);
+    if (DRV && s3 != 0) {
+      const int px = vx + ((c & 1) * HALO + (r * 66 + s3) * PXB);
+      Frag<bf16> cx[RM / 4];
 #pragma unroll
-    for (int m = 0; m < RM; ++m) fb[m].lds(smem + pb + (((m * 16) >> 6) * 66 + ((m * 16) & 63)) * PXB);
+      for (int q = 0; q < RM / 4; ++q) cx[q].lds(smem + px + q * 66 * PXB);
+#pragma unroll
+      for (int m = 0; m < RM; ++m)
+        fb[m].v = (m & 3) == 3 ? tap_shift_end(pfb[m].v, cx[m >> 2].v, l15) : tap_shift(pfb[m].v, pfb[m + 1 < RM ? m + 1 : m].v);
+    } else {
+      const int pb = vb + ((c & 1) * HALO + (r * 66 + s3) * PXB);
+#pragma unroll
+      for (int m = 0; m < RM; ++m) fb[m].lds(smem + pb + (((m * 16) >> 6) * 66 + ((m * 16) & 63)) * PXB);
+    }
   };
   f32x4 acc[RN][RM];
 #pragma unroll
@@ -1223,12 +1267,12 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     issue_b(NSB - 1, NSB - 1);
     pend = bcnt(NSB - 1);
   }
-  load_frags(fa0, fb0, 0, 0);
+  load_frags(fa0, fb0, fb1, 0, 0);
   int hn = 2, hstep = (9 * 2 - 10) / 2;
   int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
   int bj = 0;
   for (int j = 0; j < nsteps; ++j) {
-    load_frags(fa1, fb1, 2 * j + 1, bj);
+    load_frags(fa1, fb1, fb0, 2 * j + 1, bj);
     mfma_all(fa0, fb0);
     const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
     if (j + 1 < nsteps) {
@@ -1254,7 +1298,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
         issue_b(j + NSB, bj);
         pend = bcnt(j + NSB);
       }
-      load_frags(fa0, fb0, 2 * j + 2, bn1);
+      load_frags(fa0, fb0, fb1, 2 * j + 2, bn1);
       FV_DIAG_ISSUE_END();
     }
     mfma_all(fa1, fb1);
@@ -3394,6 +3438,15 @@ bool use_v2(const fv_conv_desc* d) {
 // channels).  Measured SLOWER than materialising act(BN(x)) with the separate pass (r4, one box,
 // B=32: res fwd 147-155 -> 170-172 us, wgrad 157-162 -> 169 us against the 21.5 us act_fwd pass
 // each saves; step 12.48 -> 12.70 ms), so it is off by default; FV_NAC_STAGED=1 turns it on.
+// conv3_halo_fwd3 DRV (B fragments of s > 0 taps shifted in registers); FV_TAPSHIFT=0 for A/B
+static int g_tapshift = -1;
+bool tapshift_enabled() {
+  if (g_tapshift < 0) {
+    const char* e = getenv("FV_TAPSHIFT");
+    g_tapshift = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_tapshift != 0;
+}
 static int g_nac_staged = -1;
 bool nac_staged_enabled() {
   if (g_nac_staged < 0) {
@@ -4196,7 +4249,11 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
       FV_REQUIRE(bn == 256 && psc && psh, "staged BN prologue: bad arguments");
       hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn >= 128 && a.Cin % 64 == 0) {
-      if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+      if (bn == 256 && tapshift_enabled())
+        hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
+      else if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+      else if (tapshift_enabled())
+        hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 256) {
       hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
