@@ -119,17 +119,17 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
 // Record folds (+ finalize): the per-channel sums of a BN layer arrive as `nrec` rows of partial
 // sums -- fp32 (sum, sum of squares) records of a conv epilogue / store pass ([r][2][C]), or the
 // fp64 per-block rows of a streaming pass ([b][3][C] with a count row, [b][2][C] backward sums).
-// ONE launch folds them and finishes the layer: grid = C blocks of 1024 threads, one channel per
-// block, so a fold of up to ~16k records is one round of loads on (up to) every CU (the previous
-// two-level partials -> sum_finalize pair ran on C/16 blocks: 6.7 + 8.9 us per layer, latency
-// bound).  Fixed order: thread t sums rows t, t + 1024, ... in order, then a fixed xor tree per
-// wave and the 16 wave sums in wave order -> bit-reproducible.
-// (measured and not kept, r4: (C / 64 channel groups) x (record chunks) blocks with coalesced
-// 256-B row reads, each chunk's fp64 partial published by an agent-scope release + arrival
-// counter and the last block of a group adding them in chunk order -- the release writes back
-// the XCD's L2 per block: +6..8 us per fold, step 12.50 -> 12.86 ms.)
+// ONE launch folds up to FOLDR records and finishes the layer: a block owns 8 channels, each
+// thread reads whole 32 / 64-B channel octets of rows t, t + 256, ... (r3's one-channel-per-block
+// fold read 4 B of every 128-B line -- 32x line traffic: 11-16 us per res-conv layer, 45-70 us
+// for the 16k-record full-resolution layers, r4 trace).  More records: chunk partials [chunk]
+// [NV][C] into the caller's workspace, then the same fold over them.  Fixed order (rows in
+// thread order, a fixed xor tree per wave, waves in order, chunks in order): bit-reproducible.
+// (measured and not kept, r4: one launch with the chunks published by an agent-scope release +
+// arrival counter, the last block adding them -- the release writes back the XCD's L2 per
+// block: +6..8 us per fold, step 12.50 -> 12.86 ms.)
 // ---------------------------------------------------------------------------------------------
-constexpr int FOLDT = 1024;
+constexpr int FOLDB = 256, FOLDR = 1024;    // threads per fold block, records per fold block
 enum { FOLD_STATS = 0, FOLD_FWD = 1, FOLD_BWD = 2 };
 struct FoldArgs {
   const void* src;
@@ -151,34 +151,62 @@ struct FoldArgs {
   double* red;
 };
 
-template <typename T, int NV, int MODE>
-__global__ void __launch_bounds__(FOLDT) fold_kernel(FoldArgs a) {
-  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const T* src = reinterpret_cast<const T*>(a.src) + c;
-  const long vs = a.C;
-  double acc[NV];
+// 8 consecutive channels of one row (T = float records / double streaming rows) into acc
+template <typename T>
+__device__ __forceinline__ void fold_load8(const T* p, double* acc) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+  } else {
 #pragma unroll
-  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
-#pragma unroll 8
-  for (int r = tid; r < a.nrec; r += FOLDT) {
+    for (int h = 0; h < 4; ++h) {
+      const double2 d = reinterpret_cast<const double2*>(p)[h];
+      acc[2 * h] += d.x;
+      acc[2 * h + 1] += d.y;
+    }
+  }
+}
+
+template <typename T, int NV, int MODE>
+__global__ void __launch_bounds__(FOLDB) fold_kernel(FoldArgs a, double* part) {
+  const int c0 = blockIdx.x * 8, ch = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = ch * FOLDR, r1 = min(a.nrec, r0 + FOLDR);
+  double acc[NV][8];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[v][q] = 0.0;
+  const T* src = reinterpret_cast<const T*>(a.src) + c0;
+#pragma unroll 2
+  for (int r = r0 + tid; r < r1; r += FOLDB) {
     const T* p = src + (long)r * a.rstride;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) acc[v] += (double)p[v * vs];
+    for (int v = 0; v < NV; ++v) fold_load8<T>(p + (long)v * a.C, acc[v]);
   }
-  __shared__ double red[NV][FOLDT / 64];
+  __shared__ double red[FOLDB / 64][NV * 8];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const double t = wave_sum_d(acc[v]);
-    if (lane == 0) red[v][w] = t;
-  }
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double t = wave_sum_d(acc[v][q]);
+      if (lane == 0) red[w][v * 8 + q] = t;
+    }
   __syncthreads();
-  if (tid != 0) return;
+  if (tid >= 8) return;
+  const int c = c0 + tid;
   double tot[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     double t = 0.0;
-    for (int j = 0; j < FOLDT / 64; ++j) t += red[v][j];
+#pragma unroll
+    for (int j = 0; j < FOLDB / 64; ++j) t += red[j][v * 8 + tid];
     tot[v] = t;
+  }
+  if (part) {                        // level 1 of a two-level fold: row ch of [chunk][NV][C] doubles
+#pragma unroll
+    for (int v = 0; v < NV; ++v) part[((long)ch * NV + v) * a.C + c] = tot[v];
+    return;
   }
   // (n, S, Q): rows with a count row carry it first; fp32 records are counted by P
   const double n = NV == 3 ? tot[0] : (double)a.P;
@@ -206,9 +234,23 @@ __global__ void __launch_bounds__(FOLDT) fold_kernel(FoldArgs a) {
   }
 }
 
+// scratch: room for ceil(nrec / FOLDR) x NV x C doubles when nrec > FOLDR (the records then
+// fold in two launches: chunk partials, then the partial rows)
 template <typename T, int NV, int MODE>
-int launch_fold(const FoldArgs& a, hipStream_t s, const char* what) {
-  hipLaunchKernelGGL((fold_kernel<T, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, a);
+int launch_fold(const FoldArgs& a, hipStream_t s, const char* what, double* scratch = nullptr) {
+  FV_REQUIRE(a.C % 8 == 0 && a.nrec > 0, "BN fold: channels must be a multiple of 8 (%d)", a.C);
+  const int nch = (a.nrec + FOLDR - 1) / FOLDR;
+  if (nch == 1) {
+    hipLaunchKernelGGL((fold_kernel<T, NV, MODE>), dim3(a.C / 8), dim3(FOLDB), 0, s, a, (double*)nullptr);
+    return fv_check_launch(what);
+  }
+  FV_REQUIRE(scratch && (const void*)scratch != a.src, "BN fold of %d records: no scratch", a.nrec);
+  hipLaunchKernelGGL((fold_kernel<T, NV, MODE>), dim3(a.C / 8, nch), dim3(FOLDB), 0, s, a, scratch);
+  FoldArgs b = a;
+  b.src = scratch;
+  b.nrec = nch;
+  b.rstride = (long)NV * a.C;
+  hipLaunchKernelGGL((fold_kernel<double, NV, MODE>), dim3(a.C / 8), dim3(FOLDB), 0, s, b, (double*)nullptr);
   return fv_check_launch(what);
 }
 
@@ -607,7 +649,7 @@ int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixe
   FV_REQUIRE((long)nblocks * block_pixels >= total_pixels, "bn_stats_from_partials: records do not cover the pixels");
   FoldArgs a{};
   a.src = partials; a.nrec = nblocks; a.C = c; a.rstride = 2L * c; a.P = total_pixels; a.stats = stats;
-  return launch_fold<float, 2, FOLD_STATS>(a, (hipStream_t)stream, "bn_fold_stats");
+  return launch_fold<float, 2, FOLD_STATS>(a, (hipStream_t)stream, "bn_fold_stats", (double*)ws);
 }
 
 int fv_bn_bwd_from_records(const float* records, int nrec, int record_pixels, long pixels, int c, long count,
@@ -617,7 +659,7 @@ int fv_bn_bwd_from_records(const float* records, int nrec, int record_pixels, lo
   FoldArgs a{};
   a.src = records; a.nrec = nrec; a.C = c; a.rstride = 2L * c;
   a.count = (double)count; a.dgamma = dgamma; a.dbeta = dbeta; a.k = k; a.red = red;
-  return launch_fold<float, 2, FOLD_BWD>(a, (hipStream_t)stream, "bn_bwd_fold_records");
+  return launch_fold<float, 2, FOLD_BWD>(a, (hipStream_t)stream, "bn_bwd_fold_records", (double*)ws);
 }
 
 int fv_bn_stats_tensor(int dtype, const void* x, long pixels, int c, int ldc, double* stats, void* ws,
@@ -660,12 +702,11 @@ int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_
   FV_REQUIRE(partials, "null pointer");
   FV_REQUIRE(nblocks > 0 && c > 0, "bad sizes");
   FV_REQUIRE((long)nblocks * block_pixels >= total_pixels, "bn_stats_finalize_partials: records do not cover the pixels");
-  (void)ws;
   FoldArgs a{};
   a.src = partials; a.nrec = nblocks; a.C = c; a.rstride = 2L * c; a.P = total_pixels;
   a.gamma = gamma; a.beta = beta; a.eps = eps; a.mom = momentum; a.rm = running_mean; a.rv = running_var;
   a.nbt = num_batches_tracked; a.save_mean = save_mean; a.save_invstd = save_invstd; a.scale = scale; a.shift = shift;
-  return launch_fold<float, 2, FOLD_FWD>(a, (hipStream_t)stream, "bn_fold_finalize");
+  return launch_fold<float, 2, FOLD_FWD>(a, (hipStream_t)stream, "bn_fold_finalize", (double*)ws);
 }
 
 int fv_bn_stats_finalize_tensor(int dtype, const void* x, long pixels, int c, int ldc, const float* gamma,
