@@ -119,17 +119,20 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
 // Record folds (+ finalize): the per-channel sums of a BN layer arrive as `nrec` rows of partial
 // sums -- fp32 (sum, sum of squares) records of a conv epilogue / store pass ([r][2][C]), or the
 // fp64 per-block rows of a streaming pass ([b][3][C] with a count row, [b][2][C] backward sums).
-// ONE launch folds up to FOLDR records and finishes the layer: a block owns 8 channels, each
-// thread reads whole 32 / 64-B channel octets of rows t, t + 256, ... (r3's one-channel-per-block
-// fold read 4 B of every 128-B line -- 32x line traffic: 11-16 us per res-conv layer, 45-70 us
-// for the 16k-record full-resolution layers, r4 trace).  More records: chunk partials [chunk]
-// [NV][C] into the caller's workspace, then the same fold over them.  Fixed order (rows in
-// thread order, a fixed xor tree per wave, waves in order, chunks in order): bit-reproducible.
-// (measured and not kept, r4: one launch with the chunks published by an agent-scope release +
-// arrival counter, the last block adding them -- the release writes back the XCD's L2 per
-// block: +6..8 us per fold, step 12.50 -> 12.86 ms.)
+// ONE launch folds up to FOLDR records and finishes the layer: one channel per block of 1024
+// threads (fold1_kernel).  More records (the full-resolution layers' 16k conv records): chunk
+// partials [chunk][NV][C] from blocks that own 8 channels and read whole 32 / 64-B channel
+// octets of their rows (fold_part_kernel), into the caller's workspace, then fold1 over them
+// (r3 folded 16k rows in one launch, 4 B per 128-B line: 45-70 us; now 23-25 us).  Fixed order
+// (rows in thread order, a fixed xor tree per wave, waves in order, chunks in order):
+// bit-reproducible.
+// (measured and not kept, r4: octet blocks for every fold -- 1024-row folds 11-21 us against
+// fold1's 8-13; one launch with the chunks published by an agent-scope release + arrival
+// counter, the last block adding them -- the release writes back the XCD's L2 per block: +6..8
+// us per fold, step 12.50 -> 12.86 ms.)
 // ---------------------------------------------------------------------------------------------
-constexpr int FOLDB = 256, FOLDR = 1024;    // threads per fold block, records per fold block
+constexpr int FOLDB = 256, FOLDR = 1024;    // threads per octet fold block, records per fold block
+constexpr int FOLDT = 1024;                 // threads per one-channel fold block
 enum { FOLD_STATS = 0, FOLD_FWD = 1, FOLD_BWD = 2 };
 struct FoldArgs {
   const void* src;
@@ -168,8 +171,10 @@ __device__ __forceinline__ void fold_load8(const T* p, double* acc) {
   }
 }
 
-template <typename T, int NV, int MODE>
-__global__ void __launch_bounds__(FOLDB) fold_kernel(FoldArgs a, double* part) {
+// level 1 of a fold of more than FOLDR records: block (octet, chunk) sums rows [chunk FOLDR,
+// (chunk + 1) FOLDR) of 8 channels -> part [chunk][NV][C] (fp64)
+template <typename T, int NV>
+__global__ void __launch_bounds__(FOLDB) fold_part_kernel(FoldArgs a, double* part) {
   const int c0 = blockIdx.x * 8, ch = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r0 = ch * FOLDR, r1 = min(a.nrec, r0 + FOLDR);
   double acc[NV][8];
@@ -194,19 +199,44 @@ __global__ void __launch_bounds__(FOLDB) fold_kernel(FoldArgs a, double* part) {
     }
   __syncthreads();
   if (tid >= 8) return;
-  const int c = c0 + tid;
-  double tot[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     double t = 0.0;
 #pragma unroll
     for (int j = 0; j < FOLDB / 64; ++j) t += red[j][v * 8 + tid];
-    tot[v] = t;
+    part[((long)ch * NV + v) * a.C + c0 + tid] = t;
   }
-  if (part) {                        // level 1 of a two-level fold: row ch of [chunk][NV][C] doubles
+}
+
+// <= FOLDR records (and level 2): one channel per block of 1024 threads, one row each
+template <typename T, int NV, int MODE>
+__global__ void __launch_bounds__(FOLDT) fold1_kernel(FoldArgs a) {
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const T* src = reinterpret_cast<const T*>(a.src) + c;
+  const long vs = a.C;
+  double acc[NV];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) part[((long)ch * NV + v) * a.C + c] = tot[v];
-    return;
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+#pragma unroll 8
+  for (int r = tid; r < a.nrec; r += FOLDT) {
+    const T* p = src + (long)r * a.rstride;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] += (double)p[v * vs];
+  }
+  __shared__ double red[NV][FOLDT / 64];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const double t = wave_sum_d(acc[v]);
+    if (lane == 0) red[v][w] = t;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double tot[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double t = 0.0;
+    for (int j = 0; j < FOLDT / 64; ++j) t += red[v][j];
+    tot[v] = t;
   }
   // (n, S, Q): rows with a count row carry it first; fp32 records are counted by P
   const double n = NV == 3 ? tot[0] : (double)a.P;
@@ -241,16 +271,16 @@ int launch_fold(const FoldArgs& a, hipStream_t s, const char* what, double* scra
   FV_REQUIRE(a.C % 8 == 0 && a.nrec > 0, "BN fold: channels must be a multiple of 8 (%d)", a.C);
   const int nch = (a.nrec + FOLDR - 1) / FOLDR;
   if (nch == 1) {
-    hipLaunchKernelGGL((fold_kernel<T, NV, MODE>), dim3(a.C / 8), dim3(FOLDB), 0, s, a, (double*)nullptr);
+    hipLaunchKernelGGL((fold1_kernel<T, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, a);
     return fv_check_launch(what);
   }
   FV_REQUIRE(scratch && (const void*)scratch != a.src, "BN fold of %d records: no scratch", a.nrec);
-  hipLaunchKernelGGL((fold_kernel<T, NV, MODE>), dim3(a.C / 8, nch), dim3(FOLDB), 0, s, a, scratch);
+  hipLaunchKernelGGL((fold_part_kernel<T, NV>), dim3(a.C / 8, nch), dim3(FOLDB), 0, s, a, scratch);
   FoldArgs b = a;
   b.src = scratch;
   b.nrec = nch;
   b.rstride = (long)NV * a.C;
-  hipLaunchKernelGGL((fold_kernel<double, NV, MODE>), dim3(a.C / 8), dim3(FOLDB), 0, s, b, (double*)nullptr);
+  hipLaunchKernelGGL((fold1_kernel<double, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, b);
   return fv_check_launch(what);
 }
 

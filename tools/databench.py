@@ -1,7 +1,7 @@
 """Input-pipeline throughput: FramesDataset (PNG decode, two frames per item) through a
 torch DataLoader, with and without the *_aug augmentation, on a synthetic frame tree.
 
-    python tools/databench.py [--workers 16] [--videos 64] [--frames 8] [--items 512]
+    python tools/databench.py [--workers 16] [--videos 64] [--frames 8] [--items 4096]
 
 Prints one JSON line: items/s and frames/s (an item = source + driving, 2 decoded frames) for
 each mode: the FaceVAE feed (FramesDataset(output="driving_uint8"): the driving frame as bytes,
@@ -69,7 +69,7 @@ def main():
     ap.add_argument("--workers", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--videos", type=int, default=64)
     ap.add_argument("--frames", type=int, default=8)
-    ap.add_argument("--items", type=int, default=512)
+    ap.add_argument("--items", type=int, default=4096)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--res", type=int, default=256)
     a = ap.parse_args()
