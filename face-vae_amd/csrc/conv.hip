@@ -3394,15 +3394,6 @@ bool use_v2(const fv_conv_desc* d) {
 // channels).  Measured SLOWER than materialising act(BN(x)) with the separate pass (r4, one box,
 // B=32: res fwd 147-155 -> 170-172 us, wgrad 157-162 -> 169 us against the 21.5 us act_fwd pass
 // each saves; step 12.48 -> 12.70 ms), so it is off by default; FV_NAC_STAGED=1 turns it on.
-// conv3_halo_fp8p (pipelined fp8 3x3); FV_FP8P=0 for A/B
-static int g_fp8p = -1;
-bool fp8p_enabled() {
-  if (g_fp8p < 0) {
-    const char* e = getenv("FV_FP8P");
-    g_fp8p = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_fp8p != 0;
-}
 static int g_nac_staged = -1;
 bool nac_staged_enabled() {
   if (g_nac_staged < 0) {
@@ -5047,173 +5038,6 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
 }
 
-// Pipelined variant (r4): a 3-deep weight ring issued 3 steps ahead (so a stage has two steps
-// to land, not one) and the next step's fragments read under this step's MFMAs -- the wave waits
-// at the step barrier with its MFMAs still executing (conv3_halo_fwd2's schedule, one tap of
-// K = 128 per step).  Step ks: issue stage ks + 3 into the buffer step ks - 1's barrier freed
-// (frags of ks are in registers), [halo of chunk c + 1 at t == 0], read frags of ks + 1, MFMAs
-// of ks, wait for stage ks + 2 (the younger DMAs may stay in flight), barrier.
-template <int WN, int WM, int RN, int RM>
-__global__ void __launch_bounds__(64 * WN * WM, 1)
-conv3_halo_fp8p(ConvArgs a, unsigned x_bytes) {
-  constexpr int NW = WN * WM;
-  constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
-  constexpr int HP = (TR + 2) * 66, HQ = (HP + 15) / 16;
-  constexpr int HALO = 2 * HQ * 1024;
-  constexpr int QH = 2 * HQ, JH = (QH + NW - 1) / NW;
-  constexpr int BST = BN * 128, QB = BN / 8, JB = QB / NW;
-  static_assert(QB % NW == 0, "weight pieces per wave");
-  constexpr int NSB = 3;
-  constexpr int MAIN = 2 * HALO + NSB * BST, EPI = BM * BN * 2;
-  static_assert(MAIN <= 163840, "LDS");
-  __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
-
-  if (a.roll && blockIdx.x == 0 && threadIdx.x == 0) fp8_site_roll(a.roll);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % WN, wm = wave / WN;
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int tn = lid % a.ntn, tm = lid / a.ntn;
-  const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
-  const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
-  const int co0 = tn * BN;
-  const int p0 = (n * a.H + th * TR) * a.W + tw * 64;
-
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
-  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
-
-  unsigned hoff[JH];
-#pragma unroll
-  for (int j = 0; j < JH; ++j) {
-    const int q = wave + j * NW;
-    const int img = q / HQ, hp = (q - img * HQ) * 16 + (lane >> 2), lchk = lane & 3;
-    const int hr = hp / 66, hc = hp - (hp / 66) * 66;
-    const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
-    const bool ok = q < QH && hp < HP && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-    hoff[j] = ok ? (unsigned)(((n * a.H + ih) * a.W + iw) * a.Cin + img * 64 + ((lchk ^ h3swz(hp)) << 4))
-                 : 0x80000000u;
-  }
-  const int nh = (QH - wave + NW - 1) / NW;        // halo pieces this wave issues
-  unsigned wbase[JB];
-#pragma unroll
-  for (int j = 0; j < JB; ++j) {
-    const int row = (wave + j * NW) * 8 + (lane >> 3);
-    wbase[j] = (unsigned)((co0 + row) * a.Kpad + (((lane & 7) ^ swz8(row)) << 4));
-  }
-  auto issue_b = [&](int ks) {
-    const int c = ks / 9, t = ks - c * 9;
-    const unsigned Bs = sbase + 2 * HALO + (ks % NSB) * BST;
-    const unsigned k0 = (unsigned)(t * a.Cin + c * 128);
-#pragma unroll
-    for (int j = 0; j < JB; ++j) dma16s(wr, Bs + (wave + j * NW) * 1024, wbase[j], k0);
-  };
-  auto issue_halo = [&](int c) {
-    const unsigned Hs = sbase + (c & 1) * HALO;
-#pragma unroll
-    for (int j = 0; j < JH; ++j)
-      if (j < JH - 1 || wave + j * NW < QH) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], (unsigned)(c * 128));
-  };
-
-  const int lr = lane & 15, lh = lane >> 4;
-  int hpb[RM];
-#pragma unroll
-  for (int m = 0; m < RM; ++m) {
-    const int loc = wm * RM * 16 + m * 16 + lr;
-    hpb[m] = (loc >> 6) * 66 + (loc & 63);
-  }
-  auto load_frags = [&](v8i (&fa)[RN], v8i (&fb)[RM], int ks) {
-    const int c = ks / 9, t = ks - c * 9, r = t / 3, s3 = t - (t / 3) * 3;
-    const char* Hs = smem + (c & 1) * HALO;
-    const char* Bs = smem + 2 * HALO + (ks % NSB) * BST;
-#pragma unroll
-    for (int i = 0; i < RN; ++i) {
-      const int row = wn * RN * 16 + i * 16 + lr;
-      const uint4 u0 = *reinterpret_cast<const uint4*>(Bs + row * 128 + ((lh ^ swz8(row)) << 4));
-      const uint4 u1 = *reinterpret_cast<const uint4*>(Bs + row * 128 + (((4 + lh) ^ swz8(row)) << 4));
-      fa[i] = v8i{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
-    }
-#pragma unroll
-    for (int m = 0; m < RM; ++m) {
-      const int hp = hpb[m] + r * 66 + s3;
-      const int off = hp * 64 + ((lh ^ h3swz(hp)) << 4);
-      const uint4 u0 = *reinterpret_cast<const uint4*>(Hs + off);
-      const uint4 u1 = *reinterpret_cast<const uint4*>(Hs + HQ * 1024 + off);
-      fb[m] = v8i{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
-    }
-  };
-  f32x4 acc[RN][RM];
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mfma_all = [&](const v8i (&fa)[RN], const v8i (&fb)[RM]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < RN; ++i)
-#pragma unroll
-      for (int m = 0; m < RM; ++m) acc[i][m] = mma_f8(fa[i], fb[m], acc[i][m]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  const int nch = a.Cin >> 7, nks = 9 * nch;
-  // prologue: stages 0 .. 2 and chunk 0's halo; stage 2 may stay in flight
-  issue_b(0);
-  issue_halo(0);
-  if (1 < nks) issue_b(1);
-  if (2 < nks) {
-    issue_b(2);
-    wait_vm<JB>();
-  } else {
-    wait_vm<0>();
-  }
-  __syncthreads();
-  v8i fa0[RN], fb0[RM], fa1[RN], fb1[RM];
-  load_frags(fa0, fb0, 0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();                                // buffer 0 is free for stage 3
-  // the loop body for (cur, nxt) frag sets; two copies alternate the register sets
-  int hprev = 0;                                  // halo pieces issued in the previous step
-  auto body = [&](int ks, v8i (&fac)[RN], v8i (&fbc)[RM], v8i (&fan)[RN], v8i (&fbn)[RM]) {
-    const int t = ks - (ks / 9) * 9, c = ks / 9;
-    int younger = 0;                              // DMAs issued after stage ks + 2
-    if (ks + 3 < nks) {
-      issue_b(ks + 3);
-      younger += JB;
-    }
-    int hnow = 0;
-    if (t == 0 && c + 1 < nch) {
-      issue_halo(c + 1);
-      hnow = nh;
-    }
-    if (ks + 1 < nks) load_frags(fan, fbn, ks + 1);
-    mfma_all(fac, fbc);
-    if (ks + 1 < nks) {
-      // stage ks + 2 (issued last step, BEFORE that step's halo) must land; younger: what this
-      // step issued and last step's halo (which so lands one step later, two after its issue)
-      wait_vm_dyn(younger + hnow + hprev);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    hprev = hnow;
-  };
-  for (int ks = 0; ks < nks; ks += 2) {
-    body(ks, fa0, fb0, fa1, fb1);
-    if (ks + 1 < nks) body(ks + 1, fa1, fb1, fa0, fb0);
-  }
-  wait_vm<0>();
-  const float dq = a.dq0[0] * a.dq1[0];
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int m = 0; m < RM; ++m) acc[i][m] *= dq;
-  __syncthreads();
-  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
-}
-
 // ----------------------------------------------------------------------------------------
 // fp8 (e4m3) weight gradient of the 3x3 convs (BASELINE config C5): the
 // sliding-row structure of conv3_halo_wgrad2 on v_mfma_scale_f32_16x16x128_f8f6f4, fed by the
@@ -5438,8 +5262,13 @@ int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, co
   a.ntn = cout / 128;
   const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
   const unsigned xb = (unsigned)((long)d->n * d->h * d->w * cin);
-  if (fp8p_enabled()) hipLaunchKernelGGL((conv3_halo_fp8p<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
-  else hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+  // (measured and not kept, r4: a 3-deep weight ring issued 3 steps ahead with the next tap's
+  // fragments read under this tap's MFMAs and the barrier after them, conv3_halo_fwd2's schedule:
+  // res fwd / dgrad at B = 64 188 / 172 -> 208 / 192 us.  Per step a wave reads 16 KB of
+  // fragments for 16 MFMAs of 32 cycles: 8 waves need 125 B/clk of the CU's 128 B/clk LDS
+  // bandwidth at the fp8 rate, so this tiling cannot pass ~0.5 of the fp8 peak however it
+  // is scheduled; the two waves of a SIMD already hide each other's reads.)
+  hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
   return fv_check_launch("conv2d_fp8");
 }
 
