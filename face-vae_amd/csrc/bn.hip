@@ -119,7 +119,7 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
 // Record folds (+ finalize): the per-channel sums of a BN layer arrive as `nrec` rows of partial
 // sums -- fp32 (sum, sum of squares) records of a conv epilogue / store pass ([r][2][C]), or the
 // fp64 per-block rows of a streaming pass ([b][3][C] with a count row, [b][2][C] backward sums).
-// ONE launch folds up to FOLDR records and finishes the layer: one channel per block of 1024
+// ONE launch folds up to FOLD2 records and finishes the layer: one channel per block of 1024
 // threads (fold1_kernel).  More records (the full-resolution layers' 16k conv records): chunk
 // partials [chunk][NV][C] from blocks that own 8 channels and read whole 32 / 64-B channel
 // octets of their rows (fold_part_kernel), into the caller's workspace, then fold1 over them
@@ -127,12 +127,13 @@ __global__ void finalize_kernel(const double* stats, int C, const float* gamma, 
 // (rows in thread order, a fixed xor tree per wave, waves in order, chunks in order):
 // bit-reproducible.
 // (measured and not kept, r4: octet blocks for every fold -- 1024-row folds 11-21 us against
-// fold1's 8-13; one launch with the chunks published by an agent-scope release + arrival
+// fold1's 8-13, 4096-row folds 10.6 + 3.9 us against 11.4; one launch with the chunks published by an agent-scope release + arrival
 // counter, the last block adding them -- the release writes back the XCD's L2 per block: +6..8
 // us per fold, step 12.50 -> 12.86 ms.)
 // ---------------------------------------------------------------------------------------------
 constexpr int FOLDB = 256, FOLDR = 1024;    // threads per octet fold block, records per fold block
 constexpr int FOLDT = 1024;                 // threads per one-channel fold block
+constexpr int FOLD2 = 8192;                 // records above which the fold takes two levels
 enum { FOLD_STATS = 0, FOLD_FWD = 1, FOLD_BWD = 2 };
 struct FoldArgs {
   const void* src;
@@ -208,7 +209,7 @@ __global__ void __launch_bounds__(FOLDB) fold_part_kernel(FoldArgs a, double* pa
   }
 }
 
-// <= FOLDR records (and level 2): one channel per block of 1024 threads, one row each
+// <= FOLD2 records (and level 2): one channel per block of 1024 threads, rows t, t + 1024, ...
 template <typename T, int NV, int MODE>
 __global__ void __launch_bounds__(FOLDT) fold1_kernel(FoldArgs a) {
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -264,13 +265,13 @@ __global__ void __launch_bounds__(FOLDT) fold1_kernel(FoldArgs a) {
   }
 }
 
-// scratch: room for ceil(nrec / FOLDR) x NV x C doubles when nrec > FOLDR (the records then
+// scratch: room for ceil(nrec / FOLDR) x NV x C doubles when nrec > FOLD2 (the records then
 // fold in two launches: chunk partials, then the partial rows)
 template <typename T, int NV, int MODE>
 int launch_fold(const FoldArgs& a, hipStream_t s, const char* what, double* scratch = nullptr) {
   FV_REQUIRE(a.C % 8 == 0 && a.nrec > 0, "BN fold: channels must be a multiple of 8 (%d)", a.C);
   const int nch = (a.nrec + FOLDR - 1) / FOLDR;
-  if (nch == 1) {
+  if (a.nrec <= FOLD2) {
     hipLaunchKernelGGL((fold1_kernel<T, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, a);
     return fv_check_launch(what);
   }
