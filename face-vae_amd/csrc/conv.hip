@@ -3393,17 +3393,9 @@ bool use_v2(const fv_conv_desc* d) {
 // weight gradient's PRO variant): the NAC ResBlock convs (256-channel co tiles, <= 256 input
 // channels).  Measured SLOWER than materialising act(BN(x)) with the separate pass (r4, one box,
 // B=32: res fwd 147-155 -> 170-172 us, wgrad 157-162 -> 169 us against the 21.5 us act_fwd pass
-// each saves; step 12.48 -> 12.70 ms), so it is off by default; FV_NAC_STAGED=1 turns it on.
-static int g_nac_staged = -1;
-bool nac_staged_enabled() {
-  if (g_nac_staged < 0) {
-    const char* e = getenv("FV_NAC_STAGED");
-    g_nac_staged = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_nac_staged != 0;
-}
+// each saves; step 12.48 -> 12.70 ms), so the host side does not use it by default
+// (ops._NAC_STAGED, FV_NAC_STAGED=1); this reports whether a descriptor is supported.
 static bool pro3_ok(const fv_conv_desc* d) {
-  if (!nac_staged_enabled()) return false;
   if (d->dtype != FV_BF16 || d->ksize != 3 || d->upsample || !d->pro_act) return false;
   if (d->out_nchw_f32 || d->epi_sigmoid || d->ldy % 8 || d->cout % 256) return false;
   if (d->cin % 64 || d->cin > 256 || d->cin_valid != d->cin || d->w % 64 || d->h % 4) return false;

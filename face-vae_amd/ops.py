@@ -15,6 +15,7 @@ Reference semantics restated here (file:line in Luh1124/face-vae):
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from typing import Optional
 
@@ -805,21 +806,26 @@ def _bnred_of(src):
     return None if src is None or src["nuse"] != 1 else (src["bn"], src["r"], src["y"], src["slope"])
 
 
+# BN-apply + ReLU in the NAC convs' operand staging (DESIGN.md §4 "Round 4, measured": built,
+# slower than the separate act_fwd pass on MI355X, so off unless FV_NAC_STAGED=1; tests flip it)
+_NAC_STAGED = os.environ.get("FV_NAC_STAGED", "0") == "1"
+
+
 def nac_staged(dtype, N, H, W, C, k):
     """True when the NAC convs of a ResBlock2D of this shape take the BN-apply + ReLU in their
     operand staging (fv_conv2d_pro_staged: bf16, 256-channel halo kernels): act(BN(x)) is then
-    never written to HBM."""
-    if dtype != torch.bfloat16 or k != 3:
+    never written to HBM.  Only with _NAC_STAGED."""
+    if not _NAC_STAGED or dtype != torch.bfloat16 or k != 3:
         return False
     return bool(query("fv_conv2d_pro_staged", ctypes.byref(desc(dtype, N, H, W, C, C, C, C, 3, pro=1))))
 
 
 class ResBlockFn(torch.autograd.Function):
-    """ResBlock2D: x + NAC(NAC(x)), NAC = BN -> ReLU -> conv3x3 (modules.py:116-130).
-    bf16 on the 256-channel halo kernels: each conv stages its PRE-BN input and applies BN +
-    ReLU in LDS (fv_conv2d_pro_staged), forward and weight gradient alike, so act(BN(.)) is never
-    materialised.  Otherwise (fp32 parity mode, fp8, other shapes) the BN-apply+ReLU output of
-    each NAC is materialised once (one HBM pass).  The residual add runs in conv2's epilogue."""
+    """ResBlock2D: x + NAC(NAC(x)), NAC = BN -> ReLU -> conv3x3 (modules.py:116-130).  The
+    BN-apply+ReLU output of each NAC is materialised once (one HBM pass, written with its e4m3
+    copy in fp8 mode); with _NAC_STAGED (bf16, 256-channel halo kernels) each conv instead stages
+    its PRE-BN input and applies BN + ReLU in LDS (fv_conv2d_pro_staged), forward and weight
+    gradient alike -- measured slower, off by default.  The residual add runs in conv2's epilogue."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, blk):
