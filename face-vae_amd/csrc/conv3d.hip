@@ -14,8 +14,10 @@
 //     stages ONE new input depth slice (6 rows x 64 voxels x 64 B, 24 KB) by LDS-DMA into a
 //     4-slot ring while the previous three are consumed, so an input voxel is fetched about
 //     1.5x (row halo) instead of 27x.  All 27 x 32 x 32 weights live in registers (54 MFMA
-//     A fragments, one wave per SIMD), so the only LDS reads are the activation fragments:
-//     4 ds_read_b128 per 8 v_mfma_f32_16x16x32_bf16.  Epilogue: bias, optional residual,
+//     A fragments, one wave per SIMD), so the only LDS reads are the activation fragments, and
+//     only those of the centre column tap: 4 ds_read_b128 per 24 v_mfma_f32_16x16x32_bf16, the
+//     kw = 0 / 2 fragments made by DPP lane shifts (r2-r3 read all three: 4 per 8 MFMAs, which
+//     needs the whole 128 B/clk of LDS bandwidth at one wave per SIMD).  Epilogue: bias, optional residual,
 //     BN (sum, sum of squares) partials per wave, bf16 store.
 //   conv3d_c32_wgrad -- dW[co][tap][ci] = sum_v dy[v][co] x[v + off(tap)][ci] (+ db), K =
 //     voxels.  A block of 8 waves owns 4 rows of one or more images and slides along depth
@@ -57,6 +59,33 @@ __device__ __forceinline__ bf16x8 tfrag32(const char* base, int r0, int cbase, i
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// B fragments of the kw = 0 / 2 taps from the kw = 1 (centre) fragments of the same row in
+// registers: a fragment is 16 voxels (lanes li of each 16-lane row g = channel group), so the
+// column shift is a DPP move within the row (row_shr:1 / row_shl:1), the voxel crossing into the
+// neighbouring fragment comes from it (row_shl:15 / row_shr:15), and the out-of-row voxels -1 and
+// 64 -- the zero padding -- are what bound_ctrl writes.  Bit-identical to the LDS reads.
+typedef int v4i3_t __attribute__((ext_vector_type(4)));
+template <int CTRL>
+__device__ __forceinline__ v4i3_t dpp4x(const bf16x8& x) {
+  const v4i3_t a = __builtin_bit_cast(v4i3_t, x);
+  v4i3_t o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = __builtin_amdgcn_update_dpp(0, a[k], CTRL, 0xf, 0xf, true);
+  return o;
+}
+// voxel 16 j + li - 1 (kw = 0)
+__device__ __forceinline__ bf16x8 shift_m1(const bf16x8& cur, const bf16x8* prev) {
+  v4i3_t o = dpp4x<0x111>(cur);                       // row_shr:1
+  if (prev) o |= dpp4x<0x10f>(*prev);                 // row_shl:15: lane 0 <- lane 15
+  return __builtin_bit_cast(bf16x8, o);
+}
+// voxel 16 j + li + 1 (kw = 2)
+__device__ __forceinline__ bf16x8 shift_p1(const bf16x8& cur, const bf16x8* next) {
+  v4i3_t o = dpp4x<0x101>(cur);                       // row_shl:1
+  if (next) o |= dpp4x<0x11f>(*next);                 // row_shr:15: lane 15 <- lane 0
+  return __builtin_bit_cast(bf16x8, o);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -131,7 +160,6 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
   issue(d0 - 1);
   issue(d0);
   issue(d0 + 1);
-  const bf16x8 zero8 = {};
   for (int d = d0; d < d1; ++d) {
     vm_wait0();
     __syncthreads();
@@ -147,19 +175,21 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const char* rb = sb + (wave + kh) * C3_ROWB;
+        // the row's centre fragments (kw = 1) from LDS; kw = 0 / 2 by lane shifts (shift_m1 / p1)
+        bf16x8 cx[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int v = 16 * j + li;
+          cx[j] = *reinterpret_cast<const bf16x8*>(rb + v * 64 + ((g ^ cswz(v)) << 4));
+        }
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const int t = kd * 9 + kh * 3 + kw;
           bf16x8 bx[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            int v = 16 * j + li + kw - 1;
-            const bool edge = (kw == 0 && j == 0) || (kw == 2 && j == 3);
-            const bool ok = !edge || (unsigned)v < 64u;
-            v = v < 0 ? 0 : (v > 63 ? 63 : v);
-            const bf16x8 val = *reinterpret_cast<const bf16x8*>(rb + v * 64 + ((g ^ cswz(v)) << 4));
-            bx[j] = ok ? val : zero8;
-          }
+          for (int j = 0; j < 4; ++j)
+            bx[j] = kw == 1 ? cx[j] : kw == 0 ? shift_m1(cx[j], j > 0 ? &cx[j - 1] : nullptr)
+                                              : shift_p1(cx[j], j < 3 ? &cx[j + 1] : nullptr);
 #pragma unroll
           for (int i = 0; i < 2; ++i)
 #pragma unroll

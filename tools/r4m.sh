@@ -11,3 +11,8 @@ cp gpurun_out/pmc.json gpurun_out/pmc_r4m.json
 CB_ARGS="--layers res --only fwd,wgrad --iters 5" bash tools/gpu.sh convpmc || exit 1
 cp gpurun_out/convpmc.txt gpurun_out/convpmc_r4m_res.txt
 TAG=r4m bash tools/gpu.sh prof
+TESTS="tests/test_afe3d_gpu.py tests/test_warp_gpu.py" bash tools/gpu.sh test || exit 1
+for v in "" "$BASE"; do FV_LIB_PATH=$v timeout -k 10 200 python tools/conv3dbench.py >> gpurun_out/conv3dbench_r4m.log 2>&1 || exit 1; done
+for v in "" "$BASE"; do FV_LIB_PATH=$v timeout -k 10 200 python tools/conv3dbench.py >> gpurun_out/conv3dbench_r4m.log 2>&1 || exit 1; done
+grep -v amdgpu.ids gpurun_out/conv3dbench_r4m.log
+timeout -k 10 300 python tools/fbench.py --batch 8 --steps 10 --warmup 3 > gpurun_out/fbench_r4m.log 2>&1; tail -1 gpurun_out/fbench_r4m.log
