@@ -5256,10 +5256,9 @@ int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, co
   const unsigned xb = (unsigned)((long)d->n * d->h * d->w * cin);
   // (measured and not kept, r4: a 3-deep weight ring issued 3 steps ahead with the next tap's
   // fragments read under this tap's MFMAs and the barrier after them, conv3_halo_fwd2's schedule:
-  // res fwd / dgrad at B = 64 188 / 172 -> 208 / 192 us.  Per step a wave reads 16 KB of
-  // fragments for 16 MFMAs of 32 cycles: 8 waves need 125 B/clk of the CU's 128 B/clk LDS
-  // bandwidth at the fp8 rate, so this tiling cannot pass ~0.5 of the fp8 peak however it
-  // is scheduled; the two waves of a SIMD already hide each other's reads.)
+  // res fwd / dgrad at B = 64 188 / 172 -> 208 / 192 us: the two waves of a SIMD already hide
+  // each other's fragment reads (16 KB per 16 MFMAs of 32 cycles, half the CU's 256 B/clk of
+  // LDS at the fp8 peak).)
   hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
   return fv_check_launch("conv2d_fp8");
 }

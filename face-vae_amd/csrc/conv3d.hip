@@ -16,8 +16,9 @@
 //     1.5x (row halo) instead of 27x.  All 27 x 32 x 32 weights live in registers (54 MFMA
 //     A fragments, one wave per SIMD), so the only LDS reads are the activation fragments, and
 //     only those of the centre column tap: 4 ds_read_b128 per 24 v_mfma_f32_16x16x32_bf16, the
-//     kw = 0 / 2 fragments made by DPP lane shifts (r2-r3 read all three: 4 per 8 MFMAs, which
-//     needs the whole 128 B/clk of LDS bandwidth at one wave per SIMD).  Epilogue: bias, optional residual,
+//     kw = 0 / 2 fragments made by DPP lane shifts (r2-r3 read all three: 4 per 8 MFMAs, half
+//     the CU's LDS bandwidth at the MFMA peak, each read a latency the single wave per SIMD
+//     must cover).  Epilogue: bias, optional residual,
 //     BN (sum, sum of squares) partials per wave, bf16 store.
 //   conv3d_c32_wgrad -- dW[co][tap][ci] = sum_v dy[v][co] x[v + off(tap)][ci] (+ db), K =
 //     voxels.  A block of 8 waves owns 4 rows of one or more images and slides along depth
