@@ -114,7 +114,9 @@ int fv_conv2d_dgrad_lowres(const fv_conv_desc* d);
  * whose pre-BN input is staged and transformed in LDS, so act(BN(x)) is never materialised
  * (forward: fv_conv2d_fwd / fv_conv2d_fwd_pro_sr; weight gradient: fv_conv2d_bwd_weight with
  * the same scale / shift; the data gradient is w.r.t. act(BN(x)) as before).  0: other
- * descriptors take the prologue on the generic register-staged kernels (slow). */
+ * descriptors take the prologue on the generic register-staged kernels (slow).  Measured on
+ * MI355X (DESIGN.md §4 "Round 4, measured"): slower than materialising act(BN(x)) with
+ * fv_bn_act_fwd, so the host side only uses it on request. */
 int fv_conv2d_pro_staged(const fv_conv_desc* d);
 
 /* weight gradient w.r.t. the effective (post-SN) weight, split over pixels:
