@@ -97,6 +97,16 @@ constexpr int C3_ROWB = 64 * 64;                  // one image row: 64 voxels x 
 constexpr int C3_SLOT = (C3_TH + 2) * C3_ROWB;    // 24 KB input depth slice (row halo)
 constexpr int C3_NS = 4;                          // ring slots
 
+// conv3d_c32_fwd<1> (8 waves, co halves) vs <2> (4 waves); FV_C3SPLIT=0 for A/B
+static int g_c3split = -1;
+static bool c3_split() {
+  if (g_c3split < 0) {
+    const char* e = getenv("FV_C3SPLIT");
+    g_c3split = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_c3split != 0;
+}
+
 struct C3Args {
   const bf16* x;
   const bf16* w;       // [27][32 out][32 in] bf16
@@ -109,10 +119,17 @@ struct C3Args {
   unsigned xbytes;
 };
 
-__global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
+// NI: 16-channel output tiles per wave.  NI = 2: 4 waves (one per SIMD, 358 registers, all 32
+// output channels); NI = 1: 8 waves, the two co halves of a row on two waves (two per SIMD,
+// the weights of 16 co in registers), the activation fragments read by both.
+template <int NI>
+__global__ void __launch_bounds__(64 * 4 * (2 / NI), 1) conv3d_c32_fwd(C3Args a) {
+  constexpr int NWV = 4 * (2 / NI);
   __shared__ __attribute__((aligned(1024))) char smem[C3_NS * C3_SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row = wave & 3, coh = wave >> 2;          // output row of the block, co half (NI = 1)
+  const int cb0 = coh * NI * 16;                      // the wave's first output channel
   const int nht = a.H / C3_TH;
   int b = blockIdx.x;
   const int dc = b % a.ndc;
@@ -129,8 +146,8 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
   auto issue = [&](int di) {
     const unsigned lb = sbase + ((di + 1) & 3) * C3_SLOT;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int q = wave + 4 * j;
+    for (int j = 0; j < 24 / NWV; ++j) {
+      const int q = wave + NWV * j;
       const int r = q >> 2, vv = 16 * (q & 3) + (lane >> 2);
       const int c = (lane & 3) ^ cswz(vv);
       const int h = h0 - 1 + r;
@@ -141,20 +158,20 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
   };
 
   // weights: A fragments wf[tap][i] (rows co = 16 i + li, k = ci 8 g .. 8 g + 7)
-  bf16x8 wf[27][2];
+  bf16x8 wf[27][NI];
 #pragma unroll
   for (int t = 0; t < 27; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      wf[t][i] = *reinterpret_cast<const bf16x8*>(a.w + ((t * 32 + 16 * i + li) * 32 + 8 * g));
-  float bv[2][4];
+    for (int i = 0; i < NI; ++i)
+      wf[t][i] = *reinterpret_cast<const bf16x8*>(a.w + ((t * 32 + cb0 + 16 * i + li) * 32 + 8 * g));
+  float bv[NI][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) bv[i][k] = a.bias ? a.bias[16 * i + 4 * g + k] : 0.f;
-  float ss[2][4], sq[2][4];
+    for (int k = 0; k < 4; ++k) bv[i][k] = a.bias ? a.bias[cb0 + 16 * i + 4 * g + k] : 0.f;
+  float ss[NI][4], sq[NI][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) ss[i][k] = sq[i][k] = 0.f;
 
@@ -165,9 +182,9 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
     vm_wait0();
     __syncthreads();
     if (d + 2 <= d1) issue(d + 2);
-    f32x4 acc[2][4];
+    f32x4 acc[NI][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -175,7 +192,7 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
       const char* sb = smem + ((d + kd) & 3) * C3_SLOT;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-        const char* rb = sb + (wave + kh) * C3_ROWB;
+        const char* rb = sb + (row + kh) * C3_ROWB;
         // the row's centre fragments (kw = 1) from LDS; kw = 0 / 2 by lane shifts (shift_m1 / p1)
         bf16x8 cx[4];
 #pragma unroll
@@ -192,20 +209,20 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
             bx[j] = kw == 1 ? cx[j] : kw == 0 ? shift_m1(cx[j], j > 0 ? &cx[j - 1] : nullptr)
                                               : shift_p1(cx[j], j < 3 ? &cx[j + 1] : nullptr);
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][i], bx[j], acc[i][j], 0, 0, 0);
         }
       }
     }
-    // epilogue: lane holds co = 16 i + 4 g + k of voxel 16 j + li in row h0 + wave
-    const long rowv = ((long)(n * a.D + d) * a.H + h0 + wave) << 6;
+    // epilogue: lane holds co = cb0 + 16 i + 4 g + k of voxel 16 j + li in row h0 + row
+    const long rowv = ((long)(n * a.D + d) * a.H + h0 + row) << 6;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NI; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const long e = ((rowv + 16 * j + li) << 5) + 16 * i + 4 * g;
+        const long e = ((rowv + 16 * j + li) << 5) + cb0 + 16 * i + 4 * g;
         float o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[k] = acc[i][j][k] + bv[i][k];
@@ -229,15 +246,15 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd(C3Args a) {
     }
   }
   if (a.stats) {
-    const long rec = (long)blockIdx.x * C3_TH + wave;
+    const long rec = (long)blockIdx.x * C3_TH + row;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float S = row16_sum(ss[i][k]), Q = row16_sum(sq[i][k]);
         if (li == 0) {
-          a.stats[(rec * 2) * 32 + 16 * i + 4 * g + k] = S;
-          a.stats[(rec * 2 + 1) * 32 + 16 * i + 4 * g + k] = Q;
+          a.stats[(rec * 2) * 32 + cb0 + 16 * i + 4 * g + k] = S;
+          a.stats[(rec * 2 + 1) * 32 + cb0 + 16 * i + 4 * g + k] = Q;
         }
       }
   }
@@ -614,7 +631,10 @@ static int conv3d_run(const fv_conv3d_desc* d, int cin, int cout, const void* x,
     a.dchunk = d->d / a.ndc;
     a.xbytes = (unsigned)((long)d->n * d->d * d->h * 64 * 32 * 2);
     const int nblk = d->n * (d->h / C3_TH) * a.ndc;
-    hipLaunchKernelGGL(conv3d_c32_fwd, dim3(nblk), dim3(256), 0, s, a);
+    if (c3_split())
+      hipLaunchKernelGGL((conv3d_c32_fwd<1>), dim3(nblk), dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv3d_c32_fwd<2>), dim3(nblk), dim3(256), 0, s, a);
     return fv_check_launch("conv3d_c32_fwd");
   }
   FV_REQUIRE(!stats, "conv3d: BN partials only on the fast path (query fv_conv3d_stats_blocks)");
