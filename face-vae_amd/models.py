@@ -12,6 +12,24 @@ from . import ops3d, warp
 from .modules import Conv2d, ConvBlock2D, DownBlock2D, ResBlock2D, ResBlock3D, UpBlock2D, _Block
 
 
+def _batched_weight_prep(model, device):
+    """The per-step weight work of every conv under `model` in a few launches: one batched
+    power iteration for the spectral-normed convs (ops.SNBatch, 4 launches for all of them) and
+    one re-layout launch for the generic weight layouts (ops.WPrepBatch).  Run by the top-level
+    forward of AFE / Generator / FaceVAE (sub-module calls go through forward_2d)."""
+    from .modules import _Conv
+    sb = model.__dict__.get("_snb")
+    if sb is None:
+        sb = ops.SNBatch([c for c in model.modules() if isinstance(c, _Conv) and c.sn])
+        object.__setattr__(model, "_snb", sb)
+    wb = model.__dict__.get("_wpb")
+    if wb is None:
+        wb = ops.WPrepBatch([c for c in model.modules() if isinstance(c, _Conv)])
+        object.__setattr__(model, "_wpb", wb)
+    sb.run(model.training)
+    wb.run(device)
+
+
 class AFE(_Block):
     """Appearance-feature extractor (models.py:922-945): in_conv 7x7 CNA, DownBlock2D chain,
     1x1 mid_conv (the 2-D trunk = the FaceVAE encoder), then x.view(N, C, D, H, W) and n_res
@@ -32,9 +50,10 @@ class AFE(_Block):
         return self.mid_conv(self.down(self.in_conv(x)))
 
     def forward(self, x):
-        h = self.forward_2d(x)
         if not x.is_cuda:
             raise RuntimeError("facevae_amd ops run on the GPU only (HIP); got a CPU tensor")
+        _batched_weight_prep(self, x.device)
+        h = self.forward_2d(x)
         fs = ops3d.depth_split(h, self.C, self.D, self.compute_dtype())
         return self.res(fs)
 
@@ -67,6 +86,8 @@ class Generator(_Block):
 
     def forward(self, fs, deformation=None, occlusion=None):
         mode = self.compute_dtype()
+        if fs.is_cuda:
+            _batched_weight_prep(self, fs.device)
         if fs.dim() == 5:
             if deformation is not None:
                 fs = warp.grid_sample_3d(fs, deformation, ops.storage(mode))
@@ -90,27 +111,10 @@ class FaceVAE(_Block):
         self.afe = AFE(False, list(cfg.down_seq), 0, C=2 * cfg.latent, D=1)
         self.generator = Generator(True, cfg.n_res, list(cfg.up_seq), D=1, C=cfg.latent)
 
-    def _sn_batch(self):
-        sb = getattr(self, "_snb", None)
-        if sb is None:
-            from .modules import _Conv
-            convs = [c for c in self.modules() if isinstance(c, _Conv) and c.sn]
-            sb = ops.SNBatch(convs)
-            object.__setattr__(self, "_snb", sb)
-        return sb
-
-    def _wprep_batch(self):
-        wb = getattr(self, "_wpb", None)
-        if wb is None:
-            from .modules import _Conv
-            wb = ops.WPrepBatch([c for c in self.modules() if isinstance(c, _Conv)])
-            object.__setattr__(self, "_wpb", wb)
-        return wb
-
     def forward(self, x, eps):
         if x.is_cuda:
-            self._sn_batch().run(self.training)   # all 15 power iterations in 4 launches
-            self._wprep_batch().run(x.device)       # the generic weight layouts in one launch
+            # all 15 power iterations in 4 launches, the generic weight layouts in one
+            _batched_weight_prep(self, x.device)
         h = self.afe.forward_2d(x)
         mu, logstd, z = ops.reparameterise(h, eps, self.compute_dtype())
         y = self.generator.forward_2d(z)
