@@ -97,16 +97,6 @@ constexpr int C3_ROWB = 64 * 64;                  // one image row: 64 voxels x 
 constexpr int C3_SLOT = (C3_TH + 2) * C3_ROWB;    // 24 KB input depth slice (row halo)
 constexpr int C3_NS = 4;                          // ring slots
 
-// conv3d_c32_fwd<1> (8 waves, co halves) vs <2> (4 waves); FV_C3SPLIT=0 for A/B
-static int g_c3split = -1;
-static bool c3_split() {
-  if (g_c3split < 0) {
-    const char* e = getenv("FV_C3SPLIT");
-    g_c3split = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_c3split != 0;
-}
-
 struct C3Args {
   const bf16* x;
   const bf16* w;       // [27][32 out][32 in] bf16
@@ -119,9 +109,10 @@ struct C3Args {
   unsigned xbytes;
 };
 
-// NI: 16-channel output tiles per wave.  NI = 2: 4 waves (one per SIMD, 358 registers, all 32
-// output channels); NI = 1: 8 waves, the two co halves of a row on two waves (two per SIMD,
-// the weights of 16 co in registers), the activation fragments read by both.
+// NI: 16-channel output tiles per wave.  NI = 2 (used): 4 waves, one per SIMD, 358 registers,
+// all 32 output channels.  (NI = 1 -- 8 waves, the two co halves of a row on two waves, two per
+// SIMD, the activation fragments read by both -- measured slower, r4: forward 142-148 vs
+// 158-165 us at [32, 32, 16, 64, 64].)
 template <int NI>
 __global__ void __launch_bounds__(64 * 4 * (2 / NI), 1) conv3d_c32_fwd(C3Args a) {
   constexpr int NWV = 4 * (2 / NI);
@@ -631,10 +622,7 @@ static int conv3d_run(const fv_conv3d_desc* d, int cin, int cout, const void* x,
     a.dchunk = d->d / a.ndc;
     a.xbytes = (unsigned)((long)d->n * d->d * d->h * 64 * 32 * 2);
     const int nblk = d->n * (d->h / C3_TH) * a.ndc;
-    if (c3_split())
-      hipLaunchKernelGGL((conv3d_c32_fwd<1>), dim3(nblk), dim3(512), 0, s, a);
-    else
-      hipLaunchKernelGGL((conv3d_c32_fwd<2>), dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((conv3d_c32_fwd<2>), dim3(nblk), dim3(256), 0, s, a);
     return fv_check_launch("conv3d_c32_fwd");
   }
   FV_REQUIRE(!stats, "conv3d: BN partials only on the fast path (query fv_conv3d_stats_blocks)");

@@ -26,12 +26,16 @@ import re
 # on the same grid: a step dispatches it 13 times in the forward (Generator.in_conv + 12 res
 # convs), then 13 times in the backward, so in dispatch order launch i is a forward launch when
 # (i // FWD_PER_STEP) is even.
+# The weight gradient runs on the sliding-row conv3_halo_wgrad2 (256 blocks of 512), 15
+# dispatches per step: the 13 256->256 ones first (12 res + Generator.in_conv, backward order),
+# then AFE.down2's two.
 DOMS = {
-    "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2>"), 512 * 512),
-    "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2>"), 512 * 512),
-    "wgrad": (re.compile(r"conv_wgrad_v2<3, 256, 256, 2, 4, 64, 2, false, false>"), 252 * 512),
+    "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false)?>"), 512 * 512),
+    "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false)?>"), 512 * 512),
+    "wgrad": (re.compile(r"conv3_halo_wgrad2<4(, false)?>"), 256 * 512),
 }
 FWD_PER_STEP = 13
+WGRAD_PER_STEP, WGRAD_RES = 15, 13
 RES_FLOP = 2.0 * 32 * 64 * 64 * 256 * 256 * 9     # one res-conv launch, B=32 (154.6 GFLOP)
 SIMDS = 1024
 XCDS = 8
@@ -48,6 +52,8 @@ def dom_of(name, grid, k):
     fams = [f for f, (pat, g) in DOMS.items() if pat.search(name) and grid == g]
     if "fwd" in fams and "dgrad" in fams:
         fams = ["fwd" if (k // FWD_PER_STEP) % 2 == 0 else "dgrad"]
+    if fams == ["wgrad"] and k % WGRAD_PER_STEP >= WGRAD_RES:
+        fams = []
     return fams
 
 
