@@ -1067,11 +1067,7 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
 // runs MFMAs), published by the following barrier, before its first fragment read (the first
 // read needs it published by barrier floor(9c / 2) - 1 (c even) / (9c - 3) / 2 (c odd), the
 // later half publishes at barrier 9c / 2 - 2 / (9c - 5) / 2).
-//
-// RSW: the weight stages after the first NSB travel through registers (buffer_load_dwordx4 one
-// step ahead, ds_write_b128 after the next barrier) instead of LDS-DMA, whose issue costs
-// 100-185 cycles per 1-KB piece inside a phase that also reads fragments (MI355X_MICROARCH.md).
-template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, bool RSW = false>
+template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
@@ -1169,27 +1165,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, (unsigned)u * ustep + jb * wstep);
     }
   };
-  // RSW: stage j's pieces into registers / from registers into LDS buffer `buf`
-  typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-  u4v wreg[RSW ? 2 : 1][RSW ? JB : 1];
-  auto load_b = [&](int j) {
-    if constexpr (RSW) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int jb = 0; jb < JB; ++jb)
-          wreg[h][jb] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wbase, (int)((2 * j + h) * ustep + jb * wstep), 0);
-    }
-  };
-  auto write_b = [&](int buf) {
-    if constexpr (RSW) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int jb = 0; jb < JB; ++jb)
-          *reinterpret_cast<u4v*>(smem + buf * STG + h * BST + (wave + jb * NW) * 1024 + lane * 16) = wreg[h][jb];
-    }
-  };
   // one weight DMA piece q (0 .. 2 JB - 1) of stage j: tap half q / JB, row piece q % JB
   auto issue_halo = [&](int c) {
     const unsigned Hs = sbase + WOFF + (c & 1) * HALO;
@@ -1248,7 +1223,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     issue_b(NSB - 1, NSB - 1);
     pend = bcnt(NSB - 1);
   }
-  if (RSW && NSB < nsteps) load_b(NSB);
   load_frags(fa0, fb0, 0, 0);
   int hn = 2, hstep = (9 * 2 - 10) / 2;
   int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
@@ -1277,14 +1251,9 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       }
       pend = 0;
       if (j + NSB < nsteps) {
-        if constexpr (RSW) {
-          write_b(bj);                     // stage j + NSB, loaded last step (waited above)
-        } else {
-          issue_b(j + NSB, bj);
-          pend = bcnt(j + NSB);
-        }
+        issue_b(j + NSB, bj);
+        pend = bcnt(j + NSB);
       }
-      if (RSW && j + NSB + 1 < nsteps) load_b(j + NSB + 1);
       load_frags(fa0, fb0, 2 * j + 2, bn1);
       FV_DIAG_ISSUE_END();
     }
@@ -3426,15 +3395,6 @@ bool use_v2(const fv_conv_desc* d) {
 // B=32: res fwd 147-155 -> 170-172 us, wgrad 157-162 -> 169 us against the 21.5 us act_fwd pass
 // each saves; step 12.48 -> 12.70 ms), so the host side does not use it by default
 // (ops._NAC_STAGED, FV_NAC_STAGED=1); this reports whether a descriptor is supported.
-// conv3_halo_fwd3 RSW (register-staged weight stages); FV_RSW=0 for A/B
-static int g_rsw = -1;
-static bool rsw_enabled() {
-  if (g_rsw < 0) {
-    const char* e = getenv("FV_RSW");
-    g_rsw = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_rsw != 0;
-}
 static bool pro3_ok(const fv_conv_desc* d) {
   if (d->dtype != FV_BF16 || d->ksize != 3 || d->upsample || !d->pro_act) return false;
   if (d->out_nchw_f32 || d->epi_sigmoid || d->ldy % 8 || d->cout % 256) return false;
@@ -4230,14 +4190,15 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // fragments of the column-shifted taps (s = 1, 2) made from the previous tap's in registers
     // by DPP lane shifts (row_shl:1 | row_shr:15 of the next fragment, the row-end pixel read
     // as a broadcast: 2 instead of 8 B reads per tap): res fwd / dgrad 132-135 / 125-128 ->
-    // 136-138 / 131-132 us, step +0.14 ms.)
+    // 136-138 / 131-132 us, step +0.14 ms.  The weight stages after the first two through
+    // registers (buffer_load_dwordx4 a step ahead, ds_write_b128 after the next barrier) instead
+    // of LDS-DMA: res fwd / dgrad 147 / 136 -> 150.5 / 141 us, Generator.in_conv 147-152 ->
+    // 160-162 us, step +0.17 ms.)
     if (d->pro_act) {
       FV_REQUIRE(bn == 256 && psc && psh, "staged BN prologue: bad arguments");
       hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn >= 128 && a.Cin % 64 == 0) {
-      if (bn == 256 && rsw_enabled())
-        hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
-      else if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+      if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
       else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 256) {
       hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
