@@ -806,9 +806,6 @@ def _bnred_of(src):
     return None if src is None or src["nuse"] != 1 else (src["bn"], src["r"], src["y"], src["slope"])
 
 
-# ResBlock2D backward: the BN-backward sums reduced in the data gradients' store pass (A/B knob)
-_RES_SR = os.environ.get("FV_RES_SR", "0") == "1"
-
 # BN-apply + ReLU in the NAC convs' operand staging (DESIGN.md §4 "Round 4, measured": built,
 # slower than the separate act_fwd pass on MI355X, so off unless FV_NAC_STAGED=1; tests flip it)
 _NAC_STAGED = os.environ.get("FV_NAC_STAGED", "0") == "1"
@@ -950,18 +947,15 @@ class ResBlockFn(torch.autograd.Function):
             t = pend[0]()
             if t is not None and t is dout and dout._version == pend[1]:
                 dy8 = pend[2]
-        # _RES_SR: each data gradient also reduces the BN-backward sums of the BN in front of it
-        # in its store pass (fv_conv2d_bwd_data_sr), replacing the act_bwd_reduce pass
-        sr = _RES_SR and not cs2.fp8
-        da2, dw2, db2, recs2 = conv_backward(cs2, a2, dout, C, dy8=dy8, want_recs=True,
-                                             bnred=(blk.bn2, r2, t1, 0.0) if sr else None)
+        # (the BN-backward sums reduced in the data gradients' store pass instead of the reduce
+        # pass: step 12.46 -> 12.67 ms in r4, as in r2 -- DESIGN.md §4)
+        da2, dw2, db2 = conv_backward(cs2, a2, dout, C, dy8=dy8)
         site1 = fp8_site(cs1.conv, "dy", xb.device) if cs1.fp8 else None
-        dt1, dg2, dbe2, *q = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, q8=site1, recs=recs2)
-        da1, dw1, db1, recs1 = conv_backward(cs1, a1, dt1, C, dy8=q[0] if q else None, want_recs=True,
-                                             bnred=(blk.bn1, r1, xb, 0.0) if sr else None)
+        dt1, dg2, dbe2, *q = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, q8=site1)
+        da1, dw1, db1 = conv_backward(cs1, a1, dt1, C, dy8=q[0] if q else None)
         prev = ctx.q8_prev
         dxb, dg1, dbe1, *q = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout,
-                                             q8=prev[1] if prev is not None else None, recs=recs1)
+                                             q8=prev[1] if prev is not None else None)
         if prev is not None and q and q[0] is not None:
             prev[0].__dict__["_fv_fp8_pending"] = (weakref.ref(dxb), dxb._version, q[0])
         dx = from_nhwc(dxb, x)
