@@ -3410,10 +3410,11 @@ int halo3_bn(const fv_conv_desc* d) {
   if ((long)d->n * d->h * d->w * d->ldy * 2 >= (1L << 31)) return 0;
   // co % 256: the pipelined pair-of-taps kernel (3 % over conv_fwd_v2's 256 x 256 tile on
   // the res convs) -- unless its 256-pixel x 256-co tiles leave CUs idle (fewer tiles than the
-  // 256 CUs, e.g. the 64x64 convs at B <= 8: the SURVEY 8(f) path's Generator), where the 128-co
-  // tiles double the grid
+  // 256 CUs, e.g. the 64x64 latent convs at B <= 8: the SURVEY 8(f) path's Generator), where the
+  // 128-co tiles double the grid.  Only for >= 256 input channels (the latent-resolution
+  // convs), so AFE.down2 (128 -> 256) keeps one kernel at every batch size.
   if (d->cout % 256 == 0)
-    return (long)d->n * (d->h / 4) * (d->w / 64) * (d->cout / 256) >= 256 ? 256 : 128;
+    return d->cin < 256 || (long)d->n * (d->h / 4) * (d->w / 64) * (d->cout / 256) >= 256 ? 256 : 128;
   // AFE.down1's forward (64 -> 128 channels, K = 576): conv_fwd_v2's 128 x 256 tile measured
   // 500 us against 543 (pipelined halo) / 579 (single-tap halo) at 256x256, B=32
   // (r3, stage-major weights: still 527 vs 503 us in alternating convbench runs)

@@ -246,6 +246,8 @@ def test_dataparallel_syncbn_256_two_ranks_match_single_process(dtype_name):
             assert v < max(0.25, 2 * gora[k]), (k, v, gora[k])
         assert max(bn.values()) < 5e-3
         return
+    # (both runs take the same kernels: at 2 and 4 images the latent 256-channel convs are on the
+    # 128-co tiles of conv.hip halo3_bn, AFE.down2 on its 256-co tile)
     # measured (r3): forward bit-identical (image 0.0, BN running stats 0.0), K 5e-8; gradients
     # median 2.6e-3.  The worst key, generator.mid_conv.bias (8.4e-2 in r3), is a plain sum over
     # 131,072 pixels of the residual-stream gradient, which is the bf16-rounded sum of the skip
