@@ -4906,7 +4906,9 @@ __global__ void tr8_probe_kernel(const int* lane_addr, int* out) {
 //   halo of chunk c = two images (ci 0-63 / 64-127) of [(TR+2) x 66 px][64 B], h3swz chunk
 //   swizzle (conflict-free fragment reads from any start), double-buffered across chunks.
 // Block: BN = 128 co x BM = 256 px (4 rows x 64), 8 waves 2 (co) x 4 (px), wave 64 x 64.
-template <int WN, int WM, int RN, int RM>
+// NSW: weight stages in the ring (2: issued one tap ahead; 3: two taps ahead, so a stage has two
+// taps of MFMAs to land before its barrier)
+template <int WN, int WM, int RN, int RM, int NSW = 2>
 __global__ void __launch_bounds__(64 * WN * WM, 1)
 conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
@@ -4916,7 +4918,8 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   constexpr int QH = 2 * HQ, JH = (QH + NW - 1) / NW;
   constexpr int BST = BN * 128, QB = BN / 8, JB = QB / NW;
   static_assert(QB % NW == 0, "weight pieces per wave");
-  constexpr int MAIN = 2 * HALO + 2 * BST, EPI = BM * BN * 2;
+  constexpr int MAIN = 2 * HALO + NSW * BST, EPI = BM * BN * 2;
+  static_assert(MAIN <= 163840, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
 
   // the delayed-scaling site of this launch's activation operand: its dq (read below by every
@@ -4960,7 +4963,7 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   }
   auto issue_b = [&](int ks) {
     const int c = ks / 9, t = ks - c * 9;
-    const unsigned Bs = sbase + 2 * HALO + (ks & 1) * BST;
+    const unsigned Bs = sbase + 2 * HALO + (ks % NSW) * BST;
     const unsigned k0 = (unsigned)(t * a.Cin + c * 128);
 #pragma unroll
     for (int j = 0; j < JB; ++j) dma16s(wr, Bs + (wave + j * NW) * 1024, wbase[j], k0);
@@ -4988,10 +4991,16 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   const int nch = a.Cin >> 7, nks = 9 * nch;
   issue_b(0);
   issue_halo(0);
+  if (NSW == 3 && 1 < nks) issue_b(1);
   for (int ks = 0; ks < nks; ++ks) {
     const int c = ks / 9, t = ks - c * 9;
-    // step 9c+1 may leave the halo of chunk c+1 (issued last, at step 9c) in flight
-    if (t == 1 && c + 1 < nch) {
+    if constexpr (NSW == 3) {
+      // stage ks (issued two steps ago) must land; stage ks + 1 (last step) may stay in flight,
+      // and at t == 1 the halo of chunk c + 1 issued after it at step 9c too
+      const int younger = (ks + 1 < nks ? JB : 0) + (t == 1 && c + 1 < nch ? nh : 0);
+      wait_vm_dyn(younger);
+    } else if (t == 1 && c + 1 < nch) {
+      // step 9c+1 may leave the halo of chunk c+1 (issued last, at step 9c) in flight
       if (nh == JH) wait_vm<JH>();
       else wait_vm<(JH > 0 ? JH - 1 : 0)>();
     } else {
@@ -5000,11 +5009,11 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (ks + 1 < nks) issue_b(ks + 1);
+    if (ks + NSW - 1 < nks) issue_b(ks + NSW - 1);
     if (t == 0 && c + 1 < nch) issue_halo(c + 1);
     const int r = t / 3, s3 = t - (t / 3) * 3;
     const char* Hs = smem + (c & 1) * HALO;
-    const char* Bs = smem + 2 * HALO + (ks & 1) * BST;
+    const char* Bs = smem + 2 * HALO + (ks % NSW) * BST;
     v8i fa[RN], fb[RM];
 #pragma unroll
     for (int i = 0; i < RN; ++i) {
@@ -5237,6 +5246,16 @@ conv3_wgrad_fp8(Wg8Args a) {
   });
 }
 
+// conv3_halo_fp8 with a 3-deep weight ring; FV_FP8_NSW3=0 for A/B
+static int g_nsw3 = -1;
+static bool fp8_nsw3() {
+  if (g_nsw3 < 0) {
+    const char* e = getenv("FV_FP8_NSW3");
+    g_nsw3 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_nsw3 != 0;
+}
+
 // fp8 conv eligibility: 3x3, stride 1, 'same', channel counts multiples of 128 (in and out),
 // W % 64 == 0, H % 4 == 0, bf16 NHWC output, operands < 2 GB
 bool fp8_ok(const fv_conv_desc* d) {
@@ -5266,7 +5285,8 @@ int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, co
   // res fwd / dgrad at B = 64 188 / 172 -> 208 / 192 us: the two waves of a SIMD already hide
   // each other's fragment reads (16 KB per 16 MFMAs of 32 cycles, half the CU's 256 B/clk of
   // LDS at the fp8 peak).)
-  hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+  if (fp8_nsw3()) hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
+  else hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
   return fv_check_launch("conv2d_fp8");
 }
 
