@@ -4906,8 +4906,8 @@ __global__ void tr8_probe_kernel(const int* lane_addr, int* out) {
 //   halo of chunk c = two images (ci 0-63 / 64-127) of [(TR+2) x 66 px][64 B], h3swz chunk
 //   swizzle (conflict-free fragment reads from any start), double-buffered across chunks.
 // Block: BN = 128 co x BM = 256 px (4 rows x 64), 8 waves 2 (co) x 4 (px), wave 64 x 64.
-// NSW: weight stages in the ring (2: issued one tap ahead; 3: two taps ahead, so a stage has two
-// taps of MFMAs to land before its barrier)
+// NSW: weight stages in the ring, issued NSW - 1 taps ahead (2; 3 measured slower, r4: res fwd
+// / dgrad at B = 64 195 / 177 -> 199-202 / 182-185 us, fp8 step 22.36 -> 22.69 ms)
 template <int WN, int WM, int RN, int RM, int NSW = 2>
 __global__ void __launch_bounds__(64 * WN * WM, 1)
 conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
@@ -5246,16 +5246,6 @@ conv3_wgrad_fp8(Wg8Args a) {
   });
 }
 
-// conv3_halo_fp8 with a 3-deep weight ring; FV_FP8_NSW3=0 for A/B
-static int g_nsw3 = -1;
-static bool fp8_nsw3() {
-  if (g_nsw3 < 0) {
-    const char* e = getenv("FV_FP8_NSW3");
-    g_nsw3 = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_nsw3 != 0;
-}
-
 // fp8 conv eligibility: 3x3, stride 1, 'same', channel counts multiples of 128 (in and out),
 // W % 64 == 0, H % 4 == 0, bf16 NHWC output, operands < 2 GB
 bool fp8_ok(const fv_conv_desc* d) {
@@ -5285,8 +5275,7 @@ int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, co
   // res fwd / dgrad at B = 64 188 / 172 -> 208 / 192 us: the two waves of a SIMD already hide
   // each other's fragment reads (16 KB per 16 MFMAs of 32 cycles, half the CU's 256 B/clk of
   // LDS at the fp8 peak).)
-  if (fp8_nsw3()) hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
-  else hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+  hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
   return fv_check_launch("conv2d_fp8");
 }
 
