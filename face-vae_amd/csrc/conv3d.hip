@@ -267,6 +267,7 @@ struct C3WArgs {
   float* bslab;   // [nblk][32]
   int N, D, H;
   int nper;       // images per block
+  int ndc;        // depth chunks (blocks per (images, row tile)): fills the CUs at small batch
   unsigned xbytes, dybytes;
 };
 
@@ -275,9 +276,11 @@ __global__ void __launch_bounds__(512, 1) conv3d_c32_wgrad(C3WArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nht = a.H / W3_TH;
-  const int ht = blockIdx.x % nht, nb = blockIdx.x / nht;
+  const int dc = blockIdx.x % a.ndc, rest = blockIdx.x / a.ndc;
+  const int ht = rest % nht, nb = rest / nht;
   const int h0 = ht * W3_TH;
   const int n0 = nb * a.nper, n1 = min(a.N, n0 + a.nper);
+  const int dch = (a.D + a.ndc - 1) / a.ndc, d0 = min(a.D, dc * dch), d1 = min(a.D, d0 + dch);
 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.dy), 0, (int)a.dybytes, 0x00020000);
@@ -339,16 +342,16 @@ __global__ void __launch_bounds__(512, 1) conv3d_c32_wgrad(C3WArgs a) {
     tkw[m] = t % 3;
   }
 
-  for (int n = n0; n < n1; ++n) {
-    issue_x(n, -1);
-    issue_x(n, 0);
-    issue_x(n, 1);
-    issue_dy(n, 0);
-    for (int d = 0; d < a.D; ++d) {
+  for (int n = n0; n < n1 && d0 < d1; ++n) {
+    issue_x(n, d0 - 1);
+    issue_x(n, d0);
+    issue_x(n, d0 + 1);
+    issue_dy(n, d0);
+    for (int d = d0; d < d1; ++d) {
       vm_wait0();
       __syncthreads();
-      if (d + 2 <= a.D) issue_x(n, d + 2);
-      if (d + 1 < a.D) issue_dy(n, d + 1);
+      if (d + 2 <= d1) issue_x(n, d + 2);
+      if (d + 1 < d1) issue_dy(n, d + 1);
       const char* db = smem + W3_NX * W3_XSLOT + (d & 1) * W3_DSLOT;
 #pragma unroll 1
       for (int ks = 0; ks < W3_TH * 2; ++ks) {      // 32-voxel k steps: row rr, half sg
@@ -569,7 +572,15 @@ int c3w_nper(const fv_conv3d_desc* d) {
   while (d->n % (2 * nper) == 0 && (long)(d->n / (2 * nper)) * nht >= 256) nper *= 2;
   return nper;
 }
-int c3w_nblk(const fv_conv3d_desc* d) { return (d->n / c3w_nper(d)) * (d->h / W3_TH); }
+// depth chunks: split the depth walk until the grid covers the 256 CUs (chunks of >= 4 slices;
+// each chunk re-stages its 2 halo slices)
+int c3w_ndc(const fv_conv3d_desc* d) {
+  const long nb0 = (long)(d->n / c3w_nper(d)) * (d->h / W3_TH);
+  int ndc = 1;
+  while (nb0 * ndc < 256 && d->d / (2 * ndc) >= 4) ndc *= 2;
+  return ndc;
+}
+int c3w_nblk(const fv_conv3d_desc* d) { return (d->n / c3w_nper(d)) * (d->h / W3_TH) * c3w_ndc(d); }
 constexpr int C3W_NS = 16;
 
 }  // namespace
@@ -672,7 +683,7 @@ int fv_conv3d_bwd_weight(const fv_conv3d_desc* d, const void* x, const void* dy,
     a.x = (const bf16*)x; a.dy = (const bf16*)dy;
     a.slab = (float*)ws;
     a.bslab = db ? a.slab + (long)nblk * 32 * 864 : nullptr;
-    a.N = d->n; a.D = d->d; a.H = d->h; a.nper = c3w_nper(d);
+    a.N = d->n; a.D = d->d; a.H = d->h; a.nper = c3w_nper(d); a.ndc = c3w_ndc(d);
     a.xbytes = a.dybytes = (unsigned)((long)d->n * d->d * d->h * 64 * 32 * 2);
     hipLaunchKernelGGL(conv3d_c32_wgrad, dim3(nblk), dim3(512), 0, s, a);
     if ((st = fv_check_launch("conv3d_c32_wgrad"))) return st;
