@@ -546,6 +546,51 @@ __global__ void __launch_bounds__(256) depth_split_kernel(const T* __restrict__ 
   else dst[i3] = src[i2];
 }
 
+// bf16, C = 32, D = 16 (the AFE / Generator volume): one wave per 2 pixels, the 2 x 512-element
+// [c][d] blocks through LDS -- every global access is a 32-B lane chunk (the element-wise kernel
+// above reads 2 B per lane at a 32-B stride: 1.6 TB/s at B=8, r4 trace).  split: src
+// [N][HW][c * 16 + d] -> dst [N][16][HW][32]; inverse: the reverse.
+__global__ void __launch_bounds__(256) depth_split_c32d16(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                          int HW, int inverse) {
+  __shared__ __attribute__((aligned(16))) bf16 sm[4][2 * 512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long pp = ((long)blockIdx.x * 4 + w) * 2;              // first of the wave's 2 pixels (n * HW + p)
+  const int n = (int)(pp / HW), p0 = (int)(pp - (long)n * HW);
+  bf16* const t = sm[w];
+  // the lane's (pixel, d, 16-channel half) of the [N][16][HW][32] side
+  const int px = lane >> 5, d = (lane & 31) >> 1, cb = (lane & 1) * 16;
+  const long i3 = (((long)n * 16 + d) * HW + p0 + px) * 32 + cb;
+  if (!inverse) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src + pp * 512 + lane * 16);
+    uint4* t4 = reinterpret_cast<uint4*>(t + lane * 16);
+    t4[0] = s4[0];
+    t4[1] = s4[1];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bf16 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = t[px * 512 + (cb + k) * 16 + d];
+    uint4* o = reinterpret_cast<uint4*>(dst + i3);
+    o[0] = *reinterpret_cast<const uint4*>(v);
+    o[1] = *reinterpret_cast<const uint4*>(v + 8);
+  } else {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src + i3);
+    bf16 v[16];
+    *reinterpret_cast<uint4*>(v) = s4[0];
+    *reinterpret_cast<uint4*>(v + 8) = s4[1];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t[px * 512 + (cb + k) * 16 + d] = v[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint4* o = reinterpret_cast<uint4*>(dst + pp * 512 + lane * 16);
+    const uint4* t4 = reinterpret_cast<const uint4*>(t + lane * 16);
+    o[0] = t4[0];
+    o[1] = t4[1];
+  }
+}
+
 bool c32_fast(const fv_conv3d_desc* d) {
   return d->dtype == FV_BF16 && d->cin == 32 && d->cout == 32 && d->w == 64 && d->h % 4 == 0 &&
          (long)d->n * d->d * d->h * d->w * 32 * 2 < (1L << 31);
@@ -709,6 +754,11 @@ int fv_depth_split(int dtype, const void* src, int n, int hw, int c, int d, int 
   FV_REQUIRE(src && dst && n > 0 && hw > 0 && c > 0 && d > 0, "depth_split: bad argument");
   FV_REQUIRE(dtype == FV_F32 || dtype == FV_BF16, "depth_split: f32 or bf16");
   const long per = (long)d * hw * c;
+  if (dtype == FV_BF16 && c == 32 && d == 16 && ((long)n * hw) % 8 == 0) {
+    hipLaunchKernelGGL(depth_split_c32d16, dim3((unsigned)((long)n * hw / 8)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)src, (bf16*)dst, hw, inverse);
+    return fv_check_launch("depth_split");
+  }
   dim3 g(fv_cdiv(per, 256), n);
   if (dtype == FV_BF16)
     hipLaunchKernelGGL(depth_split_kernel<bf16>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)src, (bf16*)dst,

@@ -108,6 +108,234 @@ __global__ void __launch_bounds__(256) grid_sample3d_bwd(const T* __restrict__ i
   }
 }
 
+// forward with lanes over 8-channel chunks (Chunk8: 16 B bf16 / 32 B fp32 per corner gather;
+// C % 8 == 0): the 1-channel-per-lane kernel above issued eight 2-byte gathers per bf16 row of
+// 64 B.  Same corner order and arithmetic -> bit-identical.
+template <typename T>
+__global__ void __launch_bounds__(256) grid_sample3d_fwd8(const T* __restrict__ in, const float* __restrict__ grid,
+                                                          T* __restrict__ out, int B, int Di, int Hi, int Wi, long Vo,
+                                                          int C, int group) {
+  const int C8 = C >> 3;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long v = gid / C8;
+  const int q = (int)(gid - v * C8);
+  if (v >= (long)B * Vo) return;
+  const int b = (int)(v / Vo);
+  const float* gp = grid + v * 3;
+  const float ix = src_index(gp[0], Wi), iy = src_index(gp[1], Hi), iz = src_index(gp[2], Di);
+  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+  const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+  const float tx = ix - fx, ty = iy - fy, tz = iz - fz;
+  const T* base = in + (long)(b / group) * Di * Hi * Wi * C + q * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+    const int xx = x0 + dx, yy = y0 + dy, zz = z0 + dz;
+    if ((unsigned)xx < (unsigned)Wi && (unsigned)yy < (unsigned)Hi && (unsigned)zz < (unsigned)Di) {
+      const float w = (dx ? tx : 1.f - tx) * (dy ? ty : 1.f - ty) * (dz ? tz : 1.f - tz);
+      Chunk8<T> c;
+      c.load(base + (((long)zz * Hi + yy) * Wi + xx) * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += w * c.get(j);
+    }
+  }
+  Chunk8<T> o;
+  o.set8(acc);
+  o.store(out + v * C + q * 8);
+}
+
+// ---- input gradient by gathering (fv_grid_sample3d_bwd_input) --------------------------------
+// The scatter above adds 8 corners x C float atomics per output voxel (134 M at the §8(f) shape,
+// 395 µs at B = 8).  Instead: bucket the output voxels by their base input cell (x0, y0, z0) --
+// one int atomic per voxel for the counts, an exclusive scan, a fill -- and let each input cell
+// sum the up-to-8 buckets whose corner it is.  Every gin element is written once, no zeroing.
+// Bucket keys cover base cells in [-1, size - 1] per axis (a voxel whose base is outside has no
+// corner inside and drops out).
+struct GsRec {
+  int v;
+  float tx, ty, tz;
+};
+constexpr int GS_SCAN = 1024;   // counts per scan block
+
+__device__ __forceinline__ bool gs_base(const float* grid, long v, int Di, int Hi, int Wi, int& x0, int& y0, int& z0,
+                                        float& tx, float& ty, float& tz) {
+  const float* gp = grid + v * 3;
+  const float ix = src_index(gp[0], Wi), iy = src_index(gp[1], Hi), iz = src_index(gp[2], Di);
+  const float fx = floorf(ix), fy = floorf(iy), fz = floorf(iz);
+  // NaN and far-outside coordinates fail these tests before any float -> int conversion
+  if (!(fx >= -1.f && fx <= (float)(Wi - 1) && fy >= -1.f && fy <= (float)(Hi - 1) && fz >= -1.f &&
+        fz <= (float)(Di - 1)))
+    return false;
+  x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+  tx = ix - fx, ty = iy - fy, tz = iz - fz;
+  return true;
+}
+__device__ __forceinline__ int gs_key(int bi, int z0, int y0, int x0, int Di, int Hi, int Wi) {
+  return ((bi * (Di + 1) + z0 + 1) * (Hi + 1) + y0 + 1) * (Wi + 1) + x0 + 1;
+}
+
+__global__ void __launch_bounds__(256) gs_bucket_count(const float* __restrict__ grid, long nvox, long Vo, int Di,
+                                                       int Hi, int Wi, int group, int* __restrict__ cnt,
+                                                       int2* __restrict__ keyrank) {
+  const long v = (long)blockIdx.x * 256 + threadIdx.x;
+  if (v >= nvox) return;
+  int x0, y0, z0;
+  float tx, ty, tz;
+  int2 kr = make_int2(-1, 0);
+  if (gs_base(grid, v, Di, Hi, Wi, x0, y0, z0, tx, ty, tz)) {
+    kr.x = gs_key((int)(v / Vo) / group, z0, y0, x0, Di, Hi, Wi);
+    kr.y = atomicAdd(cnt + kr.x, 1);
+  }
+  keyrank[v] = kr;
+}
+
+// exclusive scan of the block's 1024 values a[4] per thread; returns the thread's prefix and the
+// block total in *total (256 threads)
+__device__ __forceinline__ int gs_block_scan(const int (&a)[4], int* total) {
+  __shared__ int wsum[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = a[0] + a[1] + a[2] + a[3];
+  int x = t;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int wo = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) wo += k < w ? wsum[k] : 0;
+  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return wo + x - t;
+}
+
+// cnt[0, n) -> offsets within each 1024-block; bsum[blk] = the block's total
+__global__ void __launch_bounds__(256) gs_scan_blocks(int* __restrict__ cnt, long n, int* __restrict__ bsum) {
+  const long i0 = (long)blockIdx.x * GS_SCAN + threadIdx.x * 4;
+  int a[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = i0 + j < n ? cnt[i0 + j] : 0;
+  int total;
+  int e = gs_block_scan(a, &total);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (i0 + j < n) cnt[i0 + j] = e;
+    e += a[j];
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+// one block: bsum[0, nb) -> exclusive prefix sums, 1024 at a time with a carry
+__global__ void __launch_bounds__(256) gs_scan_totals(int* __restrict__ bsum, int nb) {
+  int carry = 0;
+  for (int base = 0; base < nb; base += GS_SCAN) {
+    const int i0 = base + threadIdx.x * 4;
+    int a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = i0 + j < nb ? bsum[i0 + j] : 0;
+    int total;
+    int e = gs_block_scan(a, &total) + carry;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i0 + j < nb) bsum[i0 + j] = e;
+      e += a[j];
+    }
+    carry += total;
+  }
+}
+
+__device__ __forceinline__ int gs_offset(const int* off, const int* boff, int key) {
+  return off[key] + boff[key / GS_SCAN];
+}
+
+__global__ void __launch_bounds__(256) gs_bucket_fill(const float* __restrict__ grid, const int2* __restrict__ keyrank,
+                                                      const int* __restrict__ off, const int* __restrict__ boff,
+                                                      long nvox, int Di, int Hi, int Wi, GsRec* __restrict__ rec) {
+  const long v = (long)blockIdx.x * 256 + threadIdx.x;
+  if (v >= nvox) return;
+  const int2 kr = keyrank[v];
+  if (kr.x < 0) return;
+  int x0, y0, z0;
+  float tx, ty, tz;
+  gs_base(grid, v, Di, Hi, Wi, x0, y0, z0, tx, ty, tz);
+  GsRec r;
+  r.v = (int)v, r.tx = tx, r.ty = ty, r.tz = tz;
+  rec[gs_offset(off, boff, kr.x) + kr.y] = r;
+}
+
+// one lane per (input cell, V-channel chunk); V = 8 (Chunk8 rows, C % 8 == 0) or 1
+template <typename T, int V>
+__global__ void __launch_bounds__(256) gs_gather_input(const GsRec* __restrict__ rec, const int* __restrict__ off,
+                                                       const int* __restrict__ boff, const T* __restrict__ gout,
+                                                       long ncell, int Di, int Hi, int Wi, int C, T* __restrict__ gin) {
+  const int CV = C / V;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  const long cell = gid / CV;
+  const int q = (int)(gid - cell * CV);
+  if (cell >= ncell) return;
+  const int x = (int)(cell % Wi);
+  long t = cell / Wi;
+  const int y = (int)(t % Hi);
+  t /= Hi;
+  const int z = (int)(t % Di), bi = (int)(t / Di);
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
+    const int key = gs_key(bi, z - dz, y - dy, x - dx, Di, Hi, Wi);
+    const int e = gs_offset(off, boff, key + 1);
+    for (int r = gs_offset(off, boff, key); r < e; ++r) {
+      const GsRec R = rec[r];
+      const float w = (dx ? R.tx : 1.f - R.tx) * (dy ? R.ty : 1.f - R.ty) * (dz ? R.tz : 1.f - R.tz);
+      const T* g = gout + (long)R.v * C + q * V;
+      if constexpr (V == 8) {
+        Chunk8<T> c;
+        c.load(g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += w * c.get(j);
+      } else {
+        acc[0] += w * ld(g);
+      }
+    }
+  }
+  T* o = gin + cell * C + q * V;
+  if constexpr (V == 8) {
+    Chunk8<T> c;
+    c.set8(acc);
+    c.store(o);
+  } else {
+    o[0] = Elt<T>::from_f(acc[0]);
+  }
+}
+
+struct GsWs {
+  int *cnt, *bsum;
+  int2* keyrank;
+  GsRec* rec;
+  long nkey, nblk, nvox;
+  size_t bytes;
+};
+static GsWs gs_ws_layout(void* base, int B, int Di, int Hi, int Wi, int Do, int Ho, int Wo, int group) {
+  GsWs w;
+  w.nvox = (long)B * Do * Ho * Wo;
+  w.nkey = (long)(B / group) * (Di + 1) * (Hi + 1) * (Wi + 1) + 1;   // + 1: the end offset of the last key
+  w.nblk = (w.nkey + GS_SCAN - 1) / GS_SCAN;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  char* p = (char*)base;
+  size_t o = 0;
+  w.cnt = (int*)(p + o), o += up(w.nkey * 4);
+  w.bsum = (int*)(p + o), o += up(w.nblk * 4);
+  w.keyrank = (int2*)(p + o), o += up(w.nvox * 8);
+  w.rec = (GsRec*)(p + o), o += up(w.nvox * sizeof(GsRec));
+  w.bytes = o;
+  return w;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) f32_to_kernel(const float* __restrict__ a, T* __restrict__ b, long n) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -339,6 +567,16 @@ int fv_grid_sample3d_fwd(int dtype, const void* in, const float* grid, int B, in
   FV_REQUIRE(dtype == FV_F32 || dtype == FV_BF16, "grid_sample3d: f32 or bf16");
   hipStream_t s = (hipStream_t)stream;
   const long nvox = (long)B * Do * Ho * Wo;
+  if (C % 8 == 0) {
+    const int nb8 = fv_cdiv(nvox * (C / 8), 256);
+    if (dtype == FV_BF16)
+      hipLaunchKernelGGL(grid_sample3d_fwd8<bf16>, dim3(nb8), dim3(256), 0, s, (const bf16*)in, grid, (bf16*)out, B,
+                         Di, Hi, Wi, (long)Do * Ho * Wo, C, group);
+    else
+      hipLaunchKernelGGL(grid_sample3d_fwd8<float>, dim3(nb8), dim3(256), 0, s, (const float*)in, grid, (float*)out,
+                         B, Di, Hi, Wi, (long)Do * Ho * Wo, C, group);
+    return fv_check_launch("grid_sample3d_fwd");
+  }
   const int lpv = lpv_of(C);
   const int nb = fv_cdiv(nvox * lpv, 256);
 #define GS_FWD(T, L)                                                                                              \
@@ -381,6 +619,40 @@ int fv_grid_sample3d_bwd(int dtype, const void* in, const float* grid, const voi
     GS_DISPATCH(GS_BWD, float)
   }
   return fv_check_launch("grid_sample3d_bwd");
+}
+
+size_t fv_grid_sample3d_bwd_input_ws_bytes(int B, int Di, int Hi, int Wi, int Do, int Ho, int Wo, int group) {
+  if (B <= 0 || group <= 0 || B % group) return 0;
+  return gs_ws_layout(nullptr, B, Di, Hi, Wi, Do, Ho, Wo, group).bytes;
+}
+
+int fv_grid_sample3d_bwd_input(int dtype, const float* grid, const void* gout, int B, int Di, int Hi, int Wi, int Do,
+                               int Ho, int Wo, int C, int group, void* gin, void* ws, void* stream) {
+  FV_REQUIRE(grid && gout && gin && ws && B > 0 && C > 0 && group > 0 && B % group == 0 && Di > 0 && Hi > 0 &&
+                 Wi > 0 && Do > 0 && Ho > 0 && Wo > 0,
+             "grid_sample3d_bwd_input: bad argument");
+  FV_REQUIRE(dtype == FV_F32 || dtype == FV_BF16, "grid_sample3d_bwd_input: f32 or bf16");
+  const GsWs w = gs_ws_layout(ws, B, Di, Hi, Wi, Do, Ho, Wo, group);
+  FV_REQUIRE(w.nvox < (1L << 31) && w.nkey < (1L << 31), "grid_sample3d_bwd_input: more than 2^31 voxels or cells");
+  hipStream_t s = (hipStream_t)stream;
+  const long ncell = (long)(B / group) * Di * Hi * Wi;
+  hipMemsetAsync(w.cnt, 0, w.nkey * sizeof(int), s);
+  hipLaunchKernelGGL(gs_bucket_count, dim3(fv_cdiv(w.nvox, 256)), dim3(256), 0, s, grid, w.nvox, (long)Do * Ho * Wo, Di,
+                     Hi, Wi, group, w.cnt, w.keyrank);
+  hipLaunchKernelGGL(gs_scan_blocks, dim3((unsigned)w.nblk), dim3(256), 0, s, w.cnt, w.nkey, w.bsum);
+  hipLaunchKernelGGL(gs_scan_totals, dim3(1), dim3(256), 0, s, w.bsum, (int)w.nblk);
+  hipLaunchKernelGGL(gs_bucket_fill, dim3(fv_cdiv(w.nvox, 256)), dim3(256), 0, s, grid, w.keyrank, w.cnt, w.bsum,
+                     w.nvox, Di, Hi, Wi, w.rec);
+#define GS_GATHER(T, V)                                                                                          \
+  hipLaunchKernelGGL((gs_gather_input<T, V>), dim3(fv_cdiv(ncell * (C / V), 256)), dim3(256), 0, s, w.rec, w.cnt, \
+                     w.bsum, (const T*)gout, ncell, Di, Hi, Wi, C, (T*)gin)
+  if (dtype == FV_BF16) {
+    if (C % 8 == 0) GS_GATHER(bf16, 8); else GS_GATHER(bf16, 1);
+  } else {
+    if (C % 8 == 0) GS_GATHER(float, 8); else GS_GATHER(float, 1);
+  }
+#undef GS_GATHER
+  return fv_check_launch("grid_sample3d_bwd_input");
 }
 
 int fv_f32_to(int dtype, const float* a, void* b, long n, void* stream) {

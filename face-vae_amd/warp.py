@@ -79,20 +79,18 @@ class GridSample3dFn(torch.autograd.Function):
         B, Do, Ho, Wo, _ = g32.shape
         go = gout.to(ctx.dtype).contiguous(memory_format=CL3)
         gin = ggrid = None
-        gin32 = None
         if ctx.needs_input_grad[0]:
-            gin32 = torch.empty((Bi, C, Di, Hi, Wi), dtype=F32, device=xb.device, memory_format=CL3).zero_()
+            # input gradient by bucketed gather (no float atomics, no fp32 staging buffer)
+            nws = L.query("fv_grid_sample3d_bwd_input_ws_bytes", B, Di, Hi, Wi, Do, Ho, Wo, ctx.group)
+            ws = torch.empty(nws, dtype=torch.uint8, device=xb.device)
+            gin = torch.empty((Bi, C, Di, Hi, Wi), dtype=ctx.dtype, device=xb.device, memory_format=CL3)
+            call("fv_grid_sample3d_bwd_input", L.dtype_code(ctx.dtype), ptr(g32), ptr(go), B, Di, Hi, Wi, Do, Ho, Wo,
+                 C, ctx.group, ptr(gin), ptr(ws), stream())
+            gin = gin.to(ctx.in_dtype)
         if ctx.needs_input_grad[1]:
             ggrid = torch.empty_like(g32)
-        call("fv_grid_sample3d_bwd", L.dtype_code(ctx.dtype), ptr(xb), ptr(g32), ptr(go), B, Di, Hi, Wi, Do, Ho, Wo, C,
-             ctx.group, ptr(gin32), ptr(ggrid), stream())
-        if gin32 is not None:
-            if ctx.in_dtype == F32:
-                gin = gin32
-            else:
-                gin = torch.empty((Bi, C, Di, Hi, Wi), dtype=ctx.dtype, device=xb.device, memory_format=CL3)
-                call("fv_f32_to", L.dtype_code(ctx.dtype), ptr(gin32), ptr(gin), gin.numel(), stream())
-                gin = gin.to(ctx.in_dtype)
+            call("fv_grid_sample3d_bwd", L.dtype_code(ctx.dtype), ptr(xb), ptr(g32), ptr(go), B, Di, Hi, Wi, Do, Ho,
+                 Wo, C, ctx.group, None, ptr(ggrid), stream())
         return gin, ggrid, None, None
 
 

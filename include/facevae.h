@@ -310,6 +310,12 @@ int fv_grid_sample3d_fwd(int dtype, const void* in, const float* grid, int B, in
  * either may be NULL */
 int fv_grid_sample3d_bwd(int dtype, const void* in, const float* grid, const void* gout, int B, int Di, int Hi,
                          int Wi, int Do, int Ho, int Wo, int C, int group, float* gin, float* ggrid, void* stream);
+/* gin (dtype, input layout, every element written) = dL/din without float atomics: the output
+ * voxels are bucketed by their base input cell (count, scan, fill in ws) and each input cell sums
+ * the buckets whose corner it is.  ws: fv_grid_sample3d_bwd_input_ws_bytes bytes. */
+size_t fv_grid_sample3d_bwd_input_ws_bytes(int B, int Di, int Hi, int Wi, int Do, int Ho, int Wo, int group);
+int fv_grid_sample3d_bwd_input(int dtype, const float* grid, const void* gout, int B, int Di, int Hi, int Wi, int Do,
+                               int Ho, int Wo, int C, int group, void* gin, void* ws, void* stream);
 int fv_f32_to(int dtype, const float* a, void* b, long n, void* stream);
 /* fs * occlusion (models.py:1106): x [P][C] NHWC, occ [P] fp32; backward dx = g*occ (may be
  * NULL), docc[p] = sum_c g x (may be NULL) */

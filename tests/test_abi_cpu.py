@@ -42,11 +42,15 @@ def test_descriptor_queries(lib_built):
     import ctypes
     import fvamd  # noqa: F401
     from facevae_amd import _lib, ops
-    d = ops.desc(torch.bfloat16, 2, 64, 64, 256, 256, 256, 256, 3)
+    d = ops.desc(torch.bfloat16, 32, 64, 64, 256, 256, 256, 256, 3)
     assert _lib.query("fv_conv_wk_elems", ctypes.byref(d)) == 256 * 9 * 256
     bp = _lib.query("fv_conv2d_stats_block_pixels", ctypes.byref(d))
     assert bp == 128   # 256x256 tiles for 256-channel 3x3 convs: one record per 128-pixel wave row
-    assert _lib.query("fv_conv2d_stats_blocks", ctypes.byref(d)) == 2 * 64 * 64 // bp
+    assert _lib.query("fv_conv2d_stats_blocks", ctypes.byref(d)) == 32 * 64 * 64 // bp
+    small = ops.desc(torch.bfloat16, 2, 64, 64, 256, 256, 256, 256, 3)
+    bp = _lib.query("fv_conv2d_stats_block_pixels", ctypes.byref(small))
+    assert bp == 64    # 32 256-co tiles would leave most CUs idle: the 128-co tiles, 64-pixel rows
+    assert _lib.query("fv_conv2d_stats_blocks", ctypes.byref(small)) == 2 * 64 * 64 // bp
     bad = ops.desc(torch.bfloat16, 2, 64, 64, 24, 24, 256, 256, 3)   # cin not a power of two
     assert _lib.query("fv_conv_wk_elems", ctypes.byref(bad)) == 0
     assert _lib.query("fv_conv2d_fwd", ctypes.byref(bad), None, None, None, None, None, None, None, None,

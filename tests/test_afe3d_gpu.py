@@ -96,18 +96,21 @@ def test_conv3d_kernels_vs_torch(shape, dtype):
     assert rel(db, bb.grad) < wtol
 
 
-def test_depth_split_round_trip():
+@pytest.mark.parametrize("shape", [(2, 32, 2, 8, 16), (2, 32, 16, 8, 16), (1, 32, 16, 3, 5)])
+def test_depth_split_round_trip(shape):
+    """(2, 32, 16, 8, 16): the bf16 C=32/D=16 LDS-tiled kernel; (1, 32, 16, 3, 5): its ragged fallback."""
+    n, c, d, hh, ww = shape
     g = torch.Generator().manual_seed(5)
-    h = torch.randn(2, 64, 8, 16, generator=g)
+    h = torch.randn(n, c * d, hh, ww, generator=g)
     for dt in (torch.float32, torch.bfloat16):
         hb = h.cuda().to(dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
-        fs = ops3d.DepthSplitFn.apply(hb, 32, 2, dt)
-        assert torch.equal(fs.float().cpu(), h.to(dt).float().view(2, 32, 2, 8, 16))
+        fs = ops3d.DepthSplitFn.apply(hb, c, d, dt)
+        assert torch.equal(fs.float().cpu(), h.to(dt).float().view(*shape))
         back = ops3d.DepthMergeFn.apply(fs, dt)
         assert torch.equal(back.float().cpu(), h.to(dt).float())
-        gg = torch.randn(2, 32, 2, 8, 16, generator=g).cuda()
+        gg = torch.randn(*shape, generator=g).cuda()
         fs.backward(gg)
-        assert torch.equal(hb.grad.float().cpu(), gg.to(dt).float().cpu().view(2, 64, 8, 16))
+        assert torch.equal(hb.grad.float().cpu(), gg.to(dt).float().cpu().view(n, c * d, hh, ww))
 
 
 def _res3d_case(mode):

@@ -2,7 +2,7 @@
 F.grid_sample on the CPU (same operands), the MFE motion assembly and the warped Generator
 against fixtures generated from the reference (tests/golden/warp.pt).
 
-Tolerances: fp32 1e-5 (kernels; grid_sample's input gradient sums float atomics in a run-
+Tolerances: fp32 1e-5 (kernels; grid_sample's input gradient sums each cell's buckets in a run-
 dependent order, 1e-5 relative), Generator fp32 mode 1e-4 (the north_star 1e-3 bar with
 margin); bf16 storage of the sampled volume: 4e-3 rel-L2 / 1.6e-2 max-abs of max|ref|."""
 import os
@@ -39,6 +39,8 @@ def load(k):
     (2, 32, 4, 8, 16, 3, 5, 7, 1, torch.bfloat16),
     (2, 4, 4, 8, 8, 4, 8, 8, 6, torch.float32),      # deformed source: one input per 6 grids
     (1, 24, 3, 5, 6, 2, 4, 9, 1, torch.float32),     # channel count off the power-of-two lanes
+    (1, 6, 3, 5, 6, 4, 3, 5, 1, torch.bfloat16),     # C % 8 != 0: one channel per lane
+    (3, 8, 2, 3, 4, 5, 6, 7, 2, torch.bfloat16),     # group > 1 on the 8-channel rows
 ])
 def test_grid_sample3d_vs_torch(N, C, Di, Hi, Wi, Do, Ho, Wo, group, dtype):
     g = torch.Generator().manual_seed(9)
@@ -170,3 +172,26 @@ def test_reference_size_afe_to_warped_generator_vs_oracle():
           + " ".join(f"{k} {a:.1e}/{b:.1e}" for _, k, a, b in worst[:4]))
     assert max(fwd.values()) < 1e-3, fwd
     assert worst[0][0] < 1.0, worst[:4]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_grid_sample3d_warp_shape_vs_torch(dtype):
+    """The §8(f) warp at its real volume (C = 32, 16 x 64 x 64, two images) with the fbench
+    deformation (identity + 0.05 N(0, 1)): every input cell's gradient gathered from its buckets."""
+    g = torch.Generator().manual_seed(11)
+    N, C, D, H, W = 2, 32, 16, 64, 64
+    inp = torch.randn(N, C, D, H, W, generator=g)
+    grid = warp.make_coordinate_grid_3d((D, H, W))[None] + 0.05 * torch.randn(N, D, H, W, 3, generator=g)
+    gout = torch.randn(N, C, D, H, W, generator=g)
+    xi = inp.cuda().to(dtype).contiguous(memory_format=CL3).requires_grad_(True)
+    out = warp.GridSample3dFn.apply(xi, grid.cuda(), 1, dtype)
+    out.backward(gout.cuda().to(dtype))
+    torch.cuda.synchronize()
+    ir = inp.to(dtype).float().requires_grad_(True)
+    ref = F.grid_sample(ir, grid, align_corners=True)
+    ref.backward(gout.to(dtype).float())
+    if dtype == torch.float32:
+        assert rel(out, ref) < 1e-5 and rel(xi.grad, ir.grad) < 1e-5
+    else:
+        for a, b in ((out, ref), (xi.grad, ir.grad)):
+            assert rel(a.float(), b) < 4e-3 and maxd(a.float(), b) <= 1.6e-2 * b.abs().max().item()
