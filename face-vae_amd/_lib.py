@@ -120,7 +120,7 @@ _SIGS = {
     "fv_grid_sample3d_bwd": (c_int, [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                      c_int, P, P, P]),
     "fv_grid_sample3d_bwd_input_ws_bytes": (c_size_t, [c_int] * 8),
-    "fv_grid_sample3d_bwd_input": (c_int, [c_int, P, P] + [c_int] * 10 + [P, P, P]),
+    "fv_grid_sample3d_bwd_input": (c_int, [c_int, P, P] + [c_int] * 9 + [P, P, P]),
     "fv_f32_to": (c_int, [c_int, P, P, c_long, P]),
     "fv_occlusion_fwd": (c_int, [c_int, P, P, c_long, c_int, P, P]),
     "fv_occlusion_bwd": (c_int, [c_int, P, P, P, c_long, c_int, P, P, P]),
