@@ -19,7 +19,15 @@
 //     kw = 0 / 2 fragments made by DPP lane shifts (r2-r3 read all three: 4 per 8 MFMAs, half
 //     the CU's LDS bandwidth at the MFMA peak, each read a latency the single wave per SIMD
 //     must cover).  Epilogue: bias, optional residual,
-//     BN (sum, sum of squares) partials per wave, bf16 store.
+//     BN (sum, sum of squares) partials per wave, bf16 store.  Used when the depth chunk has
+//     no 3k - 2 length (below).
+//   conv3d_c32_fwd_dr -- the same GEMM walked by INPUT slice: each slice's 12 fragments per kh
+//     (4 from LDS, 8 by DPP) feed the three outputs it touches through three rotating
+//     accumulator sets, so the fragment work is paid once per slice instead of three times; a
+//     2-slot slice ring plus the residual rows by LDS-DMA, waits that let the previous
+//     epilogue's stores pend, and a fence-free barrier (the chunk walk is peeled so the
+//     accumulator rotation is static: chunk lengths 3k - 2).  r4: [32, 32, 16, 64, 64]
+//     forward 143-146 -> 118-122 us (0.39 of the bf16 peak).
 //   conv3d_c32_wgrad -- dW[co][tap][ci] = sum_v dy[v][co] x[v + off(tap)][ci] (+ db), K =
 //     voxels.  A block of 8 waves owns 4 rows of one or more images and slides along depth
 //     with a 4-slot x ring (6 rows x 80 voxel rows incl. zero halo columns) and a 2-slot dy
@@ -28,6 +36,8 @@
 //     Per-block fp32 slabs [blk][32][27 x 32] are reduced deterministically (two passes).
 // Generic path (any C, W, fp32 parity mode or bf16): direct VALU kernels.
 #include <stdlib.h>
+
+#include <type_traits>
 
 #include "common.h"
 
@@ -246,6 +256,213 @@ __global__ void __launch_bounds__(64 * 4 * (2 / NI), 1) conv3d_c32_fwd(C3Args a)
         if (li == 0) {
           a.stats[(rec * 2) * 32 + cb0 + 16 * i + 4 * g + k] = S;
           a.stats[(rec * 2 + 1) * 32 + cb0 + 16 * i + 4 * g + k] = Q;
+        }
+      }
+  }
+}
+
+// Depth-reuse variant: the wave walks INPUT depth slices and applies each slice's 12 activation
+// fragments (4 centre + 8 DPP-shifted, per kh) to the three outputs it feeds -- s + 1 (kd = 0),
+// s (kd = 1), s - 1 (kd = 2) -- with three rotating accumulator sets, so the DPP shifts and LDS
+// reads are paid once per slice instead of once per (slice, kd): 1/3 of the VALU per MFMA of
+// conv3d_c32_fwd (whose DPP issue, 8 cycles per 16x16x32 MFMA free beside it, was the limiter).
+// Only the current slice is read, so a 2-slot ring (48 KB).  Output s - 1 is complete after
+// slice s and leaves through the same epilogue.
+constexpr int C3R_NS = 2;
+template <bool fN, bool fM, bool fP>
+__device__ __forceinline__ void c3r_slice(const char* sb, int row, int lane, const bf16x8 (&wf)[27][2],
+                                          f32x4 (&aN)[2][4], f32x4 (&aM)[2][4], f32x4 (&aP)[2][4]) {
+  const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const char* rb = sb + (row + kh) * C3_ROWB;
+    bf16x8 cx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int v = 16 * j + li;
+      cx[j] = *reinterpret_cast<const bf16x8*>(rb + v * 64 + ((g ^ cswz(v)) << 4));
+    }
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      bf16x8 bx[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bx[j] = kw == 1 ? cx[j] : kw == 0 ? shift_m1(cx[j], j > 0 ? &cx[j - 1] : nullptr)
+                                          : shift_p1(cx[j], j < 3 ? &cx[j + 1] : nullptr);
+      const int t = kh * 3 + kw;
+      if (fP) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) aP[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][i], bx[j], aP[i][j], 0, 0, 0);
+      }
+      if (fM) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            aM[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[9 + t][i], bx[j], aM[i][j], 0, 0, 0);
+      }
+      if (fN) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            aN[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[18 + t][i], bx[j], aN[i][j], 0, 0, 0);
+      }
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory"); }
+
+constexpr int C3R_RES = C3_TH * C3_ROWB;   // residual rows of one output slice (16 KB)
+__global__ void __launch_bounds__(256, 1) conv3d_c32_fwd_dr(C3Args a) {
+  // [2 input slices][2 residual slices][bias]
+  __shared__ __attribute__((aligned(1024))) char smem[C3R_NS * C3_SLOT + 2 * C3R_RES + 128];
+  float* const sbias = reinterpret_cast<float*>(smem + C3R_NS * C3_SLOT + 2 * C3R_RES);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int row = wave;
+  const int nht = a.H / C3_TH;
+  int b = blockIdx.x;
+  const int dc = b % a.ndc;
+  b /= a.ndc;
+  const int ht = b % nht, n = b / nht;
+  const int h0 = ht * C3_TH, d0 = dc * a.dchunk, d1 = d0 + a.dchunk;
+  const int li = lane & 15, g = lane >> 4;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.res ? a.res : a.x), 0, (int)a.xbytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds3_t)smem);
+  // input depth di (-1 .. D) -> slot (di + 1) & 1; pieces as conv3d_c32_fwd
+  auto issue = [&](int di) {
+    const unsigned lb = sbase + ((di + 1) & 1) * C3_SLOT;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int q = wave + 4 * j;
+      const int r = q >> 2, vv = 16 * (q & 3) + (lane >> 2);
+      const int c = (lane & 3) ^ cswz(vv);
+      const int h = h0 - 1 + r;
+      const bool ok = di >= 0 && di < a.D && h >= 0 && h < a.H;
+      const unsigned off = ok ? (unsigned)((((((n * a.D + di) * a.H + h) << 6) + vv) << 5) + c * 8) * 2u : 0x80000000u;
+      dma16s3(xr, lb + q * 1024, off);
+    }
+  };
+  // the wave's residual row of output d -> residual slot d & 1 (4 pieces, plain [voxel][64 B])
+  auto issue_res = [&](int d) {
+    const unsigned lb = sbase + C3R_NS * C3_SLOT + (d & 1) * C3R_RES + row * C3_ROWB;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int vv = 16 * p + (lane >> 2);
+      const unsigned off = (unsigned)((((((n * a.D + d) * a.H + h0 + row) << 6) + vv) << 5) + (lane & 3) * 8) * 2u;
+      dma16s3(rr, lb + p * 1024, off);
+    }
+  };
+
+  bf16x8 wf[27][2];
+#pragma unroll
+  for (int t = 0; t < 27; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      wf[t][i] = *reinterpret_cast<const bf16x8*>(a.w + ((t * 32 + 16 * i + li) * 32 + 8 * g));
+  if (tid < 32) sbias[tid] = a.bias ? a.bias[tid] : 0.f;
+  float ss[2][4], sq[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ss[i][k] = sq[i][k] = 0.f;
+
+  // output d: bias, residual (from LDS), bf16 store (8 global stores per lane, the only vector
+  // memory operations besides the DMA in the walk: step waits count them), BN partials; the set
+  // is zeroed for reuse
+  auto epilogue = [&](f32x4 (&acc)[2][4], int d) {
+    const long rowv = ((long)(n * a.D + d) * a.H + h0 + row) << 6;
+    const char* rb = smem + C3R_NS * C3_SLOT + (d & 1) * C3R_RES + row * C3_ROWB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float4 bv = *reinterpret_cast<const float4*>(sbias + 16 * i + 4 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long e = ((rowv + 16 * j + li) << 5) + 16 * i + 4 * g;
+        float o[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+        if (a.res) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(rb + (16 * j + li) * 64 + (16 * i + 4 * g) * 2);
+          o[0] += __uint_as_float(rv.x << 16);
+          o[1] += __uint_as_float(rv.x & 0xffff0000u);
+          o[2] += __uint_as_float(rv.y << 16);
+          o[3] += __uint_as_float(rv.y & 0xffff0000u);
+        }
+        bf16 t4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          t4[k] = (bf16)o[k];
+          const float r = (float)t4[k];
+          ss[i][k] += r;
+          sq[i][k] += r * r;
+        }
+        *reinterpret_cast<uint2*>(a.y + e) = *reinterpret_cast<const uint2*>(t4);
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  f32x4 A[2][4], B[2][4], C[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) A[i][j] = B[i][j] = C[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one input slice s: N = output s - 1 (kd = 2), M = output s (kd = 1), P = output s + 1 (kd = 0);
+  // F bits: 4 N (epilogue), 2 M, 1 P, 8 the previous step ran an epilogue (its 8 stores are
+  // the operations issued after this slice's DMA, so the wait lets them pend).  The flags are
+  // compile-time (the walk's first and last three slices are peeled), so the rotating
+  // accumulator sets never meet at a run-time merge.  Slices outside the volume are zero-filled
+  // by the DMA, so their MFMAs add nothing.  The barrier carries no memory fence: the only
+  // cross-wave data is DMA-written LDS, covered by each wave's own vmcnt wait.
+  auto step = [&](auto fl, int s, f32x4 (&aN)[2][4], f32x4 (&aM)[2][4], f32x4 (&aP)[2][4]) {
+    constexpr int F = decltype(fl)::value;
+    if constexpr ((F & 8) != 0) vm_wait<8>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (s + 1 <= d1) issue(s + 1);
+    if (a.res && s >= d0 && s < d1) issue_res(s);
+    const char* sb = smem + ((s + 1) & 1) * C3_SLOT;
+    c3r_slice<(F & 4) != 0, (F & 2) != 0, (F & 1) != 0>(sb, row, lane, wf, aN, aM, aP);
+    if constexpr ((F & 4) != 0) epilogue(aN, s - 1);
+  };
+  using f001 = std::integral_constant<int, 1>;
+  using f011 = std::integral_constant<int, 3>;
+  using f111 = std::integral_constant<int, 7>;
+  using f111e = std::integral_constant<int, 15>;
+  using f110e = std::integral_constant<int, 14>;
+  using f100e = std::integral_constant<int, 12>;
+  // dchunk + 2 slices, a multiple of 3 and >= 6 (host)
+  issue(d0 - 1);
+  __syncthreads();   // sbias
+  step(f001{}, d0 - 1, A, B, C);
+  step(f011{}, d0, B, C, A);
+  step(f111{}, d0 + 1, C, A, B);
+  for (int s = d0 + 2; s < d1 - 2; s += 3) {
+    step(f111e{}, s, A, B, C);
+    step(f111e{}, s + 1, B, C, A);
+    step(f111e{}, s + 2, C, A, B);
+  }
+  step(f111e{}, d1 - 2, A, B, C);
+  step(f110e{}, d1 - 1, B, C, A);
+  step(f100e{}, d1, C, A, B);
+  if (a.stats) {
+    const long rec = (long)blockIdx.x * C3_TH + row;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float S = row16_sum(ss[i][k]), Q = row16_sum(sq[i][k]);
+        if (li == 0) {
+          a.stats[(rec * 2) * 32 + 16 * i + 4 * g + k] = S;
+          a.stats[(rec * 2 + 1) * 32 + 16 * i + 4 * g + k] = Q;
         }
       }
   }
@@ -605,8 +822,19 @@ int check3(const fv_conv3d_desc* d) {
   return FV_OK;
 }
 
-// depth chunks per block for the forward kernel: enough blocks to cover the CUs twice
+// conv3d_c32_fwd_dr walks dchunk + 2 input slices in peeled groups of three
+bool c3r_chunk_ok(int dchunk) { return dchunk >= 4 && (dchunk + 2) % 3 == 0; }
+// depth chunks per block for the forward kernels.  conv3d_c32_fwd_dr (one block per CU): the
+// fewest chunks whose grid covers the 256 CUs, among the chunk lengths it walks, else the most;
+// conv3d_c32_fwd when no chunk length fits: enough blocks to cover the CUs twice
 int c3_ndc(const fv_conv3d_desc* d) {
+  int best = 0;
+  for (int k = 1; k <= d->d; k *= 2) {
+    if (d->d % k || !c3r_chunk_ok(d->d / k)) continue;
+    best = k;
+    if ((long)d->n * (d->h / C3_TH) * k >= 256) break;
+  }
+  if (best) return best;
   int ndc = 1;
   while ((long)d->n * (d->h / C3_TH) * ndc < 512 && d->d % (2 * ndc) == 0 && d->d / (2 * ndc) >= 2) ndc *= 2;
   return ndc;
@@ -678,7 +906,8 @@ static int conv3d_run(const fv_conv3d_desc* d, int cin, int cout, const void* x,
     a.dchunk = d->d / a.ndc;
     a.xbytes = (unsigned)((long)d->n * d->d * d->h * 64 * 32 * 2);
     const int nblk = d->n * (d->h / C3_TH) * a.ndc;
-    hipLaunchKernelGGL((conv3d_c32_fwd<2>), dim3(nblk), dim3(256), 0, s, a);
+    if (c3r_chunk_ok(a.dchunk)) hipLaunchKernelGGL(conv3d_c32_fwd_dr, dim3(nblk), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv3d_c32_fwd<2>), dim3(nblk), dim3(256), 0, s, a);
     return fv_check_launch("conv3d_c32_fwd");
   }
   FV_REQUIRE(!stats, "conv3d: BN partials only on the fast path (query fv_conv3d_stats_blocks)");

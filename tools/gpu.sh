@@ -13,6 +13,7 @@
 #   cbab            alternating convbench runs of $VARIANTS (";"-separated "ENV=.. -- convbench args"
 #                   strings, e.g. "-- --lib face-vae_amd/csrc/build_ab/libfacevae_base.so;"), $REPS rounds
 #   convpmc         SQ stall-anatomy counter passes over tools/convbench.py ($CB_ARGS)
+#   c3pmc           SQ + FETCH/WRITE_SIZE counter passes over tools/conv3dbench.py ($C3_ARGS)
 #   configs         bench lines of the other BASELINE configs on one GPU (512x512 B=8; B=64 bf16 / fp8)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -109,6 +110,18 @@ step_convpmc() {
       python3 $C > $O/cpmc_p$i.log 2>&1) || { echo "pmc pass $i failed"; tail -5 $O/cpmc_p$i.log; return 1; }
   done
   python tools/pmc_sq.py $O/cpmc_p1 $O/cpmc_p2 | tee $O/convpmc.txt
+}
+
+step_c3pmc() {   # SQ + HBM counter passes over tools/conv3dbench.py ($C3_ARGS)
+  local C="$R/tools/conv3dbench.py --iters 5 ${C3_ARGS:---batch 32}" i=0 c
+  for c in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    (cd /tmp && timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $O/c3pmc_p$i -o run -- \
+      python3 $C > $O/c3pmc_p$i.log 2>&1) || { echo "pmc pass $i failed"; tail -5 $O/c3pmc_p$i.log; return 1; }
+  done
+  python tools/pmc_sq.py $O/c3pmc_p1 $O/c3pmc_p2 $O/c3pmc_p3 $O/c3pmc_p4 | tee $O/c3pmc.txt
 }
 
 step_configs() {
