@@ -108,6 +108,7 @@ _SIGS = {
     "fv_tr8_probe": (c_int, [P, P, P]),
     "fv_conv3d_wk_bytes": (c_size_t, [D3]),
     "fv_conv3d_weight_prep": (c_int, [D3, P, P, P, P]),
+    "fv_conv3d_weight_prep_multi": (c_int, [D3, c_int, P, P, P, P]),
     "fv_conv3d_stats_blocks": (c_int, [D3]),
     "fv_conv3d_stats_block_pixels": (c_int, [D3]),
     "fv_conv3d_fwd": (c_int, [D3, P, P, P, P, P, P, P]),
@@ -233,6 +234,9 @@ def load():
     return lib
 
 
+_SYNC_CALLS = os.environ.get("FV_SYNC_CALLS", "0") == "1"   # debugging: a fault names its entry
+
+
 def call(name, *args):
     """Call an fv_* entry; raise FaceVAELibError with fv_last_error() on failure."""
     lib = load()
@@ -240,6 +244,12 @@ def call(name, *args):
     if st != 0:
         msg = lib.fv_last_error().decode(errors="replace")
         raise FaceVAELibError(f"{name} failed ({st}): {msg}")
+    if _SYNC_CALLS:
+        import torch
+        try:
+            torch.cuda.synchronize()
+        except Exception as e:
+            raise FaceVAELibError(f"{name}: device error after this call: {e}") from e
     return st
 
 

@@ -3443,6 +3443,15 @@ FwdTile fwd_tile_v2(int rows_needed) {
   const V2Cfg c = kV2Cfg[v2_cfg(rows_needed)];
   return {c.bn, c.bm};
 }
+// rows of a prepared weight image (forward wk: cout; data-gradient wt: cin): a whole number
+// of co tiles of EVERY kernel that may read it -- the v1 tiles (fwd_tile) and the v2 tiles
+// (fwd_tile_v2) differ for 17..32 rows (32 vs 64), and the v2 kernels' weight DMA reads the
+// whole tile (found by a 1x1 32 -> 128 conv's data gradient reading 32 rows past its wt).
+int wrows(int rows_needed) {
+  const int b1 = fwd_tile(rows_needed).bn, b2 = fwd_tile_v2(rows_needed).bn;
+  const int b = b1 > b2 ? b1 : b2;
+  return fv_cdiv(rows_needed, b) * b;
+}
 
 // mode: 0 plain, 1 upsample folded (KS 3), 2 sub-pixel phases (KS 2)
 template <int KS, int WN, int WM, int RN, int RM, int BKS>
@@ -3830,8 +3839,7 @@ extern "C" {
 
 size_t fv_conv_wk_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
-  const FwdTile t = fwd_tile(d->cout);
-  const size_t rows = (size_t)fv_cdiv(d->cout, t.bn) * t.bn;
+  const size_t rows = (size_t)wrows(d->cout);
   if (use_c7n(d)) return 32 * 448;
   if (use_subpix(d)) return 4 * rows * kpad_of(2, d->cin);
   return rows * kpad_of(d->ksize, d->cin);
@@ -3840,8 +3848,7 @@ size_t fv_conv_wk_elems(const fv_conv_desc* d) {
 size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const int cin_t = pad_pow2_8(d->cout);
-  const FwdTile t = fwd_tile(d->cin);
-  const size_t rows = (size_t)fv_cdiv(d->cin, t.bn) * t.bn;
+  const size_t rows = (size_t)wrows(d->cin);
   if (use_dgrad_lowres(d)) return rows * 16 * cin_t;
   return rows * kpad_of(d->ksize, cin_t);
 }
@@ -3929,8 +3936,7 @@ static bool h3s_layout(const fv_conv_desc* fd) {
   return !use_c7n(fd) && !halo_tr(fd) && !use_subpix(fd) && !use_c64(fd) && halo3_bn(fd) != 0;
 }
 static int wk_rows(const fv_conv_desc* fd) {
-  const FwdTile t = fwd_tile(fd->cout);
-  return fv_cdiv(fd->cout, t.bn) * t.bn;
+  return wrows(fd->cout);
 }
 static int lay_of(const fv_conv_desc* fd) { return use_c74(fd) ? 2 : h3s_layout(fd) ? 1 : 0; }
 // ... for the forward weights (wk) and the data gradient's transposed weights (wt) of conv d
@@ -3953,11 +3959,10 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   const bool generic_wt = wt && !use_dgrad_lowres(d);
   if (generic_wk && generic_wt) {
     // the common case: forward and transposed layouts in one launch
-    const FwdTile tk = fwd_tile(d->cout), tt = fwd_tile(d->cin);
     const int cin_t = pad_pow2_8(d->cout);
-    WPrepJob j0{wk, fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_lay(smaj_wk(d), kpad_of(ks, d->cin)), fv_ilog2(d->cin),
+    WPrepJob j0{wk, wrows(d->cout), kpad_lay(smaj_wk(d), kpad_of(ks, d->cin)), fv_ilog2(d->cin),
                 ks * ks * d->cin, 0, 0, smaj_wk(d)};
-    WPrepJob j1{wt, fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_lay(smaj_wt(d), kpad_of(ks, cin_t)), fv_ilog2(cin_t),
+    WPrepJob j1{wt, wrows(d->cin), kpad_lay(smaj_wt(d), kpad_of(ks, cin_t)), fv_ilog2(cin_t),
                 ks * ks * cin_t, 1, 0, smaj_wt(d)};
     j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 4096);
     j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 4096);
@@ -3973,16 +3978,14 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     hipLaunchKernelGGL(weight_prep_c7n_kernel, dim3(56), dim3(256), 0, s, w_param, sigma, (bf16*)wk, d->cout);
     if ((st = fv_check_launch("weight_prep_c7n"))) return st;
   } else if (wk && use_subpix(d)) {
-    const FwdTile t = fwd_tile(d->cout);
-    const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_of(2, d->cin);
+    const int rows = wrows(d->cout), Kp = kpad_of(2, d->cin);
     const long tot = 4L * rows * Kp;
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     hipLaunchKernelGGL(weight_prep_subpix_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wk, rows, Kp,
                        d->cout, d->cin_valid, fv_ilog2(d->cin));
     if ((st = fv_check_launch("weight_prep_subpix"))) return st;
   } else if (wk) {
-    const FwdTile t = fwd_tile(d->cout);
-    const int rows = fv_cdiv(d->cout, t.bn) * t.bn, Kp = kpad_lay(smaj_wk(d), kpad_of(ks, d->cin));
+    const int rows = wrows(d->cout), Kp = kpad_lay(smaj_wk(d), kpad_of(ks, d->cin));
     const long tot = (long)rows * Kp;
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     if (d->dtype == FV_BF16)
@@ -3995,8 +3998,7 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   }
   if (wt && use_dgrad_lowres(d)) {
     const int cin_t = pad_pow2_8(d->cout);
-    const FwdTile t = fwd_tile(d->cin);
-    const int rows = fv_cdiv(d->cin, t.bn) * t.bn, Kp = 16 * cin_t;
+    const int rows = wrows(d->cin), Kp = 16 * cin_t;
     const long tot = (long)rows * Kp;
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     hipLaunchKernelGGL(weight_prep_s2_kernel<bf16>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wt, rows, Kp,
@@ -4004,8 +4006,7 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
     if ((st = fv_check_launch("weight_prep_s2"))) return st;
   } else if (wt) {
     const int cin_t = pad_pow2_8(d->cout);
-    const FwdTile t = fwd_tile(d->cin);
-    const int rows = fv_cdiv(d->cin, t.bn) * t.bn, Kp = kpad_lay(smaj_wt(d), kpad_of(ks, cin_t));
+    const int rows = wrows(d->cin), Kp = kpad_lay(smaj_wt(d), kpad_of(ks, cin_t));
     const long tot = (long)rows * Kp;
     const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
     if (d->dtype == FV_BF16)
@@ -4038,17 +4039,15 @@ int fv_conv_weight_prep_multi(int n, const fv_conv_desc* descs, const float* con
     FV_REQUIRE(fv_conv_weight_prep_batchable(d), "weight_prep_multi: conv %d needs a special layout", i);
     FV_REQUIRE(w_params[i] && wks[i], "weight_prep_multi: null pointer (conv %d)", i);
     const int ks = d->ksize;
-    const FwdTile tk = fwd_tile(d->cout);
-    WPrepMJob j0{w_params[i], sigmas[i], wks[i], fv_cdiv(d->cout, tk.bn) * tk.bn, kpad_lay(smaj_wk(d), kpad_of(ks, d->cin)),
+    WPrepMJob j0{w_params[i], sigmas[i], wks[i], wrows(d->cout), kpad_lay(smaj_wk(d), kpad_of(ks, d->cin)),
                  fv_ilog2(d->cin),
                  ks * ks * d->cin, 0, 0, d->cout, d->cin_valid, ks, 0, smaj_wk(d)};
     j0.nb = (int)std::min<long>(fv_cdiv((long)j0.rows * j0.Kpad, 256), 256);
     nb_total = std::max(nb_total, j0.nb);
     m.j[m.n++] = j0;
     if (wts[i]) {
-      const FwdTile tt = fwd_tile(d->cin);
       const int cin_t = pad_pow2_8(d->cout);
-      WPrepMJob j1{w_params[i], sigmas[i], wts[i], fv_cdiv(d->cin, tt.bn) * tt.bn, kpad_lay(smaj_wt(d), kpad_of(ks, cin_t)),
+      WPrepMJob j1{w_params[i], sigmas[i], wts[i], wrows(d->cin), kpad_lay(smaj_wt(d), kpad_of(ks, cin_t)),
                    fv_ilog2(cin_t),
                    ks * ks * cin_t, 1, 0, d->cout, d->cin_valid, ks, 0, smaj_wt(d)};
       j1.nb = (int)std::min<long>(fv_cdiv((long)j1.rows * j1.Kpad, 256), 256);
@@ -4150,7 +4149,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.Kpad = kpad_of(2, d->cin);
     a.nks = a.Kpad / BK2;
     a.ntn = fv_cdiv(d->cout, t2.bn);
-    a.wphase = fv_cdiv(d->cout, t.bn) * t.bn * a.Kpad;
+    a.wphase = wrows(d->cout) * a.Kpad;
     const int nblk2 = 4 * a.ntn * (a.P / t2.bm);
     const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
     st = launch_v2(a, 2, t2, 2, nblk2, (unsigned)xb, s);
@@ -4666,10 +4665,9 @@ int fv_convt_weight_prep(const fv_conv_desc* d, const float* w, int demod, float
     hipLaunchKernelGGL(convt_norm_kernel, dim3(d->cout), dim3(64), 0, s, w, d->cin_valid, d->cout, inv);
     if ((st = fv_check_launch("convt_norm"))) return st;
   }
-  const FwdTile tk = fwd_tile(d->cout), tt = fwd_tile(d->cin);
   const int cin_t = pad_pow2_8(d->cout);
-  const int rows = fv_cdiv(d->cout, tk.bn) * tk.bn, Kp = kpad_of(2, d->cin);
-  const int rows_t = fv_cdiv(d->cin, tt.bn) * tt.bn;
+  const int rows = wrows(d->cout), Kp = kpad_of(2, d->cin);
+  const int rows_t = wrows(d->cin);
   const long tot = (wk ? 4L * rows * Kp : 0) + (wt ? (long)rows_t * 16 * cin_t : 0);
   const int nb = (int)std::min<long>(fv_cdiv(tot, 256), 4096);
   hipLaunchKernelGGL(convt_weight_prep_kernel, dim3(nb), dim3(256), 0, s, w, demod ? inv : nullptr, gain, (bf16*)wk,

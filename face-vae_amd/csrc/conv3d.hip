@@ -746,6 +746,31 @@ __global__ void __launch_bounds__(256) weight_prep3d_kernel(const float* __restr
   out[dst] = Elt<T>::from_f(w[e]);
 }
 
+// every conv of a trunk (same shape) in one launch, both layouts: blockIdx.y = conv, the
+// pointer tables travel in the kernel arguments (nothing to stage for graph capture)
+constexpr int W3P_MAX = 16;
+struct W3PrepMulti {
+  const float* w[W3P_MAX];
+  void* wk[W3P_MAX];
+  void* wt[W3P_MAX];
+};
+template <typename T>
+__global__ void __launch_bounds__(256) weight_prep3d_multi(W3PrepMulti m, int Co, int Ci, int out_major) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= Co * Ci * 27) return;
+  const int c = blockIdx.y;
+  const int t = e % 27, ci = (e / 27) % Ci, co = e / (27 * Ci);
+  const T v = Elt<T>::from_f(m.w[c][e]);
+  if (m.wk[c]) {
+    const long dst = out_major ? ((long)t * Co + co) * Ci + ci : ((long)t * Ci + ci) * Co + co;
+    reinterpret_cast<T*>(m.wk[c])[dst] = v;
+  }
+  if (m.wt[c]) {   // flipped taps, in / out exchanged
+    const long dst = out_major ? ((long)(26 - t) * Ci + ci) * Co + co : ((long)(26 - t) * Co + co) * Ci + ci;
+    reinterpret_cast<T*>(m.wt[c])[dst] = v;
+  }
+}
+
 // depth split of the AFE mid_conv output: h [n][p][c * D + d] <-> x3 [n][d][p][c] (c = C)
 template <typename T>
 __global__ void __launch_bounds__(256) depth_split_kernel(const T* __restrict__ src, T* __restrict__ dst, int HW,
@@ -882,6 +907,28 @@ int fv_conv3d_weight_prep(const fv_conv3d_desc* d, const float* w, void* wk, voi
     if (fast) hipLaunchKernelGGL(weight_prep3d_kernel<bf16>, dim3(nb), dim3(256), 0, s, w, d->cout, d->cin, 1, 1, (bf16*)wt);
     else hipLaunchKernelGGL(weight_prep3d_kernel<float>, dim3(nb), dim3(256), 0, s, w, d->cout, d->cin, 1, 0, (float*)wt);
     if ((st = fv_check_launch("conv3d_weight_prep_t"))) return st;
+  }
+  return FV_OK;
+}
+
+int fv_conv3d_weight_prep_multi(const fv_conv3d_desc* d, int n, const float* const* w, void* const* wk,
+                                void* const* wt, void* stream) {
+  int st = check3(d);
+  if (st) return st;
+  FV_REQUIRE(n >= 0 && (n == 0 || (w && wk && wt)), "conv3d_weight_prep_multi: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const bool fast = c32_fast(d);
+  const int nb = fv_cdiv(27L * d->cin * d->cout, 256);
+  for (int c0 = 0; c0 < n; c0 += W3P_MAX) {
+    const int k = n - c0 < W3P_MAX ? n - c0 : W3P_MAX;
+    W3PrepMulti m{};
+    for (int c = 0; c < k; ++c) {
+      FV_REQUIRE(w[c0 + c], "conv3d_weight_prep_multi: null weight");
+      m.w[c] = w[c0 + c], m.wk[c] = wk[c0 + c], m.wt[c] = wt[c0 + c];
+    }
+    if (fast) hipLaunchKernelGGL(weight_prep3d_multi<bf16>, dim3(nb, k), dim3(256), 0, s, m, d->cout, d->cin, 1);
+    else hipLaunchKernelGGL(weight_prep3d_multi<float>, dim3(nb, k), dim3(256), 0, s, m, d->cout, d->cin, 0);
+    if ((st = fv_check_launch("conv3d_weight_prep_multi"))) return st;
   }
   return FV_OK;
 }

@@ -55,6 +55,13 @@ class AFE(_Block):
         _batched_weight_prep(self, x.device)
         h = self.forward_2d(x)
         fs = ops3d.depth_split(h, self.C, self.D, self.compute_dtype())
+        if len(self.res):
+            wb = self.__dict__.get("_w3b")
+            if wb is None:
+                wb = ops3d.W3PrepBatch([c for blk in self.res for c in (blk.conv1, blk.conv2)])
+                object.__setattr__(self, "_w3b", wb)
+            N, C, D, H, W = fs.shape
+            wb.prep(ops3d.desc3(ops.storage(self.compute_dtype()), N, D, H, W, C, C), x.device)
         return self.res(fs)
 
 

@@ -48,14 +48,24 @@ def desc3(dtype, n, d, h, w, cin, cout):
     return L.Conv3dDesc(L.dtype_code(dtype), n, d, h, w, cin, cout)
 
 
+def _dkey(d):
+    return (d.dtype, d.n, d.d, d.h, d.w, d.cin, d.cout)
+
+
 class Conv3dState:
-    """Per-forward prepared weights of one Conv3d (wk forward, wt data gradient)."""
+    """Per-forward prepared weights of one Conv3d (wk forward, wt data gradient): the ones a
+    W3PrepBatch made for this forward when they match (shape and weight version), else one
+    fv_conv3d_weight_prep of its own."""
 
     def __init__(self, conv, d, device, need_wt):
         w = conv.weight
         if w.dtype != F32 or not w.is_contiguous():
             raise RuntimeError("conv3d weights must be contiguous fp32")
         self.conv, self.d, self.w = conv, d, w
+        pre = conv.__dict__.get("_c3prep")
+        if pre is not None and pre[0] == _dkey(d) and pre[1] == w._version and pre[2] is w:
+            self.wk, self.wt = pre[3], pre[4]
+            return
         nbytes = query("fv_conv3d_wk_bytes", ctypes.byref(d))
         if nbytes == 0:
             raise RuntimeError(f"conv3d: unsupported shape cin={d.cin} cout={d.cout}")
@@ -65,6 +75,38 @@ class Conv3dState:
 
     def release(self):
         self.wk = None
+
+
+class W3PrepBatch:
+    """fv_conv3d_weight_prep_multi: the forward and data-gradient weight layouts of every conv of
+    a 3-D trunk in one launch per forward (the per-conv path launched 2 per conv: 24 per AFE
+    step).  Buffers persist per shape (stable addresses for graph replay); each conv finds its
+    pair through `_c3prep`, checked against the shape and the weight's version."""
+
+    def __init__(self, convs):
+        self.convs = list(convs)
+        self.bufs = {}
+
+    def prep(self, d, device):
+        if not self.convs:
+            return
+        k = _dkey(d)
+        if k not in self.bufs:
+            nbytes = query("fv_conv3d_wk_bytes", ctypes.byref(d))
+            if nbytes == 0:
+                return
+            self.bufs = {k: [(torch.empty(nbytes, dtype=torch.uint8, device=device),
+                              torch.empty(nbytes, dtype=torch.uint8, device=device)) for _ in self.convs]}
+        pairs = self.bufs[k]
+        n = len(self.convs)
+        ws = [c.weight for c in self.convs]
+        if any(w.dtype != F32 or not w.is_contiguous() or not w.is_cuda for w in ws):
+            return
+        P = ctypes.c_void_p * n
+        call("fv_conv3d_weight_prep_multi", ctypes.byref(d), n, P(*[w.data_ptr() for w in ws]),
+             P(*[a.data_ptr() for a, _ in pairs]), P(*[b.data_ptr() for _, b in pairs]), stream())
+        for c, w, (a, b) in zip(self.convs, ws, pairs):
+            c.__dict__["_c3prep"] = (k, w._version, w, a, b)
 
 
 def conv3d_forward(cs: Conv3dState, x, bias, res=None, stats=False):

@@ -278,6 +278,10 @@ typedef struct fv_conv3d_desc {
 } fv_conv3d_desc;
 size_t fv_conv3d_wk_bytes(const fv_conv3d_desc* d);
 int fv_conv3d_weight_prep(const fv_conv3d_desc* d, const float* w_param, void* wk, void* wt, void* stream);
+/* fv_conv3d_weight_prep of n convs of one shape in one launch (host pointer tables; wk[i] / wt[i]
+ * may be NULL) */
+int fv_conv3d_weight_prep_multi(const fv_conv3d_desc* d, int n, const float* const* w_param, void* const* wk,
+                                void* const* wt, void* stream);
 /* BN partial records ([records][2][cout] (sum, sum of squares), block_pixels voxels each) that
  * fv_conv3d_fwd writes when stats != NULL; 0 = not available for this shape */
 int fv_conv3d_stats_blocks(const fv_conv3d_desc* d);

@@ -171,6 +171,36 @@ def test_afe3d_fp32_matches_reference():
         assert rel(p.grad, gd["grads"][k]) < 1e-3, k
 
 
+@pytest.mark.parametrize("mode", [torch.float32, torch.bfloat16])
+def test_afe_batched_conv3d_weight_prep_is_identical(mode, monkeypatch):
+    """AFE.forward prepares every ResBlock3D conv's weight layouts in one launch
+    (W3PrepBatch); the output and every gradient equal the per-conv preparation bit for bit
+    (bf16 at W = 64: the MFMA layouts; fp32: the direct kernels' layouts)."""
+    torch.manual_seed(3)
+    afe = fv.AFE(False, [16, 32], n_res=2, C=32, D=4).cuda().train().set_compute_dtype(mode)
+    x = torch.rand(1, 3, 128, 128, device="cuda")     # 3-D trunk [1, 32, 4, 64, 64]
+
+    def run():
+        for p in afe.parameters():
+            p.grad = None
+        y = afe(x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        torch.cuda.synchronize()
+        return y.detach().clone(), {k: p.grad.clone() for k, p in afe.named_parameters() if p.grad is not None}
+
+    sd = {k: v.clone() for k, v in afe.state_dict().items()}
+    y1, g1 = run()
+    assert afe.__dict__["_w3b"].bufs, "the batched preparation did not run"
+    afe.load_state_dict(sd)
+    monkeypatch.setattr(ops3d.W3PrepBatch, "prep", lambda self, d, device: None)
+    for c in afe.modules():
+        c.__dict__.pop("_c3prep", None)
+    y2, g2 = run()
+    assert torch.equal(y1, y2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+
+
 def test_resblock3d_bf16_full_shape_vs_oracle():
     """One ResBlock3D at the AFE trunk's real shape (C=32, D=16, 64x64; one image) on the MFMA
     kernels against the fp32 CPU oracle on the same weights and input."""

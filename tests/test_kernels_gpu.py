@@ -56,6 +56,11 @@ CONV_CASES = [
     (3, 128, 64, 10, 6, True, False),
     (7, 64, 3, 9, 13, False, False),
     (1, 512, 256, 6, 10, False, False),
+    # 17..32 output rows on the v2 path (64-row co tile over a weight image of 32 rows before
+    # wrows): a 1x1 128 -> 32 forward, the data gradient of 32 -> 128, a 3x3 with 24 outputs
+    (1, 128, 32, 8, 64, False, False),
+    (1, 32, 128, 16, 64, False, False),
+    (3, 64, 24, 8, 16, False, False),
     # 7x7 halo path (bf16, W % 64 == 0): in_conv shape, out_conv shape (+ its dgrad)
     (7, 3, 64, 16, 64, False, False),
     (7, 64, 3, 8, 128, False, False),
