@@ -559,6 +559,37 @@ __global__ void __launch_bounds__(512, 1) conv3d_c32_wgrad(C3WArgs a) {
     tkw[m] = t % 3;
   }
 
+  // Transposed-read addresses, hoisted: a fragment's rows start at a multiple of 16 plus the
+  // tap's kw (x image rows are 80 voxels, a multiple of 16), so the half-swap swizzle of
+  // tim_off is fixed per (lane, tap, column half, 4-row half) -- those lane constants are made
+  // once, the slot base joins them once per depth step, and the k step's row offset is an
+  // immediate (the k loop is unrolled).  The same reads as tfrag32: bit-identical.
+  const int li0 = lane & 15, g0 = lane >> 4;
+  auto lconst = [&](int rowl, int col) {
+    return rowl * 64 + ((((col >> 4) ^ ((rowl >> 3) & 1)) << 5) | ((col & 15) << 1));
+  };
+  unsigned lcx[4][2][2], lcd[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int rl = 8 * g0 + (li0 >> 2) + 4 * h;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = 16 * c + 4 * (li0 & 3);
+      lcd[c][h] = (unsigned)lconst(rl, col);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) lcx[m][c][h] = (unsigned)(lconst(tkw[m] + rl, col) + tkh[m] * W3_XROW * 64);
+    }
+  }
+  auto trd = [](unsigned addr) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(size_t)addr);
+  };
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  auto frag = [&](unsigned a0, unsigned a1) {
+    const s16x4 t0 = trd(a0), t1 = trd(a1);
+    const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
   for (int n = n0; n < n1 && d0 < d1; ++n) {
     issue_x(n, d0 - 1);
     issue_x(n, d0);
@@ -569,13 +600,23 @@ __global__ void __launch_bounds__(512, 1) conv3d_c32_wgrad(C3WArgs a) {
       __syncthreads();
       if (d + 2 <= d1) issue_x(n, d + 2);
       if (d + 1 < d1) issue_dy(n, d + 1);
-      const char* db = smem + W3_NX * W3_XSLOT + (d & 1) * W3_DSLOT;
-#pragma unroll 1
+      unsigned xa[4][2][2], da[2][2];
+      const unsigned dslot = dbase + (d & 1) * W3_DSLOT;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          da[c][h] = dslot + lcd[c][h];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) xa[m][c][h] = sbase + ((d + tkd[m]) & 3) * W3_XSLOT + lcx[m][c][h];
+        }
+#pragma unroll
       for (int ks = 0; ks < W3_TH * 2; ++ks) {      // 32-voxel k steps: row rr, half sg
         const int rr = ks >> 1, sg = ks & 1;
+        const unsigned od = (unsigned)((rr * 64 + 32 * sg) * 64), ox = (unsigned)((rr * W3_XROW + 32 * sg) * 64);
         bf16x8 af[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = tfrag32(db, rr * 64 + 32 * sg, 16 * i, lane);
+        for (int i = 0; i < 2; ++i) af[i] = frag(da[i][0] + od, da[i][1] + od);
         if (do_bias) {
 #pragma unroll
           for (int i = 0; i < 2; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i], 0, 0, 0);
@@ -583,11 +624,9 @@ __global__ void __launch_bounds__(512, 1) conv3d_c32_wgrad(C3WArgs a) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           if (m < 3 || ntap == 4) {
-            const char* xb = smem + ((d + tkd[m]) & 3) * W3_XSLOT;
-            const int R0 = (rr + tkh[m]) * W3_XROW + 32 * sg + tkw[m];
             bf16x8 bx[2];
 #pragma unroll
-            for (int c = 0; c < 2; ++c) bx[c] = tfrag32(xb, R0, 16 * c, lane);
+            for (int c = 0; c < 2; ++c) bx[c] = frag(xa[m][c][0] + ox, xa[m][c][1] + ox);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
