@@ -2670,6 +2670,30 @@ conv3_halo_wgrad2(H3Wg2Args a) {
     bf16x8 ones;
 #pragma unroll
     for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+    // transposed-read lane constants, hoisted out of the row loop: both images' swizzles have
+    // a 16-row period and every fragment starts at kk * 32 (+ the tap column for x), so a
+    // read's address is slot base + lane constant (per fragment and 4-row half) + an immediate
+    // (the same addresses as tfrag: bit-identical)
+    unsigned lcd[4][2], lcx[9][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rl = 8 * g + 4 * h + (li >> 2);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lcd[q][h] = (unsigned)timg_off<BC>(rl, wc * 64 + q * 16 + 4 * (li & 3));
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int kt = 9 * WK + j, tap = kt >> 2;
+        lcx[j][h] = (unsigned)timg_off<64>(tap % 3 + rl, (kt & 3) * 16 + 4 * (li & 3));
+      }
+    }
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    auto frag2 = [](const char* base, unsigned l0, unsigned l1, int off) {
+      FV_LDS char* lb = (FV_LDS char*)(base) + off;
+      const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + l0));
+      const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + l1));
+      const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+      return __builtin_bit_cast(bf16x8, v);
+    };
     for (int i = 0; i < nrow; ++i) {
       // group i landed; the younger groups issued so far (up to AHEAD - 1) may stay in flight
       const int younger = min(AHEAD - 1, nrow - 1 - i);
@@ -2687,12 +2711,12 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       for (int kk = 0; kk < 2; ++kk) {
         bf16x8 af[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) af[q] = tfrag<BC>(dys, kk * 32, wc * 64 + q * 16, lane);
+        for (int q = 0; q < 4; ++q) af[q] = frag2(dys, lcd[q][0], lcd[q][1], kk * 32 * BC * 2);
         // x fragment of k-tile j (tap row / column constant after unrolling); the next one is
         // read before the current one's 4 MFMAs so the LDS latency hides under them
         auto xfrag = [&](int j) {
           const int kt = 9 * WK + j, tap = kt >> 2;
-          return tfrag<64>(xrow[tap / 3], kk * 32 + tap % 3, (kt & 3) * 16, lane);
+          return frag2(xrow[tap / 3], lcx[j][0], lcx[j][1], kk * 32 * 128);
         };
         bf16x8 bcur = xfrag(0);
         __builtin_amdgcn_s_setprio(1);
