@@ -7,6 +7,8 @@
 //              unbiased variance) -> torch/nn/modules/_functions.py:10-125 semantics.
 //   act fwd  : out = [avgpool2](act(y*scale + shift))  (CNA + DownBlock2D's AvgPool2d).
 //   bwd      : g = dout * act'(.)  ->  sums (g, g*yhat)  ->  dx = gamma*invstd*(g - k0 - yhat*k1)
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -209,6 +211,9 @@ __global__ void __launch_bounds__(FOLDB) fold_part_kernel(FoldArgs a, double* pa
   }
 }
 
+template <int NV, int MODE>
+__device__ __forceinline__ void fold_finish(const FoldArgs& a, int c, const double* tot);
+
 // <= FOLD2 records (and level 2): one channel per block of 1024 threads, rows t, t + 1024, ...
 template <typename T, int NV, int MODE>
 __global__ void __launch_bounds__(FOLDT) fold1_kernel(FoldArgs a) {
@@ -239,6 +244,96 @@ __global__ void __launch_bounds__(FOLDT) fold1_kernel(FoldArgs a) {
     for (int j = 0; j < FOLDT / 64; ++j) t += red[v][j];
     tot[v] = t;
   }
+  fold_finish<NV, MODE>(a, c, tot);
+}
+
+// <= FOLD2 records, C % 16 == 0: one block per 16 channels, so every row is read as whole 64-B
+// (fp32) / 128-B (fp64) channel segments -- fold1 reads 4 B per sector of each row (r4: 13 us
+// for the 2048-record, 256-channel res-conv folds).  Lane l of a wave: channel l & 15 of row
+// (l >> 4) + 4 w + 64 i; fixed reduction order (xor tree over the 4 row lanes, waves in order).
+template <typename T, int NV, int MODE>
+__global__ void __launch_bounds__(FOLDT) fold16_kernel(FoldArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c0 = blockIdx.x * 16, cl = lane & 15;
+  const T* src = reinterpret_cast<const T*>(a.src) + c0 + cl;
+  const long vs = a.C;
+  double acc[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) acc[v] = 0.0;
+#pragma unroll 4
+  for (int r = (lane >> 4) + 4 * w; r < a.nrec; r += FOLDT / 16) {
+    const T* p = src + (long)r * a.rstride;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) acc[v] += (double)p[v * vs];
+  }
+  __shared__ double red[FOLDT / 64][NV][16];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double t = acc[v];
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    if (lane < 16) red[w][v][lane] = t;
+  }
+  __syncthreads();
+  if (tid >= 16) return;
+  double tot[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double t = 0.0;
+    for (int j = 0; j < FOLDT / 64; ++j) t += red[j][v][tid];
+    tot[v] = t;
+  }
+  fold_finish<NV, MODE>(a, c0 + tid, tot);
+}
+
+// level 1 of a fold of fp32 records with scratch: block (16-channel group, chunk of `rows`
+// records) -> part [chunk][NV][C] (fp64).  4 lanes per record row (16 B each: a whole 64-B
+// channel segment per row), 16 rows per wave load, every load of the chunk in flight at once
+// (the one-launch fold16 over 16-64 blocks was latency-bound: 16 us for 2048 records).
+template <int NV>
+__global__ void __launch_bounds__(256) fold16_part_kernel(FoldArgs a, int rows, double* part) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c0 = blockIdx.x * 16, ch = blockIdx.y, q = lane & 3;
+  const int r0 = ch * rows, r1 = min(a.nrec, r0 + rows);
+  const float* src = reinterpret_cast<const float*>(a.src) + c0 + 4 * q;
+  double acc[NV][4];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[v][k] = 0.0;
+#pragma unroll 4
+  for (int r = r0 + (lane >> 2) + 16 * w; r < r1; r += 64) {
+    const float* p = src + (long)r * a.rstride;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const float4 f = *reinterpret_cast<const float4*>(p + (long)v * a.C);
+      acc[v][0] += f.x; acc[v][1] += f.y; acc[v][2] += f.z; acc[v][3] += f.w;
+    }
+  }
+  // lanes with the same q hold the same 4 channels: xor over the 16 row lanes of the wave
+  __shared__ double red[4][NV][16];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double t = acc[v][k];
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+      if (lane < 4) red[w][v][4 * lane + k] = t;
+    }
+  __syncthreads();
+  if (tid >= 16) return;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    double t = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t += red[j][v][tid];
+    part[((long)ch * NV + v) * a.C + c0 + tid] = t;
+  }
+}
+
+template <int NV, int MODE>
+__device__ __forceinline__ void fold_finish(const FoldArgs& a, int c, const double* tot) {
   // (n, S, Q): rows with a count row carry it first; fp32 records are counted by P
   const double n = NV == 3 ? tot[0] : (double)a.P;
   const double S = tot[NV - 2], Q = tot[NV - 1];
@@ -265,14 +360,32 @@ __global__ void __launch_bounds__(FOLDT) fold1_kernel(FoldArgs a) {
   }
 }
 
-// scratch: room for ceil(nrec / FOLDR) x NV x C doubles when nrec > FOLD2 (the records then
-// fold in two launches: chunk partials, then the partial rows)
+// scratch: room for max(ceil(nrec / FOLDR), ceil(256 / (C / 16)) + 1) x NV x C doubles (fp32
+// records and rows beyond FOLD2 fold in two launches: chunk partials, then the partial rows)
 template <typename T, int NV, int MODE>
 int launch_fold(const FoldArgs& a, hipStream_t s, const char* what, double* scratch = nullptr) {
   FV_REQUIRE(a.C % 8 == 0 && a.nrec > 0, "BN fold: channels must be a multiple of 8 (%d)", a.C);
   const int nch = (a.nrec + FOLDR - 1) / FOLDR;
+  if (sizeof(T) == 4 && scratch && (const void*)scratch != a.src && a.C % 16 == 0 && a.rstride % 4 == 0 &&
+      a.nrec >= 256) {
+    // fp32 records: two levels over 16-channel segments, enough (group, chunk) blocks to cover
+    // the CUs (r4: res-conv folds 13.1 -> 5.4 + 5.1 us, step 12.55 -> 12.48 ms)
+    const int ng = a.C / 16;
+    int nch = (256 + ng - 1) / ng;
+    if (nch > a.nrec / 64) nch = a.nrec / 64;
+    const int rows = (a.nrec + nch - 1) / nch;
+    nch = (a.nrec + rows - 1) / rows;
+    hipLaunchKernelGGL((fold16_part_kernel<NV>), dim3(ng, nch), dim3(256), 0, s, a, rows, scratch);
+    FoldArgs b = a;
+    b.src = scratch;
+    b.nrec = nch;
+    b.rstride = (long)NV * a.C;
+    hipLaunchKernelGGL((fold1_kernel<double, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, b);
+    return fv_check_launch(what);
+  }
   if (a.nrec <= FOLD2) {
-    hipLaunchKernelGGL((fold1_kernel<T, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, a);
+    if (a.C % 16 == 0) hipLaunchKernelGGL((fold16_kernel<T, NV, MODE>), dim3(a.C / 16), dim3(FOLDT), 0, s, a);
+    else hipLaunchKernelGGL((fold1_kernel<T, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, a);
     return fv_check_launch(what);
   }
   FV_REQUIRE(scratch && (const void*)scratch != a.src, "BN fold of %d records: no scratch", a.nrec);
