@@ -318,6 +318,7 @@ template <int K>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory"); }
 
 constexpr int C3R_RES = C3_TH * C3_ROWB;   // residual rows of one output slice (16 KB)
+template <bool STATS, bool RES>
 __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd_dr(C3Args a) {
   // [2 input slices][2 residual slices][bias]
   __shared__ __attribute__((aligned(1024))) char smem[C3R_NS * C3_SLOT + 2 * C3R_RES + 128];
@@ -388,7 +389,7 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd_dr(C3Args a) {
       for (int j = 0; j < 4; ++j) {
         const long e = ((rowv + 16 * j + li) << 5) + 16 * i + 4 * g;
         float o[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
-        if (a.res) {
+        if constexpr (RES) {
           const uint2 rv = *reinterpret_cast<const uint2*>(rb + (16 * j + li) * 64 + (16 * i + 4 * g) * 2);
           o[0] += __uint_as_float(rv.x << 16);
           o[1] += __uint_as_float(rv.x & 0xffff0000u);
@@ -400,8 +401,10 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd_dr(C3Args a) {
         for (int k = 0; k < 4; ++k) {
           t4[k] = (bf16)o[k];
           const float r = (float)t4[k];
-          ss[i][k] += r;
-          sq[i][k] += r * r;
+          if constexpr (STATS) {
+            ss[i][k] += r;
+            sq[i][k] += r * r;
+          }
         }
         *reinterpret_cast<uint2*>(a.y + e) = *reinterpret_cast<const uint2*>(t4);
         acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -428,7 +431,7 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd_dr(C3Args a) {
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
     if (s + 1 <= d1) issue(s + 1);
-    if (a.res && s >= d0 && s < d1) issue_res(s);
+    if (RES && s >= d0 && s < d1) issue_res(s);
     const char* sb = smem + ((s + 1) & 1) * C3_SLOT;
     c3r_slice<(F & 4) != 0, (F & 2) != 0, (F & 1) != 0>(sb, row, lane, wf, aN, aM, aP);
     if constexpr ((F & 4) != 0) epilogue(aN, s - 1);
@@ -453,7 +456,7 @@ __global__ void __launch_bounds__(256, 1) conv3d_c32_fwd_dr(C3Args a) {
   step(f111e{}, d1 - 2, A, B, C);
   step(f110e{}, d1 - 1, B, C, A);
   step(f100e{}, d1, C, A, B);
-  if (a.stats) {
+  if (STATS) {
     const long rec = (long)blockIdx.x * C3_TH + row;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -992,7 +995,14 @@ static int conv3d_run(const fv_conv3d_desc* d, int cin, int cout, const void* x,
     a.dchunk = d->d / a.ndc;
     a.xbytes = (unsigned)((long)d->n * d->d * d->h * 64 * 32 * 2);
     const int nblk = d->n * (d->h / C3_TH) * a.ndc;
-    if (c3r_chunk_ok(a.dchunk)) hipLaunchKernelGGL(conv3d_c32_fwd_dr, dim3(nblk), dim3(256), 0, s, a);
+    if (c3r_chunk_ok(a.dchunk)) {
+      // the BN-partials and residual epilogue terms as compile-time switches (the data gradient
+      // and the block's first conv skip their VALU / DMA)
+      if (a.stats && a.res) hipLaunchKernelGGL((conv3d_c32_fwd_dr<true, true>), dim3(nblk), dim3(256), 0, s, a);
+      else if (a.stats) hipLaunchKernelGGL((conv3d_c32_fwd_dr<true, false>), dim3(nblk), dim3(256), 0, s, a);
+      else if (a.res) hipLaunchKernelGGL((conv3d_c32_fwd_dr<false, true>), dim3(nblk), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((conv3d_c32_fwd_dr<false, false>), dim3(nblk), dim3(256), 0, s, a);
+    }
     else hipLaunchKernelGGL((conv3d_c32_fwd<2>), dim3(nblk), dim3(256), 0, s, a);
     return fv_check_launch("conv3d_c32_fwd");
   }

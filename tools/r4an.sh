@@ -1,0 +1,6 @@
+# round-4 session an: conv3d_c32_fwd_dr with compile-time BN-partials / residual epilogue -- parity, A/B vs the previous build
+cd "$GRAFT_REPO_ROOT"
+TESTS="tests/test_afe3d_gpu.py tests/test_warp_gpu.py" bash tools/gpu.sh test || exit 1
+BASE=$GRAFT_REPO_ROOT/face-vae_amd/csrc/build_ab/libfacevae_base.so
+for b in 32 8; do for r in 1 2; do for v in base new; do echo "B=$b $v"; if [ $v = base ]; then L=$BASE; else L=; fi; FV_LIB_PATH=$L timeout -k 10 200 python tools/conv3dbench.py --batch $b 2>/dev/null | tail -1 | grep -o '"fwd_ms": [0-9.]*\|"dgrad_ms": [0-9.]*\|"resblock3d_fwd_bwd_ms": [0-9.]*' | paste -sd' ' || exit 1; done; done; done
+for r in 1 2; do for v in base new; do echo "fbench $v"; if [ $v = base ]; then L=$BASE; else L=; fi; FV_LIB_PATH=$L timeout -k 10 300 python tools/fbench.py --batch 8 --steps 10 --warmup 3 2>/dev/null | tail -1 | cut -c100-160 || exit 1; done; done
