@@ -293,21 +293,27 @@ __global__ void __launch_bounds__(256) gs_gather_input(const GsRec* __restrict__
       const GsRec R = rec[r];
       const float w = (dx ? R.tx : 1.f - R.tx) * (dy ? R.ty : 1.f - R.ty) * (dz ? R.tz : 1.f - R.tz);
       const T* g = gout + (long)R.v * C + q * V;
-      if constexpr (V == 8) {
-        Chunk8<T> c;
-        c.load(g);
+      if constexpr (V % 8 == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += w * c.get(j);
+        for (int h = 0; h < V / 8; ++h) {
+          Chunk8<T> c;
+          c.load(g + 8 * h);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[8 * h + j] += w * c.get(j);
+        }
       } else {
         acc[0] += w * ld(g);
       }
     }
   }
   T* o = gin + cell * C + q * V;
-  if constexpr (V == 8) {
-    Chunk8<T> c;
-    c.set8(acc);
-    c.store(o);
+  if constexpr (V % 8 == 0) {
+#pragma unroll
+    for (int h = 0; h < V / 8; ++h) {
+      Chunk8<T> c;
+      c.set8(acc + 8 * h);
+      c.store(o + 8 * h);
+    }
   } else {
     o[0] = Elt<T>::from_f(acc[0]);
   }
@@ -646,10 +652,13 @@ int fv_grid_sample3d_bwd_input(int dtype, const float* grid, const void* gout, i
 #define GS_GATHER(T, V)                                                                                          \
   hipLaunchKernelGGL((gs_gather_input<T, V>), dim3(fv_cdiv(ncell * (C / V), 256)), dim3(256), 0, s, w.rec, w.cnt, \
                      w.bsum, (const T*)gout, ncell, Di, Hi, Wi, C, (T*)gin)
+  // C = 32 (the warp volume): one lane per cell, its record read once (r4: 4 lanes of 8
+  // channels each re-read every record)
+  // (88.0 -> 73.6 us at the fbench shape, tools/r4ao.sh)
   if (dtype == FV_BF16) {
-    if (C % 8 == 0) GS_GATHER(bf16, 8); else GS_GATHER(bf16, 1);
+    if (C == 32) GS_GATHER(bf16, 32); else if (C % 8 == 0) GS_GATHER(bf16, 8); else GS_GATHER(bf16, 1);
   } else {
-    if (C % 8 == 0) GS_GATHER(float, 8); else GS_GATHER(float, 1);
+    if (C == 32) GS_GATHER(float, 32); else if (C % 8 == 0) GS_GATHER(float, 8); else GS_GATHER(float, 1);
   }
 #undef GS_GATHER
   return fv_check_launch("grid_sample3d_bwd_input");
