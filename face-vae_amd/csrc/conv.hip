@@ -610,6 +610,17 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // The asm has NO outputs (M0 is declared clobbered): hipcc models an inline asm containing a
 // VMEM op as writing its outputs asynchronously and waits vmcnt(0) before such a register is
 // reused -- with an output, every DMA of a loop waited for the previous one.
+// lgkmcnt(0) as the s_waitcnt builtin, not inline asm: the compiler's wait-count pass sees it
+// and knows every LDS read issued before it has landed.  After an inline-asm wait the pass
+// still counts those reads as outstanding, and with more than 15 reads in flight (the 4-bit
+// lgkm counter) it waits for the NEWEST reads before the first use of an old fragment: in
+// the pair-of-taps loops every step's second MFMA cluster waited for the next tap's 12
+// fragment reads (lgkmcnt(7) .. (0) in front of its first 8 MFMAs).
+__device__ __forceinline__ void wait_lgkm0() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);       // vmcnt(63) expcnt(7) lgkmcnt(0)
+}
+
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff, unsigned soff) {
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
                :
@@ -804,7 +815,8 @@ conv_fwd_v2(ConvArgs a, unsigned x_bytes) {
       const int buf = ks & 1;
       load_frags(fa1, fb1, buf, 1);
       mfma_all(fa0, fb0);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wait_lgkm0();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (ks + 2 < nks) issue(ks + 2, buf);
@@ -1008,37 +1020,44 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   // No branch around the fragment reads: a read issued on one path only makes the compiler
   // drain ALL LDS reads (lgkmcnt(0)) before the next MFMA group, exposing the F1 read latency
   // every step.  An odd last tap re-reads a valid tap and skips its MFMAs.
-  for (int j = 0; j < nsteps; ++j) {
+  // The last step is peeled (its odd tap, if any, re-reads a valid tap and skips the MFMAs):
+  // inside the loop its path (no barrier, no next-tap reads) merged into the loop's second
+  // MFMA cluster and made the wait-count pass hold that cluster for the next tap's reads.
+  for (int j = 0; j + 1 < nsteps; ++j) {
+    load_frags(fa1, fb1, 2 * j + 1, bj);
+    mfma_all(fa0, fb0);
+    const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
+    // the weight stage is issued LAST in a step, so the count left in flight is that
+    // stage's alone (a halo issued before it is waited for one step later)
+    FV_DIAG_WAIT_BEGIN();
+    if constexpr (NSB == 2) wait_vm<0>();     // stage j + 1 was the one issued last
+    else if (pend == 2 * JB) wait_vm<2 * JB>();
+    else wait_vm_dyn(pend);
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    FV_DIAG_WAIT_END();
+    if (hn < nch && j == hstep) {
+      issue_halo(hn);
+      ++hn;
+      hstep = (9 * hn - 10) / 2;
+    }
+    pend = 0;
+    if (j + NSB < nsteps) {
+      issue_b(j + NSB, bj);
+      pend = bcnt(j + NSB);
+    }
+    load_frags(fa0, fb0, 2 * j + 2, bn1);
+    FV_DIAG_ISSUE_END();
+    mfma_all(fa1, fb1);
+    bj = bn1;
+  }
+  {
+    const int j = nsteps - 1;
     const bool two = 2 * j + 1 < ntap;
     load_frags(fa1, fb1, two ? 2 * j + 1 : 2 * j, bj);
     mfma_all(fa0, fb0);
-    const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
-    if (j + 1 < nsteps) {
-      // the weight stage is issued LAST in a step, so the count left in flight is that
-      // stage's alone (a halo issued before it is waited for one step later)
-      FV_DIAG_WAIT_BEGIN();
-      if constexpr (NSB == 2) wait_vm<0>();     // stage j + 1 was the one issued last
-      else if (pend == 2 * JB) wait_vm<2 * JB>();
-      else wait_vm_dyn(pend);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      FV_DIAG_WAIT_END();
-      if (hn < nch && j == hstep) {
-        issue_halo(hn);
-        ++hn;
-        hstep = (9 * hn - 10) / 2;
-      }
-      pend = 0;
-      if (j + NSB < nsteps) {
-        issue_b(j + NSB, bj);
-        pend = bcnt(j + NSB);
-      }
-      load_frags(fa0, fb0, 2 * j + 2, bn1);
-      FV_DIAG_ISSUE_END();
-    }
     if (two) mfma_all(fa1, fb1);
-    bj = bn1;
   }
   FV_DIAG_LOOP_END();
   __syncthreads();
@@ -1067,7 +1086,14 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
 // runs MFMAs), published by the following barrier, before its first fragment read (the first
 // read needs it published by barrier floor(9c / 2) - 1 (c even) / (9c - 3) / 2 (c odd), the
 // later half publishes at barrier 9c / 2 - 2 / (9c - 5) / 2).
-template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false>
+//
+// SCH (schedule of the two waves of a SIMD, waves w and w + NW / 2): bit 0 = one static
+// s_setprio 1 for waves NW/2 .. NW-1 before the main loop instead of prio flips around every
+// MFMA cluster; bit 1 = stagger: waves NW/2 .. NW-1 pass each step's barrier before the MFMAs
+// of the tap whose fragments they hold, so they run those MFMAs while their partners issue the
+// DMA and fragment reads after the barrier, and issue their own reads while the partners run
+// MFMAs (same arithmetic, same order per accumulator: bit-identical).
+template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, int SCH = 0>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
@@ -1194,13 +1220,15 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
 #pragma unroll
     for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < RN; ++i)
 #pragma unroll
       for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(0);
   };
+  const bool hi = wave >= NW / 2;                  // the second-dispatched wave of each SIMD
+  const bool stag = (SCH & 2) && hi;
 
   // the ring and halo schedule of conv3_halo_fwd2 (nch even: no odd last tap)
   Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
@@ -1227,42 +1255,61 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   int hn = 2, hstep = (9 * 2 - 10) / 2;
   int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
   int bj = 0;
-  for (int j = 0; j < nsteps; ++j) {
+  if constexpr (SCH & 1) {
+    if (hi) __builtin_amdgcn_s_setprio(1);
+  }
+  // barrier of step j: stage j + 1 landed (own DMAs counted, then the barrier publishes them),
+  // and every wave's reads of stage j are done (its buffer is re-filled right after)
+  auto step_barrier = [&]() {
+    FV_DIAG_WAIT_BEGIN();
+    if constexpr (NSB == 2) wait_vm<0>();
+    else if (pend == 2 * JB) wait_vm<2 * JB>();
+    else wait_vm_dyn(pend);
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    FV_DIAG_WAIT_END();
+  };
+  // stagger (SCH bit 1): waves NW/2.. take the barrier BEFORE the MFMAs of tap 2j (their
+  // fragments are in registers), the others after; every read still falls in the same barrier
+  // interval as in the lockstep order, so the ring / halo hazards are unchanged.
+  // The last step is peeled: with it inside the loop (no barrier, no next-tap reads) the
+  // wait-count pass merged its state into the loop's second MFMA cluster and made that
+  // cluster wait for the next tap's fragment reads every step (lgkmcnt(7) .. (0)).
+  for (int j = 0; j + 1 < nsteps; ++j) {
     load_frags(fa1, fb1, 2 * j + 1, bj);
+    if constexpr ((SCH & 2) != 0) {
+      if (stag) step_barrier();
+    }
     mfma_all(fa0, fb0);
     const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
-    if (j + 1 < nsteps) {
-      FV_DIAG_WAIT_BEGIN();
-      if constexpr (NSB == 2) wait_vm<0>();
-      else if (pend == 2 * JB) wait_vm<2 * JB>();
-      else wait_vm_dyn(pend);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      FV_DIAG_WAIT_END();
-      if (hn < nch && j == hstep) {
-        issue_halo(hn);
-        if constexpr (PRO) {
-          xc = hn;
-          xstep = j + 1 + (wave >= 4 ? 1 : 0);   // landed by the next step's barrier
-        }
-        ++hn;
-        hstep = (9 * hn - 10) / 2;
+    if (!stag) step_barrier();
+    if (hn < nch && j == hstep) {
+      issue_halo(hn);
+      if constexpr (PRO) {
+        xc = hn;
+        xstep = j + 1 + (wave >= 4 ? 1 : 0);   // landed by the next step's barrier
       }
-      pend = 0;
-      if (j + NSB < nsteps) {
-        issue_b(j + NSB, bj);
-        pend = bcnt(j + NSB);
-      }
-      load_frags(fa0, fb0, 2 * j + 2, bn1);
-      FV_DIAG_ISSUE_END();
+      ++hn;
+      hstep = (9 * hn - 10) / 2;
     }
+    pend = 0;
+    if (j + NSB < nsteps) {
+      issue_b(j + NSB, bj);
+      pend = bcnt(j + NSB);
+    }
+    load_frags(fa0, fb0, 2 * j + 2, bn1);
+    FV_DIAG_ISSUE_END();
     mfma_all(fa1, fb1);
     if constexpr (PRO) {
       if (j == xstep) xform(xc);     // published by the next step's barrier
     }
     bj = bn1;
   }
+  load_frags(fa1, fb1, 2 * nsteps - 1, bj);
+  mfma_all(fa0, fb0);
+  mfma_all(fa1, fb1);
+  if constexpr (SCH & 1) __builtin_amdgcn_s_setprio(0);
   FV_DIAG_LOOP_END();
   __syncthreads();
   conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
@@ -1581,7 +1628,8 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
     // tile's >= 4 stores, this tile's DMA (if any) and this tile's >= 4 stores, so vmcnt(8)
     // has it landed (in-order counting); the barrier publishes it to all waves and releases
     // this tile's buffer (raw barrier: __syncthreads() would also drain the stores)
-    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     buf = buf == 2 ? 0 : buf + 1;
@@ -1689,7 +1737,7 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
     // output stores (+ 2 record stores), which stay in flight
     if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const bool more = it + 1 < niter;
@@ -2450,7 +2498,7 @@ conv_wgrad_v2(Wg2Args a) {
     for (int it = 0; it < nst; ++it) {
       const int ahead = min(NS - 2, nst - 1 - it);
       wait_ahead<NS, PW>(ahead);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_lgkm0();
       __builtin_amdgcn_s_barrier();
       const bool more = it + NS - 1 < nst;
       const RowSt r = rowal_state(it + NS - 1, (it + NS - 1) % NS);
@@ -2464,7 +2512,7 @@ conv_wgrad_v2(Wg2Args a) {
     for (int it = 0; it < nst; ++it) {
       const int ahead = min(NS - 2, nst - 1 - it);   // younger stages allowed in flight
       wait_ahead<NS, PW>(ahead);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_lgkm0();
       __builtin_amdgcn_s_barrier();
       if (it + NS - 1 < nst) issue(it + NS - 1, (it + NS - 1) % NS);
       compute_h(it % NS, [](int) {});
@@ -2698,7 +2746,7 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       // group i landed; the younger groups issued so far (up to AHEAD - 1) may stay in flight
       const int younger = min(AHEAD - 1, nrow - 1 - i);
       wait_vm_dyn(younger * npw);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_lgkm0();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (i + AHEAD < nrow) issue_group(i + AHEAD);
@@ -3088,7 +3136,7 @@ conv_halo_wgrad(HaloWgArgs a) {
   if (tile < a.ntiles) issue(tile, 0);
   for (int it = 0; tile < a.ntiles; ++it, tile += gridDim.x) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     if (tile + (int)gridDim.x < a.ntiles) issue(tile + gridDim.x, (it + 1) & 1);
     compute(it & 1);
@@ -3545,6 +3593,17 @@ bool use_subpix(const fv_conv_desc* d) {
   if (fv_ilog2(hl) < 0 || fv_ilog2(wl) < 0 || wl % 16) return false;
   const long pl = (long)d->n * hl * wl;
   return pl % fwd_tile_v2(d->cout).bm == 0;
+}
+
+// SIMD-partner schedule of the halo 3x3 kernels (conv3_halo_fwd3 / conv3_halo_fp8 SCH):
+// FV_RES_SCHED = 0 (prio flips, lockstep), 1 (static prio for waves 4-7), 2 (stagger), 3
+// (both); unset: the measured default of each kernel (dflt).  Read per call (tests compare the
+// schedules bit for bit in one process).  r5, alternating convbench runs on one box, B=32 bf16
+// res fwd / dgrad: 0: 130 / 122, 1: 124 / 118, 2: 120 / 115, 3: 126 / 119 us; B=64 fp8 res
+// fwd / dgrad: 0: 175 / 166, 1: 173 / 163, 2: 172 / 155, 3: 165 / 155 us.
+static int res_sched(int dflt) {
+  const char* e = getenv("FV_RES_SCHED");
+  return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : dflt;
 }
 
 // data gradient of an upsample + 3x3 conv computed directly at the low resolution as a
@@ -4222,8 +4281,18 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
       FV_REQUIRE(bn == 256 && psc && psh, "staged BN prologue: bad arguments");
       hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn >= 128 && a.Cin % 64 == 0) {
-      if (bn == 256) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
-      else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
+      const int sch = res_sched(2);
+      if (bn == 256) {
+        if (sch == 1) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
+        else if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+        else if (sch == 3) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
+        else hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+      } else {
+        if (sch == 1) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
+        else if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
+        else if (sch == 3) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
+        else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
+      }
     } else if (bn == 256) {
       hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 128) {
@@ -4930,7 +4999,11 @@ __global__ void tr8_probe_kernel(const int* lane_addr, int* out) {
 // Block: BN = 128 co x BM = 256 px (4 rows x 64), 8 waves 2 (co) x 4 (px), wave 64 x 64.
 // NSW: weight stages in the ring, issued NSW - 1 taps ahead (2; 3 measured slower, r4: res fwd
 // / dgrad at B = 64 195 / 177 -> 199-202 / 182-185 us, fp8 step 22.36 -> 22.69 ms)
-template <int WN, int WM, int RN, int RM, int NSW = 2>
+// SCH bit 1 (stagger, bit-identical): waves NW/2.. keep a tap's fragments across the next
+// barrier and run its MFMAs right after it, while their SIMD partners issue the DMA and read
+// their fragments; they then issue their own DMA and reads under the partners' MFMAs.
+// SCH bit 0: one static s_setprio 1 for waves NW/2.. instead of the flips around each cluster.
+template <int WN, int WM, int RN, int RM, int NSW = 2, int SCH = 0>
 __global__ void __launch_bounds__(64 * WN * WM, 1)
 conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
   constexpr int NW = WN * WM;
@@ -5011,6 +5084,19 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
     for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nch = a.Cin >> 7, nks = 9 * nch;
+  const bool stag = (SCH & 2) && wave >= NW / 2;
+  v8i fa[RN], fb[RM];
+  auto mfma_all = [&]() {
+    if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[i][m] = mma_f8(fa[i], fb[m], acc[i][m]);
+    if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(0);
+  };
+  if constexpr (SCH & 1) {
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
   issue_b(0);
   issue_halo(0);
   if (NSW == 3 && 1 < nks) issue_b(1);
@@ -5028,15 +5114,17 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
     } else {
       wait_vm<0>();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr ((SCH & 2) != 0) {
+      if (stag && ks > 0) mfma_all();          // the previous tap's fragments
+    }
     if (ks + NSW - 1 < nks) issue_b(ks + NSW - 1);
     if (t == 0 && c + 1 < nch) issue_halo(c + 1);
     const int r = t / 3, s3 = t - (t / 3) * 3;
     const char* Hs = smem + (c & 1) * HALO;
     const char* Bs = smem + 2 * HALO + (ks % NSW) * BST;
-    v8i fa[RN], fb[RM];
 #pragma unroll
     for (int i = 0; i < RN; ++i) {
       const int row = wn * RN * 16 + i * 16 + lr;
@@ -5052,13 +5140,10 @@ conv3_halo_fp8(ConvArgs a, unsigned x_bytes) {
       const uint4 u1 = *reinterpret_cast<const uint4*>(Hs + HQ * 1024 + off);
       fb[m] = v8i{(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
     }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < RN; ++i)
-#pragma unroll
-      for (int m = 0; m < RM; ++m) acc[i][m] = mma_f8(fa[i], fb[m], acc[i][m]);
-    __builtin_amdgcn_s_setprio(0);
+    if (!stag) mfma_all();
   }
+  if (stag) mfma_all();
+  if constexpr (SCH & 1) __builtin_amdgcn_s_setprio(0);
   const float dq = a.dq0[0] * a.dq1[0];
 #pragma unroll
   for (int i = 0; i < RN; ++i)
@@ -5202,7 +5287,7 @@ conv3_wgrad_fp8(Wg8Args a) {
     for (int i = 0; i < nstep; ++i) {
       const int younger = min(AHEAD - 1, nstep - 1 - i);
       wait_vm_dyn(younger * npw);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_lgkm0();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (i + AHEAD < nstep) issue_group(i + AHEAD);
@@ -5297,7 +5382,12 @@ int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, co
   // res fwd / dgrad at B = 64 188 / 172 -> 208 / 192 us: the two waves of a SIMD already hide
   // each other's fragment reads (16 KB per 16 MFMAs of 32 cycles, half the CU's 256 B/clk of
   // LDS at the fp8 peak).)
-  hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb);
+  switch (res_sched(3)) {
+    case 1: hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4, 2, 1>), dim3(nblk), dim3(512), 0, s, a, xb); break;
+    case 2: hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4, 2, 2>), dim3(nblk), dim3(512), 0, s, a, xb); break;
+    case 3: hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4, 2, 3>), dim3(nblk), dim3(512), 0, s, a, xb); break;
+    default: hipLaunchKernelGGL((conv3_halo_fp8<2, 4, 4, 4>), dim3(nblk), dim3(512), 0, s, a, xb); break;
+  }
   return fv_check_launch("conv2d_fp8");
 }
 

@@ -65,7 +65,7 @@ CASES = [(256, 256, 8, 64, 2), (128, 256, 4, 128, 2), (256, 128, 12, 64, 1), (25
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_conv_fp8_fwd_and_dgrad(case):
+def test_conv_fp8_fwd_and_dgrad(case, monkeypatch):
     cin, cout, H, W, N = case
     g = torch.Generator().manual_seed(3 + cin + H)
     x = torch.randn(N, cin, H, W, generator=g)
@@ -95,6 +95,17 @@ def test_conv_fp8_fwd_and_dgrad(case):
     L.call("fv_conv2d_bwd_data_fp8", ctypes.byref(d), dy8.data_ptr(), dydq.data_ptr(), wt.data_ptr(),
            wdq.data_ptr(), dx.data_ptr(), L.stream())
     torch.cuda.synchronize()
+    # the SIMD-partner schedules (FV_RES_SCHED, conv3_halo_fp8 SCH) only reorder instructions
+    for sched in (0, 1, 2, 3):
+        monkeypatch.setenv("FV_RES_SCHED", str(sched))
+        y2, dx2 = torch.empty_like(y), torch.empty_like(dx)
+        L.call("fv_conv2d_fwd_fp8", ctypes.byref(d), x8.data_ptr(), xdq.data_ptr(), wk.data_ptr(), wdq.data_ptr(),
+               b.cuda().data_ptr(), None, y2.data_ptr(), None, L.stream())
+        L.call("fv_conv2d_bwd_data_fp8", ctypes.byref(d), dy8.data_ptr(), dydq.data_ptr(), wt.data_ptr(),
+               wdq.data_ptr(), dx2.data_ptr(), L.stream())
+        torch.cuda.synchronize()
+        assert torch.equal(y2, y) and torch.equal(dx2, dx), f"schedule {sched} differs"
+    monkeypatch.delenv("FV_RES_SCHED")
     # references on the dequantized fp8 operands (NHWC byte order -> NCHW)
     xq = deq(x8, xdq, (N, H, W, cin)).permute(0, 3, 1, 2)
     wq = deq(wk, wdq, (cout, 3, 3, cin)).permute(0, 3, 1, 2)
