@@ -43,9 +43,12 @@ def parse():
     ap.add_argument("--no-syncbn", action="store_true", help="per-rank BN statistics (labelled)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
-    ap.add_argument("--graph", type=int, default=-1,
-                    help="1: replay the step as one captured HIP graph (StepGraph), 0: eager launches; "
-                         "default: graph at one process, eager with collectives")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1 (default): replay the captured step (StepGraph: one HIP graph at one process, "
+                         "graph segments between the collectives at N > 1), 0: eager launches")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
+                    help="N > 1 collectives: rccl (one GPU per rank, the product path) or gloo (TorchComm: "
+                         "ranks may share a GPU -- tests on the one-GPU box)")
     return ap.parse_args()
 
 
@@ -149,8 +152,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        fv.distributed.init_dist(local, world, syncbn=not args.no_syncbn)
-    torch.cuda.set_device(local)
+        fv.distributed.init_dist(local, world, backend="gloo" if args.comm == "gloo" else "nccl",
+                                 syncbn=not args.no_syncbn)
+    torch.cuda.set_device(local if args.comm == "rccl" else local % torch.cuda.device_count())
     dtype = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp8": torch.float8_e4m3fn}[args.dtype]
     cfg = fv.FaceVAEConfig(H=args.res)
     torch.manual_seed(0)
@@ -184,7 +188,7 @@ def main():
     timer = ops.KernelTimer(is_res)
     ops.TIMER = timer
 
-    use_graph = (world == 1) if args.graph < 0 else bool(args.graph)
+    use_graph = bool(args.graph)
     run = step
     # warm-up step 1 (from the initial weights): its image and losses are the GPU side of the
     # parity record (compared with the CPU oracle's first step in cpu_baseline)
@@ -273,7 +277,10 @@ def main():
                    "global_batch": B * world, "per_gpu_batch": B, "resolution": cfg.H,
                    "parallelism": f"dp{world}" + ("" if world == 1 else (" syncbn" if not args.no_syncbn else " local-bn"))},
         "host_issue_ms_per_step": round(t_host / args.steps * 1e3, 3),
-        "launch": "hip graph (one captured step replayed)" if use_graph else "eager",
+        "launch": ("hip graph (one captured step replayed)" if world == 1 else
+                   "hip graph segments between the collectives (StepGraph)") if use_graph else "eager",
+        "comm": None if world == 1 else args.comm,
+        "loss_last": round(loss.item(), 6),
         "mfma_util_step": round(step_util, 4),
         "step_flop_per_image": f_img,
         "subpixel_shortcut": {"active": subpix, "executed_flop_per_image": f_exec,

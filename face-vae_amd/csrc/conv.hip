@@ -1065,6 +1065,77 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
   FV_DIAG_END();
 }
 
+// Epilogue of conv3_halo_fwd3 MODE 1 (sub-pixel forward): tile columns are 4 phases x 64
+// channels (wave column wn = phase (pa, pb)), rows the 256 low-res pixels (h0 + r, w0 + col).
+// bias -> BN records -> bf16 through LDS -> 16-B stores to output pixel (2h + pa, 2w + pb).
+// BN records: one per (tile, wave row, phase) = RM * 16 output pixels, record index
+// ((tm * WM + wm) * 4 + wn) (stats_record_pixels: 128), so every output pixel is in one record.
+template <int WM, int RM>
+__device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[4][RM], char* smem, int tn, int n,
+                                                int h0, int w0, int tm, int wn, int wm, int lane, int tid) {
+  constexpr int RN = 4, NT = 64 * 4 * WM, BN = 256, BM = WM * RM * 16, CPR = BN / 8;
+  const int lr = lane & 15, lh = lane >> 4;
+  const int cb0 = tn * 64;
+#pragma unroll
+  for (int nn = 0; nn < RN; ++nn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = cb0 + nn * 16 + lh * 4 + i;
+      const float bv = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[nn][m][i] += bv;
+    }
+  if (a.stats) {
+    const int rec = (tm * WM + wm) * 4 + wn;
+#pragma unroll
+    for (int nn = 0; nn < RN; ++nn) {
+      float sv[4], qv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t = 0.f, q = 0.f;
+#pragma unroll
+        for (int m = 0; m < RM; ++m) {
+          t += acc[nn][m][i];
+          q += acc[nn][m][i] * acc[nn][m][i];
+        }
+        sv[i] = row16_sum(t);
+        qv[i] = row16_sum(q);
+      }
+      const int cb = cb0 + nn * 16 + lh * 4;
+      const int ii = lr & 3;
+      const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
+      const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
+      const float val = lr < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
+      if (lr < 8) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int nn = 0; nn < RN; ++nn) {
+    const int cl = wn * 64 + nn * 16 + lh * 4;
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const int pl = wm * RM * 16 + m * 16 + lr;
+      bf16 t4[4] = {(bf16)acc[nn][m][0], (bf16)acc[nn][m][1], (bf16)acc[nn][m][2], (bf16)acc[nn][m][3]};
+      char* dst = smem + pl * BN * 2 + (((cl >> 3) ^ (pl & (CPR - 1))) << 4) + ((cl & 4) << 1);
+      *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(t4);
+    }
+  }
+  __syncthreads();
+  constexpr int NIT = BM * CPR / NT;
+  static_assert(BM * CPR % NT == 0, "store pass");
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int idx = tid + it * NT;
+    const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
+    const int ph = ch >> 3, co = cb0 + (ch & 7) * 8;
+    const int oh = 2 * (h0 + (pl >> 6)) + (ph >> 1), ow = 2 * (w0 + (pl & 63)) + (ph & 1);
+    Chunk8<bf16> v;
+    v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+    v.store(reinterpret_cast<bf16*>(a.y) + ((long)(n * a.Ho + oh) * a.Wo + ow) * a.ldy + co);
+  }
+}
+
 // Linear-halo variant of conv3_halo_fwd2: every LDS fragment address is a per-lane base
 // register plus an immediate.  In fwd2 the XOR swizzle of a 64-B halo pixel moves with the tap
 // shift, so each of the 16 fragment reads of a step costs ~5 VALU (88 non-MFMA VALU per 64
@@ -1093,9 +1164,25 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
 // of the tap whose fragments they hold, so they run those MFMAs while their partners issue the
 // DMA and fragment reads after the barrier, and issue their own reads while the partners run
 // MFMAs (same arithmetic, same order per accumulator: bit-identical).
-template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, int SCH = 0>
+//
+// MODE (UpBlock2D's nearest-x2 upsample + 3x3 conv, modules.py:78-89, on this kernel's halo
+// structure; the sub-pixel algebra of conv_fwd_v2 MODE 2 / 3):
+//   1 = sub-pixel forward over the LOW-res input: the 256-row co tile is 4 phases (pa, pb) x 64
+//       channels, wave column wn = phase; a 32-channel chunk has 4 tap units q = (rr, ss), the
+//       phase's 2x2 folded taps, which read the halo window tap (pa + rr, pb + ss); the
+//       epilogue stores phase wn of low-res pixel (h, w) to output pixel (2h + pa, 2w + pb).
+//   2 = data gradient at the LOW resolution: dy viewed as 4 phase planes (py, px) of the low-res
+//       grid, the conv input = [plane][Cout] channels (a.Cin = 4 Cout, a.K = dy's channel stride,
+//       a.Hin x a.Win = dy's size); a chunk lies in one plane and its 4 units are the plane's 2x2
+//       taps at window (1 - py + a, 1 - px + b); the halo DMA gathers plane pixels (2ih + py,
+//       2iw + px) -- the stride-2 4x4 conv of conv_fwd_v2 MODE 3 without its 12 zero taps.
+// Weights (weight_prep_phase_kernel): unit u = chunk * 4 + q, [rows][32] per unit.
+template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, int SCH = 0, int MODE = 0>
 __global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
+  static_assert(MODE == 0 || !PRO, "phase modes: no prologue");
+  static_assert(MODE != 1 || (WN == 4 && RN == 4), "sub-pixel forward: one phase of 64 channels per wave column");
+  constexpr int UPC = MODE ? 4 : 9;                        // tap units per 32-channel chunk
   constexpr int NW = WN * WM;
   constexpr int BN = WN * RN * 16, BM = WM * RM * 16, TR = BM / 64;
   static_assert(RM % 4 == 0, "a wave's pixels start on an image-row boundary of the tile");
@@ -1140,7 +1227,10 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     const int hr = hp / 66, hc = hp - (hp / 66) * 66;
     const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
     const bool ok = hp < HP && ch < 4 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-    hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
+    if constexpr (MODE == 2)     // plane (0, 0) pixel of dy; the chunk's plane is a uniform offset
+      hoff[j] = ok ? (unsigned)((((n * a.Hin + 2 * ih) * a.Win + 2 * iw) * a.K + (ch << 3)) * 2) : 0x80000000u;
+    else
+      hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
     if constexpr (PRO) {
       hval |= ok ? 1u << j : 0u;
       hcb[j] = ch * 8;
@@ -1181,7 +1271,8 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   const unsigned wbase = (unsigned)((co0 + wave * 16 + lrow) * 64 + ((lchk ^ rswz<bf16>(lrow)) << 4));
   const unsigned wstep = (unsigned)(NW * 16 * 64);
   const unsigned ustep = (unsigned)a.wus;
-  const int nch = a.Cin >> 5, nsteps = 9 * nch / 2;
+  const int nch = a.Cin >> 5, nsteps = UPC * nch / 2;
+  const int cpp = a.Cin >> 7;                               // MODE 2: chunks per phase plane
   auto issue_b = [&](int j, int buf) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1191,12 +1282,23 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, (unsigned)u * ustep + jb * wstep);
     }
   };
+  // the step after whose barrier halo chunk c is issued: the last read of chunk c - 2 (same
+  // buffer) was retired by it
+  auto halo_step = [&](int c) { return MODE ? 2 * c - 3 : (9 * c - 10) / 2; };
+  auto halo_soff = [&](int c) -> unsigned {
+    if constexpr (MODE == 2) {
+      const int pl = c / cpp, cc = c - pl * cpp;
+      return (unsigned)((((pl >> 1) * a.Win + (pl & 1)) * a.K + cc * 32) * 2);
+    } else {
+      return (unsigned)(c * 64);
+    }
+  };
   // one weight DMA piece q (0 .. 2 JB - 1) of stage j: tap half q / JB, row piece q % JB
   auto issue_halo = [&](int c) {
     const unsigned Hs = sbase + WOFF + (c & 1) * HALO;
 #pragma unroll
     for (int j = 0; j < JH; ++j)
-      if (j < JH - 1 || wave + j * NW < HQ) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], (unsigned)(c * 64));
+      if (j < JH - 1 || wave + j * NW < HQ) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], halo_soff(c));
   };
 
   const int lr = lane & 15, lh = lane >> 4;
@@ -1206,7 +1308,22 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   const int va = (wn * RN * 16 + lr) * 64 + ((lh ^ rswz<bf16>(lr)) << 4);
   const int vb = WOFF + ((wm * RM / 4) * 66 + lr) * PXB + lh * 16;
   auto load_frags = [&](Frag<bf16> (&fa)[RN], Frag<bf16> (&fb)[RM], int u, int buf) {
-    const int c = u / 9, t = u - c * 9, r = t / 3, s3 = t - (t / 3) * 3;
+    int c, r, s3;
+    if constexpr (MODE == 1) {
+      c = u >> 2;
+      r = (wn >> 1) + ((u >> 1) & 1);
+      s3 = (wn & 1) + (u & 1);
+    } else if constexpr (MODE == 2) {
+      c = u >> 2;
+      const int pl = c / cpp;
+      r = ((u >> 1) & 1) + 1 - (pl >> 1);
+      s3 = (u & 1) + 1 - (pl & 1);
+    } else {
+      c = u / 9;
+      const int t = u - c * 9;
+      r = t / 3;
+      s3 = t - (t / 3) * 3;
+    }
     const int pa = va + (buf * STG + (u & 1) * BST);
     const int pb = vb + ((c & 1) * HALO + (r * 66 + s3) * PXB);
 #pragma unroll
@@ -1252,7 +1369,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
     pend = bcnt(NSB - 1);
   }
   load_frags(fa0, fb0, 0, 0);
-  int hn = 2, hstep = (9 * 2 - 10) / 2;
+  int hn = 2, hstep = halo_step(2);
   int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
   int bj = 0;
   if constexpr (SCH & 1) {
@@ -1291,7 +1408,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
         xstep = j + 1 + (wave >= 4 ? 1 : 0);   // landed by the next step's barrier
       }
       ++hn;
-      hstep = (9 * hn - 10) / 2;
+      hstep = halo_step(hn);
     }
     pend = 0;
     if (j + NSB < nsteps) {
@@ -1312,7 +1429,10 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   if constexpr (SCH & 1) __builtin_amdgcn_s_setprio(0);
   FV_DIAG_LOOP_END();
   __syncthreads();
-  conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
+  if constexpr (MODE == 1)
+    subpix_epilogue<WM, RM>(a, acc, smem, tn, n, th * TR, tw * 64, tm, wn, wm, lane, tid);
+  else
+    conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
   FV_DIAG_END();
 }
 
@@ -3306,6 +3426,63 @@ __global__ void weight_prep_s2_kernel(const float* __restrict__ wp, const float*
   }
 }
 
+// Weight images of conv3_halo_fwd3 MODE 1 / 2: unit u = chunk c * 4 + q, a [rows][32] block per
+// unit (stage-major, as weight_prep_body smaj 1), q = (q >> 1, q & 1).
+//   MODE 1 (sub-pixel forward, wk): rows = 4 cout, row = tn * 256 + phase * 64 + co % 64 for
+//     co = tn * 64 + co % 64; element k = input channel c * 32 + k: phase (pa, pb)'s 2x2 tap
+//     (rr, ss) = q, the folded 3x3 sum of weight_prep_subpix_kernel.
+//   MODE 2 (low-res data gradient, wt): rows = the tile rows (cin of the conv), chunk c = (plane
+//     (py, px) = c / cpp, 32 output channels (c % cpp) * 32 + k); q = (a, b) is the stride-2
+//     tap (tr, tc) = (2a + 1 - py, 2b + 1 - px) of weight_prep_s2_kernel.
+// CONVT: the ConvTranspose2dELR k4 s2 p1 weights w [ci][co][4][4] (x gain (x cinv[co], demod))
+// on the same kernels: phase (pa, pb) tap (rr, ss) SELECTS Weff[ci][co][3 - pa - 2 rr][3 - pb - 2 ss]
+// (convt_weight_prep_kernel's map), and the stride-2 data-gradient tap (tr, tc) is Weff[ci][co][tr][tc].
+template <int MODE, bool CONVT = false>
+__global__ void weight_prep_phase_kernel(const float* __restrict__ wp, const float* sigma, bf16* out, int rows,
+                                         int units, int cout, int cin_valid, int cpp, const float* cinv = nullptr,
+                                         float gain = 1.f) {
+  const int total = units * rows * 32;
+  const float inv = sigma ? 1.f / sigma[0] : 1.f;
+  for (int e = blockIdx.x * (int)blockDim.x + threadIdx.x; e < total; e += gridDim.x * (int)blockDim.x) {
+    const int k = e & 31, qe = e >> 5, u = qe / rows, row = qe - u * rows;
+    const int c = u >> 2, q = u & 3;
+    int co, ci, r0, r1, s0, s1;
+    if constexpr (MODE == 1) {
+      const int ph = (row >> 6) & 3, pa = ph >> 1, pb = ph & 1, rr = q >> 1, ss = q & 1;
+      co = (row >> 8) * 64 + (row & 63);
+      ci = c * 32 + k;
+      r0 = rr ? 1 + pa : 0; r1 = rr ? 2 : pa;
+      s0 = ss ? 1 + pb : 0; s1 = ss ? 2 : pb;
+    } else {
+      const int pl = c / cpp, tr = 2 * (q >> 1) + 1 - (pl >> 1), tc = 2 * (q & 1) + 1 - (pl & 1);
+      co = (c - pl * cpp) * 32 + k;
+      ci = row;
+      r0 = max(0, 2 - tr); r1 = min(2, 3 - tr);
+      s0 = max(0, 2 - tc); s1 = min(2, 3 - tc);
+    }
+    float v = 0.f;
+    if (co < cout && ci < cin_valid) {
+      if constexpr (CONVT) {
+        int tr, tc;
+        if constexpr (MODE == 1) {
+          tr = 3 - ((row >> 7) & 1) - 2 * (q >> 1);
+          tc = 3 - ((row >> 6) & 1) - 2 * (q & 1);
+        } else {
+          const int pl = c / cpp;
+          tr = 2 * (q >> 1) + 1 - (pl >> 1);
+          tc = 2 * (q & 1) + 1 - (pl & 1);
+        }
+        v = wp[((long)ci * cout + co) * 16 + tr * 4 + tc] * (cinv ? gain * cinv[co] : gain);
+      } else {
+        const float* w = wp + ((long)co * cin_valid + ci) * 9;
+        for (int r = r0; r <= r1; ++r)
+          for (int t = s0; t <= s1; ++t) v += w[r * 3 + t];
+      }
+    }
+    out[e] = Elt<bf16>::from_f(CONVT ? v : v * inv);
+  }
+}
+
 // sub-pixel phase slabs [4][nsplit][CW][KW] (k = (r'*2+s')*cin + ci) -> dW [co][ci][3][3]:
 // each 3x3 tap r takes, per phase row pa, the 2x2 tap r' whose folded range holds it
 // (pa = 0: r' = r > 0; pa = 1: r' = r == 2), columns alike; + db from the bias slabs.
@@ -3617,6 +3794,32 @@ bool use_dgrad_lowres(const fv_conv_desc* d) {
   return (long)d->n * d->h * d->w * ct * 2 < (1L << 31);
 }
 
+// UpBlock2D convs on the halo kernel (conv3_halo_fwd3 MODE 1 forward, MODE 2 low-res data
+// gradient); FV_UP_HALO=0 keeps conv_fwd_v2 MODE 2 / 3 (A/B).  Read per call.
+static bool up_halo_on() {
+  const char* e = getenv("FV_UP_HALO");
+  return !(e && e[0] == '0');
+}
+static bool use_subpix_halo(const fv_conv_desc* d) {
+  if (!up_halo_on() || !use_subpix(d)) return false;
+  const int hl = d->h / 2, wl = d->w / 2;
+  return d->cout % 64 == 0 && d->cin % 32 == 0 && d->cin >= 64 && d->cin_valid == d->cin && wl % 64 == 0 &&
+         hl % 4 == 0 && !d->out_nchw_f32 && !d->epi_sigmoid && !d->pro_act && d->ldy % 8 == 0 &&
+         (long)d->n * hl * wl * d->cin * 2 < (1L << 31) && (long)d->n * d->h * d->w * d->ldy * 2 < (1L << 31);
+}
+// co tile (256 / 128 rows) of the low-res data gradient on the halo kernel, 0 = not on it
+static int dgrad_halo_bn(const fv_conv_desc* d) {
+  if (!up_halo_on() || !use_dgrad_lowres(d)) return 0;
+  const int hl = d->h / 2, wl = d->w / 2;
+  if (pad_pow2_8(d->cout) != d->cout || d->cout % 32 || wl % 64 || hl % 4 || d->cin_valid != d->cin) return 0;
+  if ((long)d->n * d->h * d->w * d->cout * 2 >= (1L << 31)) return 0;
+  return d->cin % 256 == 0 ? 256 : d->cin % 128 == 0 ? 128 : 0;
+}
+// elements of the phase weight images (weight_prep_phase_kernel): the one size both the
+// queries and the launches use
+static long phase_wk_elems(const fv_conv_desc* d) { return 4L * (d->cin / 32) * 4 * d->cout * 32; }
+static long phase_wt_elems(const fv_conv_desc* d) { return 4L * (4 * d->cout / 32) * d->cin * 32; }
+
 // Generator.out_conv shape: 7x7, 64 -> <= 4 channels, NCHW fp32 output (bf16 operands)
 bool use_c7n(const fv_conv_desc* d) {
   return d->dtype == FV_BF16 && d->ksize == 7 && d->cin == 64 && d->cin_valid == 64 &&
@@ -3924,6 +4127,7 @@ size_t fv_conv_wk_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const size_t rows = (size_t)wrows(d->cout);
   if (use_c7n(d)) return 32 * 448;
+  if (use_subpix_halo(d)) return (size_t)phase_wk_elems(d);
   if (use_subpix(d)) return 4 * rows * kpad_of(2, d->cin);
   return rows * kpad_of(d->ksize, d->cin);
 }
@@ -3932,6 +4136,7 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   const int cin_t = pad_pow2_8(d->cout);
   const size_t rows = (size_t)wrows(d->cin);
+  if (dgrad_halo_bn(d)) return (size_t)phase_wt_elems(d);
   if (use_dgrad_lowres(d)) return rows * 16 * cin_t;
   return rows * kpad_of(d->ksize, cin_t);
 }
@@ -3987,7 +4192,8 @@ static FwdTile plan_tile(const fv_conv_desc* d) {
 
 // pixels per BN-statistics record = the pixels of one wave row of the tile (BM / WM)
 static int stats_record_pixels(const fv_conv_desc* d) {
-  if (use_c7n(d)) return 64;                                  // one 64-pixel row segment
+  if (use_c7n(d)) return 64;
+  if (use_subpix_halo(d)) return 128;                         // (tile, wave row, phase): RM * 16                                  // one 64-pixel row segment
   if (use_c74(d)) return C74_TR * 64;                         // one record per tile
   if (use_c64(d)) return C64_G * 64;                          // 8 iterations x one wave's row
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
@@ -4060,6 +4266,11 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
   if (wk && use_c7n(d)) {
     hipLaunchKernelGGL(weight_prep_c7n_kernel, dim3(56), dim3(256), 0, s, w_param, sigma, (bf16*)wk, d->cout);
     if ((st = fv_check_launch("weight_prep_c7n"))) return st;
+  } else if (wk && use_subpix_halo(d)) {
+    const int nb = (int)std::min<long>(fv_cdiv(phase_wk_elems(d), 256), 4096);
+    hipLaunchKernelGGL(weight_prep_phase_kernel<1>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wk,
+                       4 * d->cout, 4 * (d->cin / 32), d->cout, d->cin_valid, 0);
+    if ((st = fv_check_launch("weight_prep_phase1"))) return st;
   } else if (wk && use_subpix(d)) {
     const int rows = wrows(d->cout), Kp = kpad_of(2, d->cin);
     const long tot = 4L * rows * Kp;
@@ -4079,7 +4290,12 @@ int fv_conv_weight_prep(const fv_conv_desc* d, const float* w_param, const float
                          rows, Kp, d->cout, d->cin_valid, fv_ilog2(d->cin), ks, ks * ks * d->cin, 0, 0);
     if ((st = fv_check_launch("weight_prep"))) return st;
   }
-  if (wt && use_dgrad_lowres(d)) {
+  if (wt && dgrad_halo_bn(d)) {
+    const int nb = (int)std::min<long>(fv_cdiv(phase_wt_elems(d), 256), 4096);
+    hipLaunchKernelGGL(weight_prep_phase_kernel<2>, dim3(nb), dim3(256), 0, s, w_param, sigma, (bf16*)wt, d->cin,
+                       4 * (4 * d->cout / 32), d->cout, d->cin_valid, d->cout / 32);
+    if ((st = fv_check_launch("weight_prep_phase2"))) return st;
+  } else if (wt && use_dgrad_lowres(d)) {
     const int cin_t = pad_pow2_8(d->cout);
     const int rows = wrows(d->cin), Kp = 16 * cin_t;
     const long tot = (long)rows * Kp;
@@ -4221,6 +4437,24 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     else
       hipLaunchKernelGGL((conv_halo_fwd<7, 64, 1, 2, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
     return fv_check_launch("conv2d_fwd_halo");
+  }
+  if (use_subpix_halo(d)) {
+    FV_REQUIRE(!res && !a.spm, "sub-pixel conv: no residual / store-pass records");
+    a.H = a.Hin; a.W = a.Win;                       // tile space = the low-res input image
+    a.Ho = d->h; a.Wo = d->w;
+    a.P = d->n * a.H * a.W;
+    a.lgtw = 6;
+    a.wus = 4 * d->cout * 64;                       // one unit = 4 phases x cout rows of 64 B
+    a.ntn = d->cout / 64;
+    const int nblk = a.ntn * d->n * (a.H / 4) * (a.W / 64);
+    const unsigned xb = (unsigned)((long)d->n * a.H * a.W * d->cin * 2);
+    // the weight DMA of the last unit ends inside the image the queries size
+    FV_REQUIRE((long)4 * (d->cin / 32) * a.wus / 2 <= phase_wk_elems(d), "sub-pixel halo conv: weight image");
+    if (res_sched(2) == 2)
+      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
+    else
+      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 0, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
+    return fv_check_launch("conv2d_fwd_subpix_halo");
   }
   if (use_subpix(d)) {
     FV_REQUIRE(!res, "sub-pixel conv: no residual");
@@ -4413,6 +4647,32 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
   if (st) return st;
   const fv_conv_desc t = dgrad_desc(d);
   FV_REQUIRE(ldy_dy == t.cin, "bwd_data: dy channel stride must be %d (got %d)", t.cin, ldy_dy);
+  if (const int bn = dgrad_halo_bn(d)) {
+    FV_REQUIRE(dy && wt && dx, "null pointer");
+    ConvArgs a{};
+    a.x = dy; a.w = wt; a.y = dx;
+    a.N = d->n; a.H = d->h / 2; a.W = d->w / 2; a.Hin = d->h; a.Win = d->w;
+    a.Ho = a.H; a.Wo = a.W;
+    a.P = d->n * a.H * a.W;
+    a.Cin = 4 * d->cout;                            // the 4 phase planes of dy as input channels
+    a.K = d->cout;                                  // dy's channel stride
+    a.Cout = d->cin; a.ldy = d->cin;
+    a.lgtw = 6;
+    a.wus = d->cin * 64;
+    a.ntn = d->cin / bn;
+    const int nblk = a.ntn * d->n * (a.H / 4) * (a.W / 64);
+    const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cout * 2);
+    FV_REQUIRE((long)(a.Cin / 32) * 4 * a.wus / 2 <= phase_wt_elems(d), "low-res halo dgrad: weight image");
+    const int sch = res_sched(2);
+    if (bn == 256) {
+      if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
+      else hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 0, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
+    } else {
+      if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 2, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
+      else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 0, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
+    }
+    return fv_check_launch("conv2d_bwd_data_lowres_halo");
+  }
   if (use_dgrad_lowres(d)) {
     FV_REQUIRE(dy && wt && dx, "null pointer");
     ConvArgs a{};
@@ -4758,6 +5018,23 @@ int fv_convt_weight_prep(const fv_conv_desc* d, const float* w, int demod, float
     hipLaunchKernelGGL(convt_norm_kernel, dim3(d->cout), dim3(64), 0, s, w, d->cin_valid, d->cout, inv);
     if ((st = fv_check_launch("convt_norm"))) return st;
   }
+  // the halo kernels' phase layouts (conv3_halo_fwd3 MODE 1 / 2) where those kernels take the launch
+  const float* cinv = demod ? inv : nullptr;
+  if (wk && use_subpix_halo(d)) {
+    const int nb1 = (int)std::min<long>(fv_cdiv(phase_wk_elems(d), 256), 4096);
+    hipLaunchKernelGGL((weight_prep_phase_kernel<1, true>), dim3(nb1), dim3(256), 0, s, w, nullptr, (bf16*)wk,
+                       4 * d->cout, 4 * (d->cin / 32), d->cout, d->cin_valid, 0, cinv, gain);
+    if ((st = fv_check_launch("convt_weight_prep_phase1"))) return st;
+    wk = nullptr;
+  }
+  if (wt && dgrad_halo_bn(d)) {
+    const int nb2 = (int)std::min<long>(fv_cdiv(phase_wt_elems(d), 256), 4096);
+    hipLaunchKernelGGL((weight_prep_phase_kernel<2, true>), dim3(nb2), dim3(256), 0, s, w, nullptr, (bf16*)wt, d->cin,
+                       4 * (4 * d->cout / 32), d->cout, d->cin_valid, d->cout / 32, cinv, gain);
+    if ((st = fv_check_launch("convt_weight_prep_phase2"))) return st;
+    wt = nullptr;
+  }
+  if (!wk && !wt) return FV_OK;
   const int cin_t = pad_pow2_8(d->cout);
   const int rows = wrows(d->cout), Kp = kpad_of(2, d->cin);
   const int rows_t = wrows(d->cin);
