@@ -100,6 +100,11 @@ _SIGS = {
     "fv_quantize_fp8_site": (c_int, [c_int, P, c_long, P, P, c_int, P, P]),
     "fv_conv2d_fwd_fp8_site": (c_int, [D, P, P, P, P, P, P, P, P, P]),
     "fv_conv2d_bwd_data_fp8_site": (c_int, [D, P, P, P, P, P, P]),
+    "fv_fp8_set_deferred_roll": (c_int, [c_int]),
+    "fv_fp8_amax": (c_int, [c_int, P, c_long, P, P, P]),
+    "fv_fp8_site_seed": (c_int, [P, P, P]),
+    "fv_fp8_sites_inflight": (c_int, [c_int, P, P, P]),
+    "fv_fp8_sites_roll": (c_int, [c_int, P, P, P]),
     "fv_conv2d_wgrad_fp8_supported": (c_int, [D]),
     "fv_conv2d_bwd_weight_fp8": (c_int, [D, P, P, P, P, P, P, P]),
     "fv_conv2d_fp8_stats_blocks": (c_int, [D]),

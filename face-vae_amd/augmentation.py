@@ -11,7 +11,7 @@ same arithmetic:
   RandomPerspective cv2.getPerspectiveTransform on the reference's four point pairs, then
                    cv2.warpPerspective(..., (256, 256), BORDER_REPLICATE): bilinear inverse map
   RandomFlip       np.fliplr / time reversal
-  RandomResize / RandomCrop  skimage resize (bilinear, anti_aliasing off) / random crop + pad
+  RandomResize / RandomCrop  skimage resize (order 0 / 1, anti-aliased, zero fill) / random crop + pad
   ColorJitter      torchvision.transforms.functional.adjust_{brightness, saturation, hue,
                    contrast} on the uint8 PIL image (ImageEnhance blends; hue via PIL HSV),
                    in a random order, as augmentation.py:245-281
@@ -86,14 +86,23 @@ def warp_perspective(img: np.ndarray, M: np.ndarray, size) -> np.ndarray:
     return _bilinear(img, ys, xs, "edge").astype(img.dtype)
 
 
-def resize(img: np.ndarray, size) -> np.ndarray:
-    """skimage.transform.resize(img, size, order=1, anti_aliasing=False): pixel-centre mapping."""
-    H, W = img.shape[:2]
-    h, w = size
-    ys = (np.arange(h) + 0.5) * (H / h) - 0.5
-    xs = (np.arange(w) + 0.5) * (W / w) - 0.5
-    yy, xx = np.meshgrid(ys, xs, indexing="ij")
-    return _bilinear(img, yy, xx, "edge").astype(img.dtype)
+def resize(img: np.ndarray, size, order: int = 1) -> np.ndarray:
+    """skimage.transform.resize(img, size, order, preserve_range=True, mode='constant',
+    anti_aliasing=True) (augmentation.py:58-59), restated on scipy.ndimage as skimage computes it:
+    a Gaussian pre-filter with sigma = max(0, (in / out - 1) / 2) per axis (zero padding; a no-op
+    when upscaling), ndimage.zoom with grid_mode=True (pixel-centre mapping) in 'grid-constant'
+    mode (samples past the border blend with 0), then the output clipped to the input's range
+    extended by the 0 fill.  Float input keeps its dtype, integer input comes back float64
+    (preserve_range)."""
+    from scipy import ndimage as ndi
+    x = img if img.dtype.char in "df" else img.astype(np.float64)
+    out_shape = tuple(int(v) for v in size) + x.shape[2:]
+    factors = np.divide(x.shape, out_shape)
+    sigma = np.maximum(0, (factors - 1) / 2)
+    filtered = ndi.gaussian_filter(x, sigma, cval=0, mode="constant")
+    out = ndi.zoom(filtered, [1 / f for f in factors], order=order, mode="grid-constant", cval=0, grid_mode=True)
+    lo, hi = min(float(x.min()), 0.0), float(x.max())
+    return np.clip(out, lo, hi)
 
 
 class RandomFlip:
@@ -155,7 +164,8 @@ class RandomResize:
     def __call__(self, clip):
         s = random.uniform(self.ratio[0], self.ratio[1])
         h, w = clip[0].shape[:2]
-        return [resize(img, (int(h * s), int(w * s))) for img in clip]
+        order = 1 if self.interpolation == "bilinear" else 0        # augmentation.py:58
+        return [resize(img, (int(h * s), int(w * s)), order) for img in clip]
 
 
 class RandomCrop:

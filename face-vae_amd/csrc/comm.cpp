@@ -59,7 +59,7 @@ int fv_comm_allreduce(fv_comm_t comm, void* buf, size_t count, int dtype, int op
   ncclDataType_t dt;
   int st = map_dtype(dtype, &dt);
   if (st) return st;
-  const ncclRedOp_t rop = op == 1 ? ncclAvg : ncclSum;
+  const ncclRedOp_t rop = op == 1 ? ncclAvg : op == 2 ? ncclMax : ncclSum;
   return nccl_check(ncclAllReduce(buf, buf, count, dt, rop, (ncclComm_t)comm, (hipStream_t)stream),
                     "ncclAllReduce");
 }

@@ -2691,6 +2691,10 @@ struct H3Wg2Args {
   float slope;
 };
 
+// (measured r5, not kept: one static s_setprio 1 for waves 4-7 instead of the per-half flips,
+// and the second k-half's dy fragments read under the first half's last MFMA group -- res /
+// down2 / down1 143 / 288 / 355 us either way, the prefetch variant spills at 256 VGPRs;
+// profiles/r5/r5c_*)
 template <int AHEAD, bool PRO = false>
 __global__ void __launch_bounds__(512, 1)
 conv3_halo_wgrad2(H3Wg2Args a) {
@@ -2875,23 +2879,24 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       const char* xrow[3];
 #pragma unroll
       for (int r = 0; r < 3; ++r) xrow[r] = xr_ + ((i + r) % NSX) * XB;     // x rows h - 1, h, h + 1
+      // x fragment of k-tile j of k-half kk (tap row / column constant after unrolling)
+      auto xfrag = [&](int j, int kk) {
+        const int kt = 9 * WK + j, tap = kt >> 2;
+        return frag2(xrow[tap / 3], lcx[j][0], lcx[j][1], kk * 32 * 128);
+      };
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         bf16x8 af[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) af[q] = frag2(dys, lcd[q][0], lcd[q][1], kk * 32 * BC * 2);
-        // x fragment of k-tile j (tap row / column constant after unrolling); the next one is
-        // read before the current one's 4 MFMAs so the LDS latency hides under them
-        auto xfrag = [&](int j) {
-          const int kt = 9 * WK + j, tap = kt >> 2;
-          return frag2(xrow[tap / 3], lcx[j][0], lcx[j][1], kk * 32 * 128);
-        };
-        bf16x8 bcur = xfrag(0);
+        // the next x fragment is read before the current one's 4 MFMAs so the LDS latency hides
+        // under them
+        bf16x8 bcur = xfrag(0, kk);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 9; ++j) {
           bf16x8 bnext = bcur;
-          if (j + 1 < 9) bnext = xfrag(j + 1);
+          if (j + 1 < 9) bnext = xfrag(j + 1, kk);
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bcur, acc[q][j], 0, 0, 0);
           bcur = bnext;
@@ -3778,6 +3783,10 @@ bool use_subpix(const fv_conv_desc* d) {
 // schedules bit for bit in one process).  r5, alternating convbench runs on one box, B=32 bf16
 // res fwd / dgrad: 0: 130 / 122, 1: 124 / 118, 2: 120 / 115, 3: 126 / 119 us; B=64 fp8 res
 // fwd / dgrad: 0: 175 / 166, 1: 173 / 163, 2: 172 / 155, 3: 165 / 155 us.
+// data-parallel fp8 (fv_fp8_set_deferred_roll): the *_site convs leave the in-flight amax in the
+// site; the caller all-reduces (MAX) every site's amax once per step and rolls them together
+static int g_fp8_defer_roll = 0;
+
 static int res_sched(int dflt) {
   const char* e = getenv("FV_RES_SCHED");
   return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : dflt;
@@ -5161,6 +5170,35 @@ __global__ void fp8_site_seed_kernel(const float* part, int np, unsigned* st) {
   }
 }
 
+// data-parallel global scaling (fv_fp8_set_deferred_roll): the sites' in-flight amax words,
+// gathered into one float vector (all-reduced MAX across ranks by the caller), then rolled into
+// every site's history at once -- identical histories, so identical scales, on every rank
+__global__ void fp8_sites_inflight_kernel(int n, const unsigned long long* __restrict__ sites, float* amax) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) amax[i] = __uint_as_float(reinterpret_cast<const unsigned*>(sites[i])[16]);
+}
+__global__ void fp8_sites_roll_kernel(int n, const unsigned long long* __restrict__ sites, const float* amax) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned* st = reinterpret_cast<unsigned*>(sites[i]);
+  st[16] = __float_as_uint(amax[i]);
+  fp8_site_roll(st);
+}
+// a site's first call under global scaling: the history filled with a given (all-reduced) amax
+__global__ void fp8_site_seed_from_kernel(const float* amax, unsigned* st) {
+  if (threadIdx.x < FP8_HIST) st[threadIdx.x] = __float_as_uint(amax[0]);
+  if (threadIdx.x == 0) {
+    st[16] = 0u;
+    st[17] = 0u;
+  }
+}
+// amax of the partials -> one float
+__global__ void fp8_amax_final_kernel(const float* part, int np, float* out) {
+  __shared__ float sh[4];
+  const float m = amax_of_parts(part, np, sh);
+  if (threadIdx.x == 0) out[0] = m;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) quantize_fp8_delayed_kernel(const T* __restrict__ x, long n, unsigned* st,
                                                                    uint8_t* __restrict__ y) {
@@ -5694,6 +5732,47 @@ int fv_quantize_fp8(int dtype_in, const void* x, long count, uint8_t* y, float* 
 
 size_t fv_fp8_site_bytes(void) { return FP8_SITE * sizeof(unsigned); }
 
+int fv_fp8_set_deferred_roll(int on) {
+  g_fp8_defer_roll = on ? 1 : 0;
+  return FV_OK;
+}
+
+int fv_fp8_amax(int dtype_in, const void* x, long count, float* amax, void* ws, void* stream) {
+  FV_REQUIRE(x && amax && ws && count > 0, "fp8_amax: bad args");
+  FV_REQUIRE(dtype_in == FV_BF16 || dtype_in == FV_F32, "fp8_amax: input must be bf16 or f32");
+  hipStream_t s = (hipStream_t)stream;
+  const long chunks = (count + 7) / 8;
+  const int nb = (int)std::min<long>(FP8_NPART, std::max<long>(1, (chunks + 255) / 256));
+  if (dtype_in == FV_BF16)
+    hipLaunchKernelGGL(amax_kernel<bf16>, dim3(nb), dim3(256), 0, s, (const bf16*)x, count, (float*)ws);
+  else
+    hipLaunchKernelGGL(amax_kernel<float>, dim3(nb), dim3(256), 0, s, (const float*)x, count, (float*)ws);
+  hipLaunchKernelGGL(fp8_amax_final_kernel, dim3(1), dim3(256), 0, s, (const float*)ws, nb, amax);
+  return fv_check_launch("fp8_amax");
+}
+
+int fv_fp8_site_seed(void* site, const float* amax, void* stream) {
+  FV_REQUIRE(site && amax, "fp8_site_seed: bad args");
+  hipLaunchKernelGGL(fp8_site_seed_from_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, amax, (unsigned*)site);
+  return fv_check_launch("fp8_site_seed_from");
+}
+
+int fv_fp8_sites_inflight(int n, const uint64_t* sites, float* amax, void* stream) {
+  FV_REQUIRE(n >= 0 && (n == 0 || (sites && amax)), "fp8_sites_inflight: bad args");
+  if (n == 0) return FV_OK;
+  hipLaunchKernelGGL(fp8_sites_inflight_kernel, dim3(fv_cdiv(n, 64)), dim3(64), 0, (hipStream_t)stream, n,
+                     (const unsigned long long*)sites, amax);
+  return fv_check_launch("fp8_sites_inflight");
+}
+
+int fv_fp8_sites_roll(int n, const uint64_t* sites, const float* amax, void* stream) {
+  FV_REQUIRE(n >= 0 && (n == 0 || (sites && amax)), "fp8_sites_roll: bad args");
+  if (n == 0) return FV_OK;
+  hipLaunchKernelGGL(fp8_sites_roll_kernel, dim3(fv_cdiv(n, 64)), dim3(64), 0, (hipStream_t)stream, n,
+                     (const unsigned long long*)sites, amax);
+  return fv_check_launch("fp8_sites_roll");
+}
+
 int fv_quantize_fp8_site(int dtype_in, const void* x, long count, uint8_t* y, void* site, int seeded, void* ws,
                          void* stream) {
   FV_REQUIRE(x && y && site && ws && count > 0, "quantize_fp8_site: bad args");
@@ -5768,7 +5847,7 @@ int fv_conv2d_fwd_fp8_site(const fv_conv_desc* d, const uint8_t* x8, void* site,
   FV_REQUIRE(!(res && stats), "fp8 conv: residual and BN statistics in one call are not supported");
   unsigned* sp = (unsigned*)site;
   return conv_fp8_run(d, d->cin, d->cout, x8, (const float*)(sp + 18), wk, w_dq, bias, res, y, stats,
-                      (hipStream_t)stream, sp);
+                      (hipStream_t)stream, g_fp8_defer_roll ? nullptr : sp);
 }
 
 int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void* site, const uint8_t* wt,
@@ -5779,7 +5858,7 @@ int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void*
   FV_REQUIRE(dy8 && site && wt && wt_dq && dx, "null pointer");
   unsigned* sp = (unsigned*)site;
   return conv_fp8_run(d, d->cout, d->cin, dy8, (const float*)(sp + 18), wt, wt_dq, nullptr, nullptr, dx, nullptr,
-                      (hipStream_t)stream, sp);
+                      (hipStream_t)stream, g_fp8_defer_roll ? nullptr : sp);
 }
 
 int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const float* dy_dq, const uint8_t* wt,

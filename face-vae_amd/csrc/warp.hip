@@ -266,6 +266,50 @@ __global__ void __launch_bounds__(256) gs_bucket_fill(const float* __restrict__ 
   rec[gs_offset(off, boff, kr.x) + kr.y] = r;
 }
 
+// The fill places a bucket's records in atomicAdd-rank order, which changes run to run; the
+// gather sums them in bucket order.  One thread per bucket sorts it by voxel index, so the
+// input gradient is bit-reproducible: insertion sort for the common few records, heapsort
+// (O(n log n), in place) when a degenerate grid piles many voxels onto one cell.
+__device__ __forceinline__ void gs_sift(GsRec* a, int i, int n) {
+  const GsRec x = a[i];
+  while (true) {
+    int c = 2 * i + 1;
+    if (c >= n) break;
+    if (c + 1 < n && a[c + 1].v > a[c].v) ++c;
+    if (a[c].v <= x.v) break;
+    a[i] = a[c];
+    i = c;
+  }
+  a[i] = x;
+}
+__global__ void __launch_bounds__(256) gs_bucket_sort(GsRec* __restrict__ rec, const int* __restrict__ off,
+                                                      const int* __restrict__ boff, long nkey) {
+  const long key = (long)blockIdx.x * 256 + threadIdx.x;
+  if (key >= nkey - 1) return;
+  const int b = gs_offset(off, boff, (int)key), n = gs_offset(off, boff, (int)key + 1) - b;
+  if (n < 2) return;
+  GsRec* a = rec + b;
+  if (n <= 16) {
+    for (int i = 1; i < n; ++i) {
+      const GsRec x = a[i];
+      int j = i - 1;
+      while (j >= 0 && a[j].v > x.v) {
+        a[j + 1] = a[j];
+        --j;
+      }
+      a[j + 1] = x;
+    }
+    return;
+  }
+  for (int i = n / 2 - 1; i >= 0; --i) gs_sift(a, i, n);
+  for (int e = n - 1; e > 0; --e) {
+    const GsRec t = a[0];
+    a[0] = a[e];
+    a[e] = t;
+    gs_sift(a, 0, e);
+  }
+}
+
 // one lane per (input cell, V-channel chunk); V = 8 (Chunk8 rows, C % 8 == 0) or 1
 template <typename T, int V>
 __global__ void __launch_bounds__(256) gs_gather_input(const GsRec* __restrict__ rec, const int* __restrict__ off,
@@ -642,13 +686,15 @@ int fv_grid_sample3d_bwd_input(int dtype, const float* grid, const void* gout, i
   FV_REQUIRE(w.nvox < (1L << 31) && w.nkey < (1L << 31), "grid_sample3d_bwd_input: more than 2^31 voxels or cells");
   hipStream_t s = (hipStream_t)stream;
   const long ncell = (long)(B / group) * Di * Hi * Wi;
-  hipMemsetAsync(w.cnt, 0, w.nkey * sizeof(int), s);
+  const hipError_t me = hipMemsetAsync(w.cnt, 0, w.nkey * sizeof(int), s);
+  FV_REQUIRE(me == hipSuccess, "grid_sample3d_bwd_input: hipMemsetAsync: %s", hipGetErrorString(me));
   hipLaunchKernelGGL(gs_bucket_count, dim3(fv_cdiv(w.nvox, 256)), dim3(256), 0, s, grid, w.nvox, (long)Do * Ho * Wo, Di,
                      Hi, Wi, group, w.cnt, w.keyrank);
   hipLaunchKernelGGL(gs_scan_blocks, dim3((unsigned)w.nblk), dim3(256), 0, s, w.cnt, w.nkey, w.bsum);
   hipLaunchKernelGGL(gs_scan_totals, dim3(1), dim3(256), 0, s, w.bsum, (int)w.nblk);
   hipLaunchKernelGGL(gs_bucket_fill, dim3(fv_cdiv(w.nvox, 256)), dim3(256), 0, s, grid, w.keyrank, w.cnt, w.bsum,
                      w.nvox, Di, Hi, Wi, w.rec);
+  hipLaunchKernelGGL(gs_bucket_sort, dim3(fv_cdiv(w.nkey - 1, 256)), dim3(256), 0, s, w.rec, w.cnt, w.bsum, w.nkey);
 #define GS_GATHER(T, V)                                                                                          \
   hipLaunchKernelGGL((gs_gather_input<T, V>), dim3(fv_cdiv(ncell * (C / V), 256)), dim3(256), 0, s, w.rec, w.cnt, \
                      w.bsum, (const T*)gout, ncell, Di, Hi, Wi, C, (T*)gin)

@@ -93,8 +93,9 @@ class RcclComm:
         if _deferred(lambda: self.allreduce_(t, op, wait_back)):
             return t
         L = self._L
+        code = {"sum": 0, "avg": 1, "max": 2}[op]
         return self._launch(lambda s: L.call("fv_comm_allreduce", self._h, t.data_ptr(), t.numel(),
-                                             L.dtype_code(t.dtype), 1 if op == "avg" else 0, s), t, wait_back)
+                                             L.dtype_code(t.dtype), code, s), t, wait_back)
 
     def broadcast_(self, t: torch.Tensor, root: int = 0, wait_back: bool = True):
         if _deferred(lambda: self.broadcast_(t, root, wait_back)):
@@ -126,7 +127,7 @@ class TorchComm:
     def allreduce_(self, t, op="sum", wait_back=True):
         if _deferred(lambda: self.allreduce_(t, op, wait_back)):
             return t
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM, group=self.group)
         if op == "avg":
             t.div_(self.world_size)
         return t
@@ -180,9 +181,9 @@ def init_seeds(cuda_deterministic: bool = True):
     """distributed.py:9-21: seed = 1 + rank for python, numpy and torch (CPU and every GPU).
     train.py:12 calls it BEFORE init_dist, so the rank is 0 and every rank seeds 1 (SURVEY.md
     Appendix A.1).  The cuDNN flags have no counterpart here (no cuDNN on this path).  The
-    FaceVAE step's HIP kernels are deterministic either way (no atomics, fixed reduction
-    orders); the exception is the §8(f)2 warp path: grid_sample3d's backward accumulates the
-    input gradient with fp32 float atomics (warp.hip), whose order is not fixed run to run."""
+    FaceVAE step's HIP kernels are deterministic either way (no float atomics, fixed reduction
+    orders), the §8(f)2 warp path included: grid_sample3d's input gradient gathers buckets
+    ordered by voxel index (warp.hip gs_bucket_sort)."""
     seed = 1 + get_rank()
     random.seed(seed)
     np.random.seed(seed)
@@ -305,9 +306,15 @@ class DataParallel(torch.nn.Module):
         self.launch_order: List[int] = []      # bucket indices in launch order, last backward
         self._hooks = []
         self._armed = False
+        self._fp8_key = None
         if self.world > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            # fp8 operands (config C5): one scale per operand for the whole global batch, as
+            # SyncBN's statistics (ops.quantize_fp8_site seeds, _sync_fp8 rolls once per step)
+            from . import _lib, ops
+            ops.FP8_GLOBAL = self.comm
+            _lib.call("fv_fp8_set_deferred_roll", 1)
 
     def forward(self, *args, **kwargs):
         self._pending = [len(b) for b in self.buckets]
@@ -335,11 +342,43 @@ class DataParallel(torch.nn.Module):
             self.launch_order.append(bi)
             self.comm.allreduce_(self._flat[bi], op="avg", wait_back=False)
 
+    def _fp8_sites(self):
+        sites = []
+        for m in self.module.modules():
+            d = m.__dict__.get("_fv_fp8_sites")
+            if d:
+                sites.extend(d[k][0] for k in sorted(d))
+        return sites
+
+    def _sync_fp8(self):
+        """Every fp8 site's in-flight amax of this step, all-reduced (MAX) in ONE collective and
+        rolled into every history at once (include/facevae.h fv_fp8_sites_roll): after it all
+        ranks hold identical histories, so the next step's scales are global.  Sites exist
+        after the first (eager) step; the device table of their pointers is rebuilt only when
+        the set changes."""
+        sites = self._fp8_sites()
+        if not sites:
+            return
+        from . import _lib
+        key = tuple(t.data_ptr() for t in sites)
+        if key != self._fp8_key:
+            dev = sites[0].device
+            self._fp8_tab = torch.tensor(key, dtype=torch.int64).to(dev)
+            self._fp8_amax = torch.empty(len(sites), dtype=torch.float32, device=dev)
+            self._fp8_key = key
+        _lib.call("fv_fp8_sites_inflight", len(sites), self._fp8_tab.data_ptr(), self._fp8_amax.data_ptr(),
+                  _lib.stream())
+        self.comm.allreduce_(self._fp8_amax, op="max", wait_back=True)
+        _lib.call("fv_fp8_sites_roll", len(sites), self._fp8_tab.data_ptr(), self._fp8_amax.data_ptr(),
+                  _lib.stream())
+
     def _finish(self):
         for bi, n in enumerate(self._pending):     # params that got no grad this step
             if n != 0 and n != len(self.buckets[bi]):
                 raise RuntimeError("DataParallel: a bucket was only partially reduced "
                                    "(unused parameters are not supported)")
+        if self._params and self._params[0].is_cuda:
+            self._sync_fp8()
         if self._params:
             self.comm.fence(self._params[0].device if self._params[0].is_cuda else None)
         for bi, b in enumerate(self.buckets):

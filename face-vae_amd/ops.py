@@ -54,12 +54,26 @@ def fp8_site(conv, which: str, device):
     return st
 
 
+# data-parallel global fp8 scaling (distributed.DataParallel at world > 1 installs its
+# communicator here and turns on the deferred roll, include/facevae.h fv_fp8_set_deferred_roll)
+FP8_GLOBAL = None
+
+
 def quantize_fp8_site(t: torch.Tensor, site):
     """(uint8 e4m3 copy of t quantized with the site's delayed scale, dq view [1] fp32); the
-    first call of a site quantizes exactly and seeds its history."""
+    first call of a site quantizes exactly and seeds its history -- under data parallelism
+    with the exact amax all-reduced (MAX) across ranks, so every rank starts from the same
+    scale (the single process on the global batch)."""
     y = _empty(t.numel(), torch.uint8, t.device)
     ws = _empty(query("fv_fp8_ws_bytes") // 4, F32, t.device)
-    call("fv_quantize_fp8_site", L.dtype_code(t.dtype), ptr(t), t.numel(), ptr(y), ptr(site[0]), int(site[1]),
+    seeded = int(site[1])
+    if not seeded and FP8_GLOBAL is not None:
+        amax = _empty(1, F32, t.device)
+        call("fv_fp8_amax", L.dtype_code(t.dtype), ptr(t), t.numel(), ptr(amax), ptr(ws), stream())
+        FP8_GLOBAL.allreduce_(amax, op="max", wait_back=True)
+        call("fv_fp8_site_seed", ptr(site[0]), ptr(amax), stream())
+        seeded = 1
+    call("fv_quantize_fp8_site", L.dtype_code(t.dtype), ptr(t), t.numel(), ptr(y), ptr(site[0]), seeded,
          ptr(ws), stream())
     site[1] = True
     return y, site[0][18:19].view(F32)
@@ -340,9 +354,10 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
     if cs.fp8:
         site = fp8_site(cs.conv, "x", x.device)
         x8, xdq = x8 if x8 is not None else quantize_fp8_site(x, site)
-        # the e4m3 operand stays for the fp8 weight gradient (its dq is the site's word 18, which
-        # only this forward's quantization wrote until the next forward)
-        cs.x8 = (x8, xdq)
+        # the e4m3 operand stays for the fp8 weight gradient with a COPY of its dq: the site's
+        # word 18 is rewritten by the site's next quantization (a second forward through this
+        # conv, or an eval forward, before this backward)
+        cs.x8 = (x8, xdq.clone())
         _timed("fwd", d, lambda: call("fv_conv2d_fwd_fp8_site", ctypes.byref(d), ptr(x8), ptr(site[0]), ptr(cs.wk),
                                       ptr(cs.wdq), ptr(bias), ptr(res), ptr(y), ptr(part), stream()))
         if CHECK is not None:

@@ -12,8 +12,10 @@ meaning, device-agnostic (the reference hard-codes .cuda(), utils.py:81-82, 93-9
                                       (models.py:1103, utils.py:175): trilinear, zeros padding
   occlusion_multiply                  fs * occlusion (models.py:1106)
 The 5-D feature volumes are NDHWC (torch.channels_last_3d); motion fields / grids stay fp32
-[N, ..., 3] as the reference's.  grid_sample's input gradient is accumulated with fp32 float
-atomics (as torch's own GPU kernel): its summation order is not fixed run to run.
+[N, ..., 3] as the reference's.  grid_sample's input gradient is a bucketed gather (output
+voxels counting-sorted by base input cell, each bucket then ordered by voxel index, each input
+cell summing its <= 8 neighbouring buckets): no float atomics and a fixed summation order, so
+it is bit-reproducible (torch's own GPU kernel uses float atomics).
 """
 from __future__ import annotations
 
@@ -80,11 +82,14 @@ class GridSample3dFn(torch.autograd.Function):
         go = gout.to(ctx.dtype).contiguous(memory_format=CL3)
         gin = ggrid = None
         if ctx.needs_input_grad[0]:
-            # input gradient by bucketed gather (no float atomics, no fp32 staging buffer)
+            # input gradient by bucketed gather (no float atomics, no fp32 staging buffer); an fp32
+            # input sampled in bf16 gets its gradient summed and stored in fp32
+            gd = F32 if ctx.in_dtype == F32 else ctx.dtype
+            gsrc = go if gd == ctx.dtype else go.to(gd)
             nws = L.query("fv_grid_sample3d_bwd_input_ws_bytes", B, Di, Hi, Wi, Do, Ho, Wo, ctx.group)
             ws = torch.empty(nws, dtype=torch.uint8, device=xb.device)
-            gin = torch.empty((Bi, C, Di, Hi, Wi), dtype=ctx.dtype, device=xb.device, memory_format=CL3)
-            call("fv_grid_sample3d_bwd_input", L.dtype_code(ctx.dtype), ptr(g32), ptr(go), B, Di, Hi, Wi, Do, Ho, Wo,
+            gin = torch.empty((Bi, C, Di, Hi, Wi), dtype=gd, device=xb.device, memory_format=CL3)
+            call("fv_grid_sample3d_bwd_input", L.dtype_code(gd), ptr(g32), ptr(gsrc), B, Di, Hi, Wi, Do, Ho, Wo,
                  C, ctx.group, ptr(gin), ptr(ws), stream())
             gin = gin.to(ctx.in_dtype)
         if ctx.needs_input_grad[1]:

@@ -250,6 +250,19 @@ int fv_conv2d_fwd_fp8_site(const fv_conv_desc* d, const uint8_t* x8, void* site,
                            void* stream);
 int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void* site, const uint8_t* wt,
                                 const float* wt_dq, void* dx, void* stream);
+/* Data-parallel global scaling (BASELINE config C5 at N > 1; the fp8 counterpart of SyncBN's
+ * global statistics, modules.py:120-121 under logger.py:54-58): with the deferred roll on, the
+ * *_site convs leave each call's amax in its site; once per step the caller gathers every
+ * site's in-flight amax (fv_fp8_sites_inflight, `sites` = device array of site pointers),
+ * all-reduces it with MAX (fv_comm_allreduce op 2) and rolls all sites at once
+ * (fv_fp8_sites_roll), so every rank quantizes with the same scales.  A site's first call
+ * takes the exact amax (fv_fp8_amax), all-reduced, as its seed (fv_fp8_site_seed) and then
+ * quantizes as a seeded site.  Process-wide switch. */
+int fv_fp8_set_deferred_roll(int on);
+int fv_fp8_amax(int dtype_in, const void* x, long count, float* amax, void* ws, void* stream);
+int fv_fp8_site_seed(void* site, const float* amax, void* stream);
+int fv_fp8_sites_inflight(int n, const uint64_t* sites, float* amax, void* stream);
+int fv_fp8_sites_roll(int n, const uint64_t* sites, const float* amax, void* stream);
 /* fp8 weight gradient of a 3x3 conv (k = (tap, ci), pixel-pair MFMA K = 128) from the e4m3 copies
  * of its input (x8, dequantisation factor x_dq) and output gradient (dy8, dy_dq) -- the operands
  * the fp8 forward and data gradient consumed: slab / bias slab as fv_conv2d_bwd_weight (sizes from
@@ -551,7 +564,7 @@ int fv_copy_h2d_async(void* dst, const void* src_pinned, size_t bytes, void* str
 typedef void* fv_comm_t;
 int fv_comm_unique_id(uint8_t out[128]);
 int fv_comm_init(const uint8_t id[128], int nranks, int rank, int device, fv_comm_t* comm);
-/* op: 0 = sum, 1 = average; dtype: FV_F32 / FV_BF16 / FV_F64 */
+/* op: 0 = sum, 1 = average, 2 = max; dtype: FV_F32 / FV_BF16 / FV_F64 */
 int fv_comm_allreduce(fv_comm_t comm, void* buf, size_t count, int dtype, int op,
                       void* stream);
 int fv_comm_allgather(fv_comm_t comm, const void* send, void* recv, size_t count_per_rank,

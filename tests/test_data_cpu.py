@@ -230,3 +230,19 @@ def test_uint8_conversion_is_img_as_float32():
     assert np.array_equal(D.u8_to_float(x), ref)
     assert int((x.astype(np.float32) / 255.0 != ref).sum()) == 126
     assert torch.equal(D.to_device_frames(torch.from_numpy(x), "cpu"), torch.from_numpy(ref))
+
+
+def test_resize_is_skimage_antialiased_constant_mode():
+    """augmentation.py:58-59 calls skimage resize with anti_aliasing=True, mode='constant' (skimage
+    is not importable here: parity unpinned, properties only).  A 1-pixel checkerboard shrunk 4x
+    comes out near its mean (the Gaussian pre-filter; plain bilinear sampling would alias to the
+    extremes); the zero fill darkens the border rows of a constant image when upscaling."""
+    cb = (np.indices((64, 64)).sum(0) % 2).astype(np.float32)[..., None]
+    small = A.resize(cb, (16, 16))
+    assert abs(small[4:-4, 4:-4].mean() - 0.5) < 0.02 and small[4:-4, 4:-4].std() < 0.05
+    one = np.ones((8, 8, 1), np.float32)
+    big = A.resize(one, (16, 16))
+    assert np.allclose(big[4:-4, 4:-4], 1.0) and big[0, 8, 0] < 0.9      # grid-constant: 0 outside
+    assert big.min() >= 0.0 and big.max() <= 1.0                         # clipped to [min(0, lo), hi]
+    q = A.resize((np.arange(16).reshape(4, 4, 1) * 10).astype(np.uint8), (8, 8), order=0)
+    assert q.dtype == np.float64                                         # preserve_range on integers

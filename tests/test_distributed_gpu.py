@@ -178,12 +178,12 @@ def test_dataparallel_syncbn_256_two_ranks_match_single_process(dtype_name):
     roundings such differences flip: the image, losses, BN running statistics and gradients
     must agree far inside the bf16-vs-fp32 deviation (~2e-2 image).
 
-    float8_e4m3fn (BASELINE config C5's combination, VERDICT r3 missing item 4): the fp8 convs
-    under DataParallel + SyncBN + the gradient all-reduce, each rank with its own delayed-scaling
-    sites.  A rank's first-step scale comes from its OWN two images' amax, so the e4m3 operands
-    (and everything after them) legitimately differ from the 4-image single process: checked at
-    fp8 tolerance against the single process and the fp32 oracle, and for identical averaged
-    gradients on both ranks."""
+    float8_e4m3fn (BASELINE config C5's combination): the fp8 convs under DataParallel + SyncBN
+    + the gradient all-reduce with GLOBAL delayed scaling: a site's first
+    call seeds its history with the exact amax all-reduced (MAX) over the ranks, and every step's
+    in-flight amax of all sites is all-reduced in one collective and rolled together
+    (DataParallel._sync_fp8), so both ranks quantize with the scales of the 4-image single
+    process: the same gates as bf16 (summation order only)."""
     import facevae_amd as fv
     from facevae_amd import distributed as D
     from oracle import facevae_cpu as O          # checker only
@@ -233,19 +233,6 @@ def test_dataparallel_syncbn_256_two_ranks_match_single_process(dtype_name):
           f"(1 process vs oracle: median {go[len(go) // 2]:.2e}); "
           + ", ".join(f"{k} {gdev[k]:.2e} (1 process vs oracle {gora[k]:.2e})" for k in top)
           + f"; BN running stats worst {max(bn.values()):.2e}")
-    if fp8:
-        assert dev["image_vs_1proc"] < 5e-2 and dev["R_vs_1proc"] < 1e-2 and dev["K_vs_1proc"] < 1e-3
-        assert dev["image_vs_oracle"] < 5e-2 and dev["R_vs_oracle"] < 1e-2
-        # measured (r4): median 0.42 against the single process, whose own median deviation from
-        # the fp32 oracle is of the same size -- on a first step from random init most gradients
-        # here (BN gamma / beta, the ResBlock convs behind a BN) are pixel sums that cancel to a
-        # few % of their terms, so the e4m3 rounding of dy / x (2^-4 relative) dominates them.
-        # Two scale choices are two independent draws of that noise: gated at twice its size
-        assert gv[len(gv) // 2] < 2 * go[len(go) // 2]
-        for k, v in gdev.items():
-            assert v < max(0.25, 2 * gora[k]), (k, v, gora[k])
-        assert max(bn.values()) < 5e-3
-        return
     # (both runs take the same kernels: at 2 and 4 images the latent 256-channel convs are on the
     # 128-co tiles of conv.hip halo3_bn, AFE.down2 on its 256-co tile)
     # measured (r3): forward bit-identical (image 0.0, BN running stats 0.0), K 5e-8; gradients
@@ -257,10 +244,14 @@ def test_dataparallel_syncbn_256_two_ranks_match_single_process(dtype_name):
     # gradient, and for such a sum at twice its own single-process-vs-fp32-oracle deviation
     # (the bf16 floor of that key)
     assert dev["image_vs_1proc"] < 1e-5 and dev["R_vs_1proc"] < 1e-5 and dev["K_vs_1proc"] < 1e-5
-    assert dev["image_vs_oracle"] < 2e-2 and dev["R_vs_oracle"] < 1e-3
+    assert dev["image_vs_oracle"] < (5e-2 if fp8 else 2e-2) and dev["R_vs_oracle"] < (1e-2 if fp8 else 1e-3)
     assert gv[len(gv) // 2] < 1e-2
+    # fp8 (measured r5): forward bit-identical, gradient median 6.2e-3; the keys above 3e-2 are
+    # sums whose e4m3 floor is itself 0.2-0.75 (Generator.in_conv's weight: 7.1e-2 against a
+    # 0.75 single-process-vs-oracle deviation; the residual-stream biases) -- two summation
+    # orders of the fp64 BN sums flip a few e4m3 roundings of dy, gated at twice that floor
     for k, v in gdev.items():
-        assert v <= 3e-2 or (residual_sum_bias(k) and v <= 2 * gora[k]), (k, v, gora[k])
+        assert v <= 3e-2 or ((fp8 or residual_sum_bias(k)) and v <= 2 * gora[k]), (k, v, gora[k])
     assert max(bn.values()) < 1e-5
 
 

@@ -61,3 +61,4 @@ def test_res_schedules_bit_identical(case, monkeypatch):
         assert torch.equal(y, y0), f"schedule {s}: forward differs"
         assert torch.equal(p, p0), f"schedule {s}: BN records differ"
         assert torch.equal(dx, dx0), f"schedule {s}: data gradient differs"
+

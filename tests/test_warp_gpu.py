@@ -2,8 +2,8 @@
 F.grid_sample on the CPU (same operands), the MFE motion assembly and the warped Generator
 against fixtures generated from the reference (tests/golden/warp.pt).
 
-Tolerances: fp32 1e-5 (kernels; grid_sample's input gradient sums each cell's buckets in a run-
-dependent order, 1e-5 relative), Generator fp32 mode 1e-4 (the north_star 1e-3 bar with
+Tolerances: fp32 1e-5 (kernels; grid_sample's input gradient sums each cell's buckets in voxel
+order, bit-reproducible: test_grid_sample3d_input_gradient_is_deterministic), Generator fp32 mode 1e-4 (the north_star 1e-3 bar with
 margin); bf16 storage of the sampled volume: 4e-3 rel-L2 / 1.6e-2 max-abs of max|ref|."""
 import os
 
@@ -195,3 +195,28 @@ def test_grid_sample3d_warp_shape_vs_torch(dtype):
     else:
         for a, b in ((out, ref), (xi.grad, ir.grad)):
             assert rel(a.float(), b) < 4e-3 and maxd(a.float(), b) <= 1.6e-2 * b.abs().max().item()
+
+
+@pytest.mark.parametrize("collapse", [False, True])
+def test_grid_sample3d_input_gradient_is_deterministic(collapse):
+    """The bucketed gather's buckets are sorted by voxel index (warp.hip gs_bucket_sort), so the
+    input gradient is bit-identical run to run; `collapse` squeezes every sample into a corner
+    cell (buckets of thousands of voxels: the heapsort path) -- still vs F.grid_sample."""
+    g = torch.Generator().manual_seed(11)
+    N, C, Di, Hi, Wi, Do, Ho, Wo = 2, 32, 4, 8, 16, 8, 16, 16
+    inp = torch.randn(N, C, Di, Hi, Wi, generator=g)
+    grid = (torch.rand(N, Do, Ho, Wo, 3, generator=g) - 0.5) * 2.2
+    if collapse:
+        grid = grid * 0.01 - 0.99
+    gout = torch.randn(N, C, Do, Ho, Wo, generator=g)
+    grads = []
+    for _ in range(3):
+        xi = inp.cuda().contiguous(memory_format=CL3).requires_grad_(True)
+        out = warp.GridSample3dFn.apply(xi, grid.cuda(), 1, torch.float32)
+        out.backward(gout.cuda())
+        torch.cuda.synchronize()
+        grads.append(xi.grad.cpu())
+    assert all(torch.equal(grads[0], t) for t in grads[1:])
+    ir = inp.clone().requires_grad_(True)
+    F.grid_sample(ir, grid, align_corners=True).backward(gout)
+    assert rel(grads[0], ir.grad) < 1e-5
