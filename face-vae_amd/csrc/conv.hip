@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[
 //       2iw + px) -- the stride-2 4x4 conv of conv_fwd_v2 MODE 3 without its 12 zero taps.
 // Weights (weight_prep_phase_kernel): unit u = chunk * 4 + q, [rows][32] per unit.
 template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, int SCH = 0, int MODE = 0>
-__global__ void __launch_bounds__(64 * WN * WM, WN * RN * 16 >= 256 ? 1 : 2)
+__global__ void __launch_bounds__(64 * WN * WM, (WN * RN * 16 >= 256 || WN == 1) ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   static_assert(MODE == 0 || !PRO, "phase modes: no prologue");
   static_assert(MODE != 1 || (WN == 4 && RN == 4), "sub-pixel forward: one phase of 64 channels per wave column");
@@ -1189,8 +1189,10 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   constexpr int PXB = 96;                                  // LDS bytes per halo pixel
   constexpr int HP = (TR + 2) * 66, HSL = HP * (PXB / 16), HQ = (HSL + 63) / 64, JH = (HQ + NW - 1) / NW;
   constexpr int HALO = HQ * 1024;
-  constexpr int QB = BN / 16, JB = QB / NW;
-  static_assert(QB % NW == 0, "weight pieces per wave");
+  // weight DMA pieces (16 rows) per tap: JB per wave, or one per wave for waves < QB when the
+  // co tile has fewer pieces than waves (the 64-channel tile on 8 waves)
+  constexpr int QB = BN / 16, JB = QB >= NW ? QB / NW : 1;
+  static_assert(QB % NW == 0 || NW % QB == 0, "weight pieces per wave");
   constexpr int BST = BN * 64, STG = 2 * BST, WOFF = NSB * STG;
   constexpr int PROB = PRO ? 2 * 256 * 4 : 0;              // scale / shift of <= 256 input channels
   constexpr int MAIN = WOFF + 2 * HALO + PROB, EPI = BM * BN * 2;
@@ -1279,7 +1281,8 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       const int u = 2 * j + h;
       const unsigned Bs = sbase + buf * STG + h * BST;
 #pragma unroll
-      for (int jb = 0; jb < JB; ++jb) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, (unsigned)u * ustep + jb * wstep);
+      for (int jb = 0; jb < JB; ++jb)
+        if (QB >= NW || wave < QB) dma16s(wr, Bs + (wave + jb * NW) * 1024, wbase, (unsigned)u * ustep + jb * wstep);
     }
   };
   // the step after whose barrier halo chunk c is issued: the last read of chunk c - 2 (same
@@ -1349,13 +1352,23 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
 
   // the ring and halo schedule of conv3_halo_fwd2 (nch even: no odd last tap)
   Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
-  auto bcnt = [&](int j) { return j < nsteps ? 2 * JB : 0; };
+  auto bcnt = [&](int j) { return j < nsteps && (QB >= NW || wave < QB) ? 2 * JB : 0; };
   issue_b(0, 0);
   issue_halo(0);
   issue_halo(1);
   for (int i = 1; i < NSB - 1; ++i)
     if (i < nsteps) issue_b(i, i);
-  wait_vm<0>();
+  // the first reads need weight stage 0 and halo chunk 0 only: the DMAs issued after them
+  // (chunk 1, first read at unit UPC; stages 1 .. NSB - 2) stay in flight past the prologue
+  // barrier and are waited for at the first step barriers (the loop's counted waits)
+  if constexpr (PRO) {
+    wait_vm<0>();                          // chunks 0 and 1 are transformed right after the barrier
+  } else {
+    const int nh1 = (JH - 1) + ((JH - 1) * NW + wave < HQ ? 1 : 0);
+    int later = nh1;
+    for (int i = 1; i < NSB - 1; ++i) later += bcnt(i);
+    wait_vm_dyn(later);
+  }
   __syncthreads();
   if constexpr (PRO) {
     xform(0);
@@ -3777,6 +3790,13 @@ bool use_subpix(const fv_conv_desc* d) {
   return pl % fwd_tile_v2(d->cout).bm == 0;
 }
 
+// the 64-channel co tile on conv3_halo_fwd3 (8 waves, 8-row tiles); FV_C64T=0 keeps
+// conv3_halo_fwd2<1, 4, 4, 4, 3> (A/B).  Read per call.
+static bool c64t_on() {
+  const char* e = getenv("FV_C64T");
+  return !(e && e[0] == '0');
+}
+
 // SIMD-partner schedule of the halo 3x3 kernels (conv3_halo_fwd3 / conv3_halo_fp8 SCH):
 // FV_RES_SCHED = 0 (prio flips, lockstep), 1 (static prio for waves 4-7), 2 (stagger), 3
 // (both); unset: the measured default of each kernel (dflt).  Read per call (tests compare the
@@ -4412,6 +4432,18 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   a.sigmoid = d->epi_sigmoid; a.nchw = d->out_nchw_f32;
   a.ntn = fv_cdiv(d->cout, t.bn);
   int st;
+  // the weight image the caller sized with fv_conv_wk_elems(d) (fv_conv_wt_elems for a data
+  // gradient: the same function of the transposed descriptor) must hold every row and k this
+  // launch's weight DMA reads: rows = the co tiles it covers, k = its K per row (r4 fault: a
+  // tile larger than the image read past its end)
+  const long wk_have = (long)fv_conv_wk_elems(d);
+  auto wext = [&](long rows, long kk, const char* what) {
+    if (rows * kk > wk_have) {
+      fv_set_error("conv %s: weight DMA extent %ld x %ld > weight image %ld elements", what, rows, kk, wk_have);
+      return FV_E_BADARG;
+    }
+    return FV_OK;
+  };
   if (use_c7n(d)) {
     FV_REQUIRE(!res, "out_conv kernel: no residual");
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
@@ -4424,6 +4456,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   // ResBlock conv) runs conv_fwd_v2, which reads the same plain [co][Kpad] weights (lay_of)
   const bool c64 = use_c64(d);
   if (c64 && !res && !a.spm) {
+    if ((st = wext(d->cout, kpad_of(3, 64), "c64"))) return st;
     const int nb = c64_bands(d);
     const int nblk = d->n * (d->w / 64) * (d->cout / 64) * nb;
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
@@ -4438,6 +4471,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     return fv_check_launch("conv2d_fwd_c74");
   }
   if (const int tr = halo_tr(d)) {
+    if ((st = wext(plan_tile(d).bn, kpad_of(7, d->cin), "halo7"))) return st;
     a.lgtw = 6;
     const int nblk = d->n * (d->h / tr) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
@@ -4476,6 +4510,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.nks = a.Kpad / BK2;
     a.ntn = fv_cdiv(d->cout, t2.bn);
     a.wphase = wrows(d->cout) * a.Kpad;
+    if ((st = wext(4L * a.ntn * t2.bn, a.Kpad, "subpix"))) return st;
     const int nblk2 = 4 * a.ntn * (a.P / t2.bm);
     const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
     st = launch_v2(a, 2, t2, 2, nblk2, (unsigned)xb, s);
@@ -4490,6 +4525,9 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     a.lgtw = 6;
     a.wus = wk_rows(d) * 64;
     a.ntn = d->cout / bn;
+    // stage-major: units of wk_rows(d) rows x 32; the tiles read rows [0, ntn * bn) of each
+    if ((st = wext(a.ntn * bn, 9L * d->cin, "halo3")) || (st = wext(wk_rows(d), 9L * d->cin, "halo3 units")))
+      return st;
     const int nblk = a.ntn * d->n * (d->h / 4) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
     // linear-halo pair-of-taps kernel (conv3_halo_fwd3) for the 256 / 128-channel co tiles;
@@ -4540,6 +4578,13 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
       hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 128) {
       hipLaunchKernelGGL((conv3_halo_fwd2<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
+    } else if (d->h % 8 == 0 && a.Cin % 64 == 0 && c64t_on()) {
+      // 64-channel co tile (AFE.down1's data gradient): 8 waves over 8 rows x 64 px, the
+      // linear-halo kernel (fwd2's XOR-swizzled halo addressing was its VALU
+      // limiter); waves 0-3 issue the 4 weight pieces of a tap
+      const int nblk8 = a.ntn * d->n * (d->h / 8) * (d->w / 64);
+      if (res_sched(2) == 2) hipLaunchKernelGGL((conv3_halo_fwd3<1, 8, 4, 4, 2, false, 2>), dim3(nblk8), dim3(512), 0, s, a, xb);
+      else hipLaunchKernelGGL((conv3_halo_fwd3<1, 8, 4, 4, 2, false, 0>), dim3(nblk8), dim3(512), 0, s, a, xb);
     } else {
       hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4, 3>), dim3(nblk), dim3(256), 0, s, a, xb);
     }
@@ -4550,6 +4595,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     const FwdTile t2 = fwd_tile_v2(d->cout);
     a.ntn = fv_cdiv(d->cout, t2.bn);
     a.nks = a.Kpad / BK2;            // 64-deep steps; the 32-deep kernels double it themselves
+    if ((st = wext((long)a.ntn * t2.bn, a.Kpad, "v2"))) return st;
     const int nblk2 = a.ntn * fv_cdiv(a.P, t2.bm);
     const long xb = (long)d->n * a.Hin * a.Win * d->cin * 2;
     st = launch_v2(a, d->ksize, t2, d->upsample, nblk2, (unsigned)xb, s);
@@ -4560,6 +4606,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     return fv_check_launch("conv2d_fwd_v2");
   }
   const int nblk = a.ntn * fv_cdiv(a.P, t.bm);
+  if ((st = wext((long)a.ntn * t.bn, a.Kpad, "v1"))) return st;
   st = d->dtype == FV_BF16 ? launch_fwd<bf16>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s)
                            : launch_fwd<float>(a, d->ksize, t, d->pro_act, d->upsample, nblk, s);
   if (st) {

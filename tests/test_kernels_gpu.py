@@ -70,6 +70,7 @@ CONV_CASES = [
     (3, 64, 128, 8, 64, False, False),
     (3, 256, 256, 4, 64, False, False),
     (3, 128, 64, 12, 128, False, False),
+    (3, 128, 64, 16, 64, False, False),    # 64-co tile on 8-row tiles (conv3_halo_fwd3<1, 8, ...>)
     # sub-pixel phases of upsample + 3x3 (bf16, power-of-two low-res side >= 16): UpBlock2D shapes
     (3, 128, 64, 16, 16, True, False),
     (3, 256, 128, 16, 32, True, False),

@@ -24,6 +24,7 @@ CASES = [
     (1, 256, 256, 8, 128),
     (2, 64, 128, 8, 64),
     (4, 128, 128, 12, 64),
+    (2, 128, 64, 16, 64),      # the 64-co tile (AFE.down1's data gradient shape)
 ]
 
 
