@@ -187,9 +187,16 @@ __device__ __forceinline__ f32x4 mma(const Frag<float>& a, const Frag<float>& b,
 // STAGED (bf16 NHWC only): after bias and BN partials the tile is rounded to bf16, written
 // to LDS (16-B chunks XOR-swizzled by pixel row) and stored with coalesced 16-B row
 // segments; the residual (if any) is added in that pass.  smem must hold BM*BN*2 bytes.
-template <typename T, int WN, int WM, int RN, int RM, bool STAGED = false>
+// mid (persistent kernels): with a callable other than NoMid, every thread reads its store
+// chunks back into registers, the block syncs (LDS free again) and mid() runs -- it issues
+// the next tile's LDS-DMA prologue -- before the stores, which then drain under that DMA.
+struct NoMid {
+  __device__ void operator()() const {}
+};
+template <typename T, int WN, int WM, int RN, int RM, bool STAGED = false, typename Mid = NoMid>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN][RM], char* smem, int co0, int p0,
-                                              int tm, int wn, int wm, int lane, int tid) {
+                                              int tm, int wn, int wm, int lane, int tid, Mid mid = Mid{}) {
+  constexpr bool kMid = !std::is_same<Mid, NoMid>::value;
   constexpr int NT = 64 * WN * WM;
   constexpr int BN = WN * RN * 16;
   constexpr int BM = WM * RM * 16;
@@ -200,7 +207,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
   // store loop they were serialised behind its stores: +22 us per res conv at 64x64, B=32)
   constexpr int SCPR = BN / 8, NRES = STAGED ? (BM * SCPR + NT - 1) / NT : 1;
   uint4 rpre[NRES];
-  if constexpr (STAGED) {
+  // (with a mid hook the residual chunks are loaded after the LDS read-back instead, when the
+  // accumulators are dead: their registers and the read-back's cannot all be live at once)
+  auto load_res = [&]() {
     if (a.res) {
 #pragma unroll
       for (int it = 0; it < NRES; ++it) {
@@ -214,7 +223,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
                                                       (long)out_pix(a, tp) * a.ldy + co);
       }
     }
-  }
+  };
+  if constexpr (STAGED && !kMid) load_res();
   float bv[RN][4];
 #pragma unroll
   for (int n = 0; n < RN; ++n)
@@ -302,6 +312,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
       }
     }
     __syncthreads();
+    uint4 vv[kMid ? NRES : 1];
+    if constexpr (kMid) {
+#pragma unroll
+      for (int it = 0; it < NRES; ++it) {
+        const int idx = tid + it * NT;
+        const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
+        if (idx < BM * CPR) vv[it] = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+      }
+      __syncthreads();
+      load_res();
+      mid();
+    }
+    auto chunk = [&](int it, int pl, int ch) -> uint4 {
+      if constexpr (kMid) return vv[it];
+      else return *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+    };
     if (!a.spm) {
       // the plain store pass (kept free of the record code below: +2-3 us per res conv)
 #pragma unroll
@@ -314,7 +340,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
         if (tp >= a.P || co >= a.Cout) continue;
         const int pix = out_pix(a, tp);
         Chunk8<bf16> v;
-        v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+        v.raw = chunk(it, pl, ch);
         T* yp = reinterpret_cast<T*>(a.y) + (long)pix * a.ldy + co;
         if (a.res) {
           Chunk8<bf16> r;
@@ -355,7 +381,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
       if (tp >= a.P || co >= a.Cout) continue;
       const int pix = out_pix(a, tp);
       Chunk8<bf16> v;
-      v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+      v.raw = chunk(it, pl, ch);
       T* yp = reinterpret_cast<T*>(a.y) + (long)pix * a.ldy + co;
       Chunk8<bf16> r;
       r.raw = rpre[it];
@@ -885,6 +911,17 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
   }
 }
 
+// wave-uniform count 0 .. 63 (gfx950's vmcnt range) -> the matching immediate
+template <int N = 63>
+__device__ __forceinline__ void wait_vm_upto(int n) {
+  if constexpr (N == 0) {
+    wait_vm<0>();
+  } else {
+    if (n >= N) wait_vm<N>();
+    else wait_vm_upto<N - 1>(n);
+  }
+}
+
 // Software-pipelined variant: a step is a PAIR of taps (64 k), the weight stage holds both
 // taps' 32-channel slices, and the loop is conv_fwd_v2's: the fragments of the step's second
 // tap are read while the first tap's MFMAs run and the barrier sits between the two MFMA
@@ -1070,9 +1107,11 @@ conv3_halo_fwd2(ConvArgs a, unsigned x_bytes) {
 // bias -> BN records -> bf16 through LDS -> 16-B stores to output pixel (2h + pa, 2w + pb).
 // BN records: one per (tile, wave row, phase) = RM * 16 output pixels, record index
 // ((tm * WM + wm) * 4 + wn) (stats_record_pixels: 128), so every output pixel is in one record.
-template <int WM, int RM>
+template <int WM, int RM, typename Mid = NoMid>
 __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[4][RM], char* smem, int tn, int n,
-                                                int h0, int w0, int tm, int wn, int wm, int lane, int tid) {
+                                                int h0, int w0, int tm, int wn, int wm, int lane, int tid,
+                                                Mid mid = Mid{}) {
+  constexpr bool kMid = !std::is_same<Mid, NoMid>::value;
   constexpr int RN = 4, NT = 64 * 4 * WM, BN = 256, BM = WM * RM * 16, CPR = BN / 8;
   const int lr = lane & 15, lh = lane >> 4;
   const int cb0 = tn * 64;
@@ -1124,6 +1163,17 @@ __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[
   __syncthreads();
   constexpr int NIT = BM * CPR / NT;
   static_assert(BM * CPR % NT == 0, "store pass");
+  uint4 vv[kMid ? NIT : 1];
+  if constexpr (kMid) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * NT;
+      const int pl = idx / CPR, ch = idx - (idx / CPR) * CPR;
+      vv[it] = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+    }
+    __syncthreads();
+    mid();
+  }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int idx = tid + it * NT;
@@ -1131,7 +1181,8 @@ __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[
     const int ph = ch >> 3, co = cb0 + (ch & 7) * 8;
     const int oh = 2 * (h0 + (pl >> 6)) + (ph >> 1), ow = 2 * (w0 + (pl & 63)) + (ph & 1);
     Chunk8<bf16> v;
-    v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
+    if constexpr (kMid) v.raw = vv[it];
+    else v.raw = *reinterpret_cast<const uint4*>(smem + pl * BN * 2 + ((ch ^ (pl & (CPR - 1))) << 4));
     v.store(reinterpret_cast<bf16*>(a.y) + ((long)(n * a.Ho + oh) * a.Wo + ow) * a.ldy + co);
   }
 }
@@ -1177,9 +1228,17 @@ __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[
 //       taps at window (1 - py + a, 1 - px + b); the halo DMA gathers plane pixels (2ih + py,
 //       2iw + px) -- the stride-2 4x4 conv of conv_fwd_v2 MODE 3 without its 12 zero taps.
 // Weights (weight_prep_phase_kernel): unit u = chunk * 4 + q, [rows][32] per unit.
-template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, int SCH = 0, int MODE = 0>
+//
+// PERS (persistent, one block per CU): the block walks the tiles v = blockIdx.x + k * gridDim.x
+// (the tiles its XCD runs in the one-tile-per-block grid of ntiles blocks).  After a tile's
+// epilogue staged its output in LDS and read it back into registers, the next tile's
+// prologue DMA (weight stage 0, halo chunks 0 / 1) is issued and THEN the stores: every CU
+// reaches its epilogue at the same time, so a tile's 128 KB of stores (HBM-bound as a burst)
+// drain under the next tile's prologue instead of after it.
+template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, int SCH = 0, int MODE = 0, bool PERS = false>
 __global__ void __launch_bounds__(64 * WN * WM, (WN * RN * 16 >= 256 || WN == 1) ? 1 : 2)
-conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
+conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
+  static_assert(!(PERS && PRO), "persistent tiles: no staged prologue");
   static_assert(MODE == 0 || !PRO, "phase modes: no prologue");
   static_assert(MODE != 1 || (WN == 4 && RN == 4), "sub-pixel forward: one phase of 64 channels per wave column");
   constexpr int UPC = MODE ? 4 : 9;                        // tap units per 32-channel chunk
@@ -1204,40 +1263,67 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave % WN, wm = wave / WN;
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int tn = lid % a.ntn, tm = lid / a.ntn;
+  const int ntl = PERS ? ntiles : (int)gridDim.x;
+  // tile of launch index v: the XCD-aware bijective remap (consecutive tiles on one XCD)
+  auto remap = [&](int v) {
+    const int q8 = ntl / 8, r8 = ntl % 8, x8 = v % 8;
+    return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + v / 8;
+  };
   const int tiles_w = a.W >> 6, tiles_h = a.H / TR;
-  const int tw = tm % tiles_w, th = (tm / tiles_w) % tiles_h, n = tm / (tiles_w * tiles_h);
-  const int co0 = tn * BN;
-  const int p0 = (n * a.H + th * TR) * a.W + tw * 64;
-
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0, 0x7fffffff, 0x00020000);
   const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
   const int lrow = lane >> 2, lchk = lane & 3;
+  // Weights are stage-major (weight_prep_body smaj): tap unit u = c * 9 + t is a [Cout][32]
+  // block, so the 16 rows of a DMA piece are one contiguous KB (8 whole 128-B lines; the
+  // [co][Kpad] rows made every piece 16 separate 64-B segments).  Piece jb of unit u starts at
+  // u * ustep + (co0 + (wave + jb * NW) * 16) * 64; the lane's source chunk carries the LDS
+  // chunk swizzle.
+  const unsigned wstep = (unsigned)(NW * 16 * 64);
+  const unsigned ustep = (unsigned)a.wus;
+  const int nch = a.Cin >> 5, nsteps = UPC * nch / 2;
+  const int cpp = a.Cin >> 7;                               // MODE 2: chunks per phase plane
 
+  struct Tile {
+    int tn, tm, tw, th, n, co0, p0;
+    unsigned wbase;
+  };
+  auto tile_of = [&](int v) {
+    Tile t;
+    const int lid = remap(v);
+    t.tn = lid % a.ntn;
+    t.tm = lid / a.ntn;
+    t.tw = t.tm % tiles_w;
+    t.th = (t.tm / tiles_w) % tiles_h;
+    t.n = t.tm / (tiles_w * tiles_h);
+    t.co0 = t.tn * BN;
+    t.p0 = (t.n * a.H + t.th * TR) * a.W + t.tw * 64;
+    t.wbase = (unsigned)((t.co0 + wave * 16 + lrow) * 64 + ((lchk ^ rswz<bf16>(lrow)) << 4));
+    return t;
+  };
   // halo slots of this wave: slot k = 16-B chunk k % 6 of halo pixel k / 6 (chunks 4, 5 pad)
   unsigned hoff[JH];
   unsigned hval = 0;             // PRO: bit j = slot j holds image data (a transform target)
   int hcb[PRO ? JH : 1];         // PRO: the slot's channel offset in a 32-channel chunk
+  auto mk_hoff = [&](const Tile& t) {
+    hval = 0;
 #pragma unroll
-  for (int j = 0; j < JH; ++j) {
-    const int k = (wave + j * NW) * 64 + lane;
-    const int hp = k / 6, ch = k - (k / 6) * 6;
-    const int hr = hp / 66, hc = hp - (hp / 66) * 66;
-    const int ih = th * TR + hr - 1, iw = tw * 64 + hc - 1;
-    const bool ok = hp < HP && ch < 4 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-    if constexpr (MODE == 2)     // plane (0, 0) pixel of dy; the chunk's plane is a uniform offset
-      hoff[j] = ok ? (unsigned)((((n * a.Hin + 2 * ih) * a.Win + 2 * iw) * a.K + (ch << 3)) * 2) : 0x80000000u;
-    else
-      hoff[j] = ok ? (unsigned)(((((n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
-    if constexpr (PRO) {
-      hval |= ok ? 1u << j : 0u;
-      hcb[j] = ch * 8;
+    for (int j = 0; j < JH; ++j) {
+      const int k = (wave + j * NW) * 64 + lane;
+      const int hp = k / 6, ch = k - (k / 6) * 6;
+      const int hr = hp / 66, hc = hp - (hp / 66) * 66;
+      const int ih = t.th * TR + hr - 1, iw = t.tw * 64 + hc - 1;
+      const bool ok = hp < HP && ch < 4 && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      if constexpr (MODE == 2)     // plane (0, 0) pixel of dy; the chunk's plane is a uniform offset
+        hoff[j] = ok ? (unsigned)((((t.n * a.Hin + 2 * ih) * a.Win + 2 * iw) * a.K + (ch << 3)) * 2) : 0x80000000u;
+      else
+        hoff[j] = ok ? (unsigned)(((((t.n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
+      if constexpr (PRO) {
+        hval |= ok ? 1u << j : 0u;
+        hcb[j] = ch * 8;
+      }
     }
-  }
+  };
   float* const sst = reinterpret_cast<float*>(smem + WOFF + 2 * HALO);    // PRO: [scale 256][shift 256]
   if constexpr (PRO) {
     for (int i = tid; i < a.Cin; i += NW * 64) {
@@ -1265,17 +1351,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       }
     }
   };
-  // Weights are stage-major (weight_prep_body smaj): tap unit u = c * 9 + t is a [Cout][32]
-  // block, so the 16 rows of a DMA piece are one contiguous KB (8 whole 128-B lines; the
-  // [co][Kpad] rows made every piece 16 separate 64-B segments).  Piece jb of unit u starts at
-  // u * ustep + (co0 + (wave + jb * NW) * 16) * 64; the lane's source chunk carries the LDS
-  // chunk swizzle.
-  const unsigned wbase = (unsigned)((co0 + wave * 16 + lrow) * 64 + ((lchk ^ rswz<bf16>(lrow)) << 4));
-  const unsigned wstep = (unsigned)(NW * 16 * 64);
-  const unsigned ustep = (unsigned)a.wus;
-  const int nch = a.Cin >> 5, nsteps = UPC * nch / 2;
-  const int cpp = a.Cin >> 7;                               // MODE 2: chunks per phase plane
-  auto issue_b = [&](int j, int buf) {
+  auto issue_b = [&](unsigned wbase, int j, int buf) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int u = 2 * j + h;
@@ -1296,12 +1372,20 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
       return (unsigned)(c * 64);
     }
   };
-  // one weight DMA piece q (0 .. 2 JB - 1) of stage j: tap half q / JB, row piece q % JB
   auto issue_halo = [&](int c) {
     const unsigned Hs = sbase + WOFF + (c & 1) * HALO;
 #pragma unroll
     for (int j = 0; j < JH; ++j)
       if (j < JH - 1 || wave + j * NW < HQ) dma16s(xr, Hs + (wave + j * NW) * 1024, hoff[j], halo_soff(c));
+  };
+  auto bcnt = [&](int j) { return j < nsteps && (QB >= NW || wave < QB) ? 2 * JB : 0; };
+  // a tile's prologue DMA: weight stage 0, halo chunks 0 / 1, stages 1 .. NSB - 2
+  auto issue_prologue = [&](const Tile& t) {
+    issue_b(t.wbase, 0, 0);
+    issue_halo(0);
+    issue_halo(1);
+    for (int i = 1; i < NSB - 1; ++i)
+      if (i < nsteps) issue_b(t.wbase, i, i);
   };
 
   const int lr = lane & 15, lh = lane >> 4;
@@ -1334,119 +1418,148 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes) {
 #pragma unroll
     for (int m = 0; m < RM; ++m) fb[m].lds(smem + pb + (((m * 16) >> 6) * 66 + ((m * 16) & 63)) * PXB);
   };
-  f32x4 acc[RN][RM];
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
-    if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < RN; ++i)
-#pragma unroll
-      for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
-    if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(0);
-  };
   const bool hi = wave >= NW / 2;                  // the second-dispatched wave of each SIMD
   const bool stag = (SCH & 2) && hi;
 
-  // the ring and halo schedule of conv3_halo_fwd2 (nch even: no odd last tap)
-  Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
-  auto bcnt = [&](int j) { return j < nsteps && (QB >= NW || wave < QB) ? 2 * JB : 0; };
-  issue_b(0, 0);
-  issue_halo(0);
-  issue_halo(1);
-  for (int i = 1; i < NSB - 1; ++i)
-    if (i < nsteps) issue_b(i, i);
-  // the first reads need weight stage 0 and halo chunk 0 only: the DMAs issued after them
-  // (chunk 1, first read at unit UPC; stages 1 .. NSB - 2) stay in flight past the prologue
-  // barrier and are waited for at the first step barriers (the loop's counted waits)
-  if constexpr (PRO) {
-    wait_vm<0>();                          // chunks 0 and 1 are transformed right after the barrier
-  } else {
-    const int nh1 = (JH - 1) + ((JH - 1) * NW + wave < HQ ? 1 : 0);
-    int later = nh1;
-    for (int i = 1; i < NSB - 1; ++i) later += bcnt(i);
-    wait_vm_dyn(later);
-  }
-  __syncthreads();
-  if constexpr (PRO) {
-    xform(0);
-    xform(1);
+  int v = blockIdx.x;
+  Tile t = tile_of(v);
+  mk_hoff(t);
+  issue_prologue(t);
+  bool first = true;
+  for (;;) {
+    // the first reads need weight stage 0 and halo chunk 0 only: on the first tile the DMAs
+    // issued after them (chunk 1, first read at unit UPC; stages 1 .. NSB - 2) stay in flight
+    // past the prologue barrier and are waited for at the first step barriers; a later tile's
+    // prologue was issued before the previous tile's stores, so all is waited for
+    if (PRO) {
+      wait_vm<0>();                        // chunks 0 and 1 are transformed right after the barrier
+    } else {
+      const int nh1 = (JH - 1) + ((JH - 1) * NW + wave < HQ ? 1 : 0);
+      int later = nh1;
+      for (int i = 1; i < NSB - 1; ++i) later += bcnt(i);
+      // a later tile: the previous epilogue's stores were issued after this prologue (vmcnt
+      // retires in issue order on gfx9), so they may stay in flight too: NRES (+ 4 record
+      // stores with store-pass records) per wave
+      if (!first) later += BM * BN / (8 * NW * 64) + (MODE != 1 && a.spm ? 4 : 0);
+      wait_vm_upto(later);
+    }
     __syncthreads();
-  }
-  FV_DIAG_PROLOGUE();
-  int pend = 0;
-  if (NSB - 1 < nsteps) {
-    issue_b(NSB - 1, NSB - 1);
-    pend = bcnt(NSB - 1);
-  }
-  load_frags(fa0, fb0, 0, 0);
-  int hn = 2, hstep = halo_step(2);
-  int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
-  int bj = 0;
-  if constexpr (SCH & 1) {
-    if (hi) __builtin_amdgcn_s_setprio(1);
-  }
-  // barrier of step j: stage j + 1 landed (own DMAs counted, then the barrier publishes them),
-  // and every wave's reads of stage j are done (its buffer is re-filled right after)
-  auto step_barrier = [&]() {
-    FV_DIAG_WAIT_BEGIN();
-    if constexpr (NSB == 2) wait_vm<0>();
-    else if (pend == 2 * JB) wait_vm<2 * JB>();
-    else wait_vm_dyn(pend);
-    wait_lgkm0();
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    FV_DIAG_WAIT_END();
-  };
-  // stagger (SCH bit 1): waves NW/2.. take the barrier BEFORE the MFMAs of tap 2j (their
-  // fragments are in registers), the others after; every read still falls in the same barrier
-  // interval as in the lockstep order, so the ring / halo hazards are unchanged.
-  // The last step is peeled: with it inside the loop (no barrier, no next-tap reads) the
-  // wait-count pass merged its state into the loop's second MFMA cluster and made that
-  // cluster wait for the next tap's fragment reads every step (lgkmcnt(7) .. (0)).
-  for (int j = 0; j + 1 < nsteps; ++j) {
-    load_frags(fa1, fb1, 2 * j + 1, bj);
-    if constexpr ((SCH & 2) != 0) {
-      if (stag) step_barrier();
-    }
-    mfma_all(fa0, fb0);
-    const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
-    if (!stag) step_barrier();
-    if (hn < nch && j == hstep) {
-      issue_halo(hn);
-      if constexpr (PRO) {
-        xc = hn;
-        xstep = j + 1 + (wave >= 4 ? 1 : 0);   // landed by the next step's barrier
-      }
-      ++hn;
-      hstep = halo_step(hn);
-    }
-    pend = 0;
-    if (j + NSB < nsteps) {
-      issue_b(j + NSB, bj);
-      pend = bcnt(j + NSB);
-    }
-    load_frags(fa0, fb0, 2 * j + 2, bn1);
-    FV_DIAG_ISSUE_END();
-    mfma_all(fa1, fb1);
     if constexpr (PRO) {
-      if (j == xstep) xform(xc);     // published by the next step's barrier
+      xform(0);
+      xform(1);
+      __syncthreads();
     }
-    bj = bn1;
+    FV_DIAG_PROLOGUE();
+    f32x4 acc[RN][RM];
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[i][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mfma_all = [&](const Frag<bf16> (&fa)[RN], const Frag<bf16> (&fb)[RM]) {
+      if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < RN; ++i)
+#pragma unroll
+        for (int m = 0; m < RM; ++m) acc[i][m] = mma(fa[i], fb[m], acc[i][m]);
+      if constexpr (!(SCH & 1)) __builtin_amdgcn_s_setprio(0);
+    };
+
+    // the ring and halo schedule of conv3_halo_fwd2 (nch even: no odd last tap)
+    Frag<bf16> fa0[RN], fb0[RM], fa1[RN], fb1[RM];
+    int pend = 0;
+    if (NSB - 1 < nsteps) {
+      issue_b(t.wbase, NSB - 1, NSB - 1);
+      pend = bcnt(NSB - 1);
+    }
+    load_frags(fa0, fb0, 0, 0);
+    int hn = 2, hstep = halo_step(2);
+    int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
+    int bj = 0;
+    if constexpr (SCH & 1) {
+      if (hi) __builtin_amdgcn_s_setprio(1);
+    }
+    // barrier of step j: stage j + 1 landed (own DMAs counted, then the barrier publishes them),
+    // and every wave's reads of stage j are done (its buffer is re-filled right after)
+    auto step_barrier = [&]() {
+      FV_DIAG_WAIT_BEGIN();
+      if constexpr (NSB == 2) wait_vm<0>();
+      else if (pend == 2 * JB) wait_vm<2 * JB>();
+      else wait_vm_dyn(pend);
+      wait_lgkm0();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      FV_DIAG_WAIT_END();
+    };
+    // stagger (SCH bit 1): waves NW/2.. take the barrier BEFORE the MFMAs of tap 2j (their
+    // fragments are in registers), the others after; every read still falls in the same barrier
+    // interval as in the lockstep order, so the ring / halo hazards are unchanged.
+    // The last step is peeled: with it inside the loop (no barrier, no next-tap reads) the
+    // wait-count pass merged its state into the loop's second MFMA cluster and made that
+    // cluster wait for the next tap's fragment reads every step (lgkmcnt(7) .. (0)).
+    for (int j = 0; j + 1 < nsteps; ++j) {
+      load_frags(fa1, fb1, 2 * j + 1, bj);
+      if constexpr ((SCH & 2) != 0) {
+        if (stag) step_barrier();
+      }
+      mfma_all(fa0, fb0);
+      const int bn1 = bj + 1 == NSB ? 0 : bj + 1;
+      if (!stag) step_barrier();
+      if (hn < nch && j == hstep) {
+        issue_halo(hn);
+        if constexpr (PRO) {
+          xc = hn;
+          xstep = j + 1 + (wave >= 4 ? 1 : 0);   // landed by the next step's barrier
+        }
+        ++hn;
+        hstep = halo_step(hn);
+      }
+      pend = 0;
+      if (j + NSB < nsteps) {
+        issue_b(t.wbase, j + NSB, bj);
+        pend = bcnt(j + NSB);
+      }
+      load_frags(fa0, fb0, 2 * j + 2, bn1);
+      FV_DIAG_ISSUE_END();
+      mfma_all(fa1, fb1);
+      if constexpr (PRO) {
+        if (j == xstep) xform(xc);     // published by the next step's barrier
+      }
+      bj = bn1;
+    }
+    load_frags(fa1, fb1, 2 * nsteps - 1, bj);
+    mfma_all(fa0, fb0);
+    mfma_all(fa1, fb1);
+    if constexpr (SCH & 1) __builtin_amdgcn_s_setprio(0);
+    FV_DIAG_LOOP_END();
+    __syncthreads();
+    const int vn = v + (int)gridDim.x;
+    const bool nxt = PERS && vn < ntl;
+    const Tile cur = t;
+    if constexpr (PERS) {
+      // the next tile's geometry and prologue DMA, issued between the epilogue's LDS read-back
+      // and its stores (conv_epilogue / subpix_epilogue `mid`)
+      auto mid = [&]() {
+        if (nxt) {
+          t = tile_of(vn);
+          mk_hoff(t);
+          issue_prologue(t);
+        }
+      };
+      if constexpr (MODE == 1)
+        subpix_epilogue<WM, RM>(a, acc, smem, cur.tn, cur.n, cur.th * TR, cur.tw * 64, cur.tm, wn, wm, lane, tid, mid);
+      else
+        conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, cur.co0, cur.p0, cur.tm, wn, wm, lane, tid, mid);
+    } else {
+      if constexpr (MODE == 1)
+        subpix_epilogue<WM, RM>(a, acc, smem, cur.tn, cur.n, cur.th * TR, cur.tw * 64, cur.tm, wn, wm, lane, tid);
+      else
+        conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, cur.co0, cur.p0, cur.tm, wn, wm, lane, tid);
+    }
+    FV_DIAG_END();
+    if (!nxt) break;
+    v = vn;
+    first = false;
   }
-  load_frags(fa1, fb1, 2 * nsteps - 1, bj);
-  mfma_all(fa0, fb0);
-  mfma_all(fa1, fb1);
-  if constexpr (SCH & 1) __builtin_amdgcn_s_setprio(0);
-  FV_DIAG_LOOP_END();
-  __syncthreads();
-  if constexpr (MODE == 1)
-    subpix_epilogue<WM, RM>(a, acc, smem, tn, n, th * TR, tw * 64, tm, wn, wm, lane, tid);
-  else
-    conv_epilogue<bf16, WN, WM, RN, RM, true>(a, acc, smem, co0, p0, tm, wn, wm, lane, tid);
-  FV_DIAG_END();
 }
 
 // ----------------------------------------------------------------------------------------
@@ -3799,7 +3912,8 @@ static bool c64t_on() {
 
 // SIMD-partner schedule of the halo 3x3 kernels (conv3_halo_fwd3 / conv3_halo_fp8 SCH):
 // FV_RES_SCHED = 0 (prio flips, lockstep), 1 (static prio for waves 4-7), 2 (stagger), 3
-// (both); unset: the measured default of each kernel (dflt).  Read per call (tests compare the
+// (both); unset: the measured default of each kernel (dflt).  conv3_halo_fwd3 keeps 0 and 2
+// (1 / 3 measured no better, below).  Read per call (tests compare the
 // schedules bit for bit in one process).  r5, alternating convbench runs on one box, B=32 bf16
 // res fwd / dgrad: 0: 130 / 122, 1: 124 / 118, 2: 120 / 115, 3: 126 / 119 us; B=64 fp8 res
 // fwd / dgrad: 0: 175 / 166, 1: 173 / 163, 2: 172 / 155, 3: 165 / 155 us.
@@ -4404,6 +4518,52 @@ static int sr_geometry(const fv_conv_desc* d, int* bp) {
   return (int)(P / 256 * nw);
 }
 
+extern "C++" {
+// CUs of the current device (persistent grids), queried once
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+// persistent tiles for conv3_halo_fwd3 (PERS); FV_PERS=0 launches one block per tile (A/B).
+// Read per call.
+static bool pers_on() {
+  const char* e = getenv("FV_PERS");
+  return !(e && e[0] == '0');
+}
+// one conv3_halo_fwd3 launch over ntiles tiles: schedule SCH 2 (stagger) unless FV_RES_SCHED
+// says 0 / 1 (-> 0), persistent (one block per CU) when there are more tiles than CUs
+template <int WN, int WM, int RN, int RM, int NSB, int MODE>
+static void launch_h3(int ntiles, hipStream_t s, const ConvArgs& a, unsigned xb) {
+  const int sch = res_sched(2) >= 2 ? 2 : 0;
+  // FV_PERS_GRID=k caps the persistent grid at k blocks (tests: several tiles per block at
+  // small shapes)
+  const char* e = getenv("FV_PERS_GRID");
+  const int cap = (e && atoi(e) > 0) ? atoi(e) : cu_count();
+  // (the 256-row co tiles spill ~130 registers in the persistent form -- the epilogue's
+  // read-back beside the carried tile state -- and ran res fwd 120 -> 166 us, r5; kept to the
+  // smaller co tiles: AFE.down1's data gradient 366 -> 348 us)
+  const bool pers = WN * RN * 16 < 256 && pers_on() && ntiles > cap;
+  const dim3 g(pers ? cap : ntiles), b(64 * WN * WM);
+  if constexpr (WN * RN * 16 < 256) {
+    if (pers) {
+      if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 2, MODE, true>), g, b, 0, s, a, xb, ntiles);
+      else hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 0, MODE, true>), g, b, 0, s, a, xb, ntiles);
+      return;
+    }
+  }
+  {
+    if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 2, MODE, false>), g, b, 0, s, a, xb, ntiles);
+    else hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 0, MODE, false>), g, b, 0, s, a, xb, ntiles);
+  }
+}
+}  // extern "C++"
+
 static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
                     const float* psc, const float* psh, const void* res, void* y, float* stats,
                     hipStream_t s, const fv_store_reduce* sr = nullptr) {
@@ -4493,10 +4653,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     const unsigned xb = (unsigned)((long)d->n * a.H * a.W * d->cin * 2);
     // the weight DMA of the last unit ends inside the image the queries size
     FV_REQUIRE((long)4 * (d->cin / 32) * a.wus / 2 <= phase_wk_elems(d), "sub-pixel halo conv: weight image");
-    if (res_sched(2) == 2)
-      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
-    else
-      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 0, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
+    launch_h3<4, 2, 4, 8, 2, 1>(nblk, s, a, xb);
     return fv_check_launch("conv2d_fwd_subpix_halo");
   }
   if (use_subpix(d)) {
@@ -4560,20 +4717,10 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // 160-162 us, step +0.17 ms.)
     if (d->pro_act) {
       FV_REQUIRE(bn == 256 && psc && psh, "staged BN prologue: bad arguments");
-      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb);
+      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb, nblk);
     } else if (bn >= 128 && a.Cin % 64 == 0) {
-      const int sch = res_sched(2);
-      if (bn == 256) {
-        if (sch == 1) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
-        else if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
-        else if (sch == 3) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
-        else hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
-      } else {
-        if (sch == 1) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 1>), dim3(nblk), dim3(512), 0, s, a, xb);
-        else if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
-        else if (sch == 3) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
-        else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3>), dim3(nblk), dim3(512), 0, s, a, xb);
-      }
+      if (bn == 256) launch_h3<4, 2, 4, 8, 2, 0>(nblk, s, a, xb);
+      else launch_h3<2, 4, 4, 4, 3, 0>(nblk, s, a, xb);
     } else if (bn == 256) {
       hipLaunchKernelGGL((conv3_halo_fwd2<4, 2, 4, 8, 2>), dim3(nblk), dim3(512), 0, s, a, xb);
     } else if (bn == 128) {
@@ -4583,8 +4730,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
       // linear-halo kernel (fwd2's XOR-swizzled halo addressing was its VALU
       // limiter); waves 0-3 issue the 4 weight pieces of a tap
       const int nblk8 = a.ntn * d->n * (d->h / 8) * (d->w / 64);
-      if (res_sched(2) == 2) hipLaunchKernelGGL((conv3_halo_fwd3<1, 8, 4, 4, 2, false, 2>), dim3(nblk8), dim3(512), 0, s, a, xb);
-      else hipLaunchKernelGGL((conv3_halo_fwd3<1, 8, 4, 4, 2, false, 0>), dim3(nblk8), dim3(512), 0, s, a, xb);
+      launch_h3<1, 8, 4, 4, 2, 0>(nblk8, s, a, xb);
     } else {
       hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4, 3>), dim3(nblk), dim3(256), 0, s, a, xb);
     }
@@ -4719,14 +4865,8 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
     const int nblk = a.ntn * d->n * (a.H / 4) * (a.W / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cout * 2);
     FV_REQUIRE((long)(a.Cin / 32) * 4 * a.wus / 2 <= phase_wt_elems(d), "low-res halo dgrad: weight image");
-    const int sch = res_sched(2);
-    if (bn == 256) {
-      if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
-      else hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, false, 0, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
-    } else {
-      if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 2, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
-      else hipLaunchKernelGGL((conv3_halo_fwd3<2, 4, 4, 4, 3, false, 0, 2>), dim3(nblk), dim3(512), 0, (hipStream_t)stream, a, xb);
-    }
+    if (bn == 256) launch_h3<4, 2, 4, 8, 2, 2>(nblk, (hipStream_t)stream, a, xb);
+    else launch_h3<2, 4, 4, 4, 3, 2>(nblk, (hipStream_t)stream, a, xb);
     return fv_check_launch("conv2d_bwd_data_lowres_halo");
   }
   if (use_dgrad_lowres(d)) {

@@ -28,9 +28,13 @@ CASES = [
 ]
 
 
-def _run(case, sched, monkeypatch):
+def _run(case, sched, monkeypatch, pers_grid=None):
     N, cin, cout, H, W = case
     monkeypatch.setenv("FV_RES_SCHED", str(sched))
+    if pers_grid is None:
+        monkeypatch.delenv("FV_PERS_GRID", raising=False)
+    else:
+        monkeypatch.setenv("FV_PERS_GRID", str(pers_grid))
     g = gen(300 + cin + H)
     x = torch.randn(N, cin, H, W, generator=g)
     w = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
@@ -62,4 +66,9 @@ def test_res_schedules_bit_identical(case, monkeypatch):
         assert torch.equal(y, y0), f"schedule {s}: forward differs"
         assert torch.equal(p, p0), f"schedule {s}: BN records differ"
         assert torch.equal(dx, dx0), f"schedule {s}: data gradient differs"
+    # persistent tiles (FV_PERS_GRID: a grid of 3 blocks walks every tile, the next tile's
+    # prologue DMA issued under the previous epilogue's stores): the same bits
+    for s in (0, 2):
+        _, _, _, _, y, p, dx = _run(case, s, monkeypatch, pers_grid=3)
+        assert torch.equal(y, y0) and torch.equal(p, p0) and torch.equal(dx, dx0), f"persistent, schedule {s}"
 
