@@ -104,12 +104,13 @@ step_cbab() {
 step_convpmc() {
   local C="$R/tools/convbench.py --iters 5 ${CB_ARGS:---layers res --only fwd,wgrad}" i=0 c
   for c in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_VALU SQ_INSTS_SALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_MFMA SQ_WAVES"; do
     i=$((i+1))
     (cd /tmp && timeout -s KILL 200 rocprofv3 --pmc $c --output-format csv -d $O/cpmc_p$i -o run -- \
       python3 $C > $O/cpmc_p$i.log 2>&1) || { echo "pmc pass $i failed"; tail -5 $O/cpmc_p$i.log; return 1; }
   done
-  python tools/pmc_sq.py $O/cpmc_p1 $O/cpmc_p2 | tee $O/convpmc.txt
+  python tools/pmc_sq.py $O/cpmc_p1 $O/cpmc_p2 $O/cpmc_p3 | tee $O/convpmc.txt
 }
 
 step_c3pmc() {   # SQ + HBM counter passes over tools/conv3dbench.py ($C3_ARGS)

@@ -30,8 +30,9 @@ import re
 # dispatches per step: the 13 256->256 ones first (12 res + Generator.in_conv, backward order),
 # then AFE.down2's two.
 DOMS = {
-    "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false)?>"), 512 * 512),
-    "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false)?>"), 512 * 512),
+    # (r5 names: conv3_halo_fwd3<4, 2, 4, 8, 2, false, SCH, MODE 0, false>)
+    "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false(, \d, 0, false)?)?>"), 512 * 512),
+    "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false(, \d, 0, false)?)?>"), 512 * 512),
     "wgrad": (re.compile(r"conv3_halo_wgrad2<4(, false)?>"), 256 * 512),
 }
 FWD_PER_STEP = 13
@@ -139,7 +140,8 @@ def main():
            "corrections": __doc__.split("\n\n")[0], "dominant": {}, "families": {}, "step": {}}
     for fam, (pat, g) in DOMS.items():
         s = summarize(cnt, dur, "dom:" + fam)
-        s["kernel"] = f"{pat.pattern} grid {g} @64x64 B=32 (res conv {fam})"
+        shown = re.sub(r"\(.*\)\?", "", pat.pattern)     # the pattern without its optional groups
+        s["kernel"] = f"{shown} grid {g} @64x64 B=32 (res conv {fam})"
         s["algorithmic_flop"] = RES_FLOP
         out["dominant"][fam] = s
     fams = sorted({k for k, _ in cnt if not k.startswith("dom:")} | {k for k in dur if not k.startswith("dom:")})
