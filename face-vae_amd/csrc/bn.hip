@@ -878,6 +878,7 @@ int fv_bn_stats_finalize_tensor(int dtype, const void* x, long pixels, int c, in
 
 int fv_bn_act_fwd(int dtype, const void* y, int n, int h, int w, int c, int ldc, const float* scale,
                   const float* shift, float slope, int pool, void* out, void* stream) {
+  FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, ldc);
   if (st) return st;
   FV_REQUIRE(!pool || (h % 2 == 0 && w % 2 == 0), "pool needs even h, w");
@@ -899,6 +900,7 @@ int fv_bn_act_fwd(int dtype, const void* y, int n, int h, int w, int c, int ldc,
 int fv_bn_act_bwd_reduce(int dtype, const void* dout, const void* y, int n, int h, int w, int c, int ldc,
                          const float* mean, const float* invstd, const float* gamma, const float* beta,
                          float slope, int pool, double* red, void* ws, void* stream) {
+  FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, ldc);
   if (st) return st;
   FV_REQUIRE(!pool || ldc == c, "pooled bwd needs dense channels");
@@ -935,6 +937,7 @@ int fv_bn_act_bwd_reduce_finalize(int dtype, const void* dout, const void* y, in
                                   int ldc, const float* mean, const float* invstd, const float* gamma,
                                   const float* beta, float slope, int pool, long count, float* dgamma,
                                   float* dbeta, float* k, void* ws, void* stream) {
+  FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, ldc);
   if (st) return st;
   FV_REQUIRE(!pool || ldc == c, "pooled bwd needs dense channels");
@@ -988,6 +991,7 @@ int fv_bn_bwd_finalize_dev(const double* red, int c, const double* count, float*
 int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h, int w, int c, int ldc,
                         const float* mean, const float* invstd, const float* gamma, const float* beta,
                         float slope, int pool, const float* k, const void* addend, void* dx, void* stream) {
+  FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, ldc);
   if (st) return st;
   FV_REQUIRE(!pool || ldc == c, "pooled bwd needs dense channels");
@@ -1028,6 +1032,7 @@ constexpr int Q8_BLOCKS = 2048;
 
 int fv_bn_act_fwd_q8(int dtype, const void* y, int n, int h, int w, int c, const float* scale,
                      const float* shift, float slope, void* out, void* out8, void* site, void* stream) {
+  FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, c);
   if (st) return st;
   FV_REQUIRE(y && scale && shift && out && out8 && site, "bn_act_fwd_q8: null pointer");
@@ -1049,6 +1054,7 @@ int fv_bn_act_bwd_apply_q8(int dtype, const void* dout, const void* y, int n, in
                            const float* mean, const float* invstd, const float* gamma, const float* beta,
                            float slope, const float* k, const void* addend, void* dx, void* dx8, void* site,
                            void* stream) {
+  FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, c);
   if (st) return st;
   FV_REQUIRE(dout && y && mean && invstd && gamma && beta && k && dx && dx8 && site,

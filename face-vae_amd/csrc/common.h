@@ -83,7 +83,12 @@ template <> struct Chunk8<float> {
   }
 };
 
-__device__ __forceinline__ float fv_act(float v, float slope) { return v > 0.f ? v : v * slope; }
+// ReLU / LeakyReLU, 0 <= slope <= 1 (ReLU 0, LeakyReLU 0.2: modules.py:41-47): max(v, v * slope)
+// is v for v > 0 and v * slope otherwise, bit for bit (signed zeros and NaN included; only
+// -inf at slope 0 differs: -inf, not NaN) -- one v_mul + one v_max instead of a compare-select.
+// The entry points reject slopes outside [0, 1] (fv_slope_ok)
+__device__ __forceinline__ float fv_act(float v, float slope) { return fmaxf(v, v * slope); }
+static inline bool fv_slope_ok(float slope) { return slope >= 0.f && slope <= 1.f; }
 
 // wave-level reductions (wave64)
 __device__ __forceinline__ float wave_sum(float v) {

@@ -1906,10 +1906,19 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
 // over 8 iterations = one record of 512 pixels per (wave row, 8 iterations), 16-B bf16 stores
 // (v_permlane16_swap pairs the two 16-channel fragments).  Replaces conv_fwd_v2's per-tap DMA.
 // ----------------------------------------------------------------------------------------
+// PRO ("option B": AFE.in_conv's BN-apply + ReLU in this consumer): x is the
+// PRE-BN in_conv output; each wave transforms the input-row pieces it DMA'd, in LDS, once they
+// landed (its own counted vmcnt) and before the barrier that publishes them --
+// v -> bf16(act(v * scale[c] + shift[c])), act_fwd's arithmetic; out-of-image slots stay 0 --
+// so the separate act_fwd pass over the 256x256x64 tensor (and its output) disappears.
 constexpr int C64_PXB = 160, C64_ROWB = 11 * 1024, C64_NR = 10, C64_G = 8;
+constexpr int C64_XK = 10;             // PRO: k-step at which the next rows' transform starts
+template <bool PRO = false>
 __global__ void __launch_bounds__(512, 1)
 conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
   __shared__ __attribute__((aligned(1024))) char smem[C64_NR * C64_ROWB];
+  __shared__ __attribute__((aligned(16))) float sst[PRO ? 128 : 4];     // PRO: [scale 64][shift 64]
+  __shared__ __attribute__((aligned(16))) float sbias[64];              // the block's 64 biases
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cg = wave & 1, rw = wave >> 1;
@@ -1927,24 +1936,65 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
   const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
   // DMA slots of a row: 16-B chunk k = piece * 64 + lane -> halo pixel k / 10, chunk k % 10
-  unsigned poff[11];
-#pragma unroll
-  for (int p = 0; p < 11; ++p) {
-    const int k = p * 64 + lane, px = k / 10, ch = k - (k / 10) * 10;
+  // (recomputed per piece: a register table of the 11 offsets does not fit beside the weights)
+  auto poff_of = [&](int p, int ln) {
+    const int k = p * 64 + ln, px = k / 10, ch = k - px * 10;
     const int iw = w0 - 1 + px;
-    poff[p] = (px < 66 && ch < 8 && iw >= 0 && iw < a.W) ? (unsigned)((iw * 64 + ch * 8) * 2) : 0x80000000u;
-  }
+    return (px < 66 && ch < 8 && iw >= 0 && iw < a.W) ? (unsigned)((iw * 64 + ch * 8) * 2) : 0x80000000u;
+  };
   auto row_slot = [&](int y) { return (y - hb + 1) % C64_NR; };
   // piece q (0 .. 11 * rows - 1) of the rows starting at y0: row y0 + q / 11, piece q % 11
   auto issue_piece = [&](int y0, int q) {                  // rows outside the image -> zeros
     const int y = y0 + q / 11, p = q % 11;
     const bool rok = y >= 0 && y < a.H;
-    unsigned v = 0x80000000u;
-#pragma unroll
-    for (int j = 0; j < 11; ++j)
-      if (j == p) v = poff[j];
+    const unsigned v = poff_of(p, lane);
     dma16s(xr, sbase + row_slot(y) * C64_ROWB + p * 1024, rok ? v : 0x80000000u,
            rok ? (unsigned)((n * a.H + y) * a.W) * 128u : 0u);
+  };
+  // PRO: BN-apply + activation of this wave's landed pieces q = wave + 8 (j0 .. j0 + XB - 1)
+  // (< nq) of the rows starting at y0, every LDS read issued before any use.  Pad chunks, halo
+  // columns outside the image and rows outside it keep their DMA zeros.
+  auto xform_batch = [&](int y0, int nq, int j0, auto xb) {
+    if constexpr (PRO) {
+      constexpr int XB = decltype(xb)::value;
+      // an opaque copy of the lane id: otherwise the per-piece addresses / channels (loop
+      // invariants) are hoisted out of the row loop and held in registers the weights need
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      uint4 raw[XB];
+      unsigned addr[XB];
+      int c0s[XB];
+      bool okp[XB];
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        const int q = wave + 8 * (j0 + u);
+        const int y = y0 + q / 11, p = q % 11;
+        const unsigned v = poff_of(p, ln);
+        okp[u] = q < nq && y >= 0 && y < a.H && v != 0x80000000u;
+        const int ch = (p * 64 + ln) % 10;
+        c0s[u] = (ch < 8 ? ch : 7) * 8;
+        addr[u] = (unsigned)(row_slot(q < nq ? y : y0) * C64_ROWB + p * 1024 + ln * 16);
+        raw[u] = *reinterpret_cast<const uint4*>(smem + addr[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < XB; ++u) {
+        Chunk8<bf16> c;
+        c.raw = raw[u];
+        // 2 channels at a time: (scale, shift) in 4 registers, the result packed at once (8
+        // channels' worth of (scale, shift) spills beside the 144 weight registers)
+        unsigned o[4];
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh) {
+          const float2 sc = *reinterpret_cast<const float2*>(sst + c0s[u] + 2 * hh);
+          const float2 sh = *reinterpret_cast<const float2*>(sst + 64 + c0s[u] + 2 * hh);
+          const bf16 t[2] = {(bf16)fv_act(c.get(2 * hh) * sc.x + sh.x, a.slope),
+                             (bf16)fv_act(c.get(2 * hh + 1) * sc.y + sh.y, a.slope)};
+          o[hh] = *reinterpret_cast<const unsigned*>(t);
+        }
+        c.raw = make_uint4(o[0], o[1], o[2], o[3]);
+        if (okp[u]) *reinterpret_cast<uint4*>(smem + addr[u]) = c.raw;
+      }
+    }
   };
 
   // the wave's weights: A fragment (cf, ks) = 16 channels x 32 k, k = tap * 64 + ci
@@ -1955,14 +2005,16 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks)
       wf[cf][ks] = *reinterpret_cast<const bf16x8*>(wk + (long)(cw + cf * 16 + lr) * a.Kpad + ks * 32 + lh * 8);
-  float bv[2][4];
-#pragma unroll
-  for (int cf = 0; cf < 2; ++cf)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bv[cf][i] = a.bias ? a.bias[cw + cf * 16 + lh * 4 + i] : 0.f;
 
   // prologue: input rows hb - 1 .. hb + 4 (66 pieces)
   for (int q = wave; q < 66; q += 8) issue_piece(hb - 1, q);
+  // biases (and the PRO scale / shift) in LDS, read back per epilogue: 8 registers fewer beside
+  // the 144 weight registers (loaded after the prologue DMA is on its way)
+  if (tid < 64) sbias[tid] = a.bias ? a.bias[cgrp * 64 + tid] : 0.f;
+  if constexpr (PRO) {
+    if (tid < 128) sst[tid] = tid < 64 ? a.psc[tid] : a.psh[tid - 64];
+  }
+  __syncthreads();
 
   float st[2][4], sq[2][4];
 #pragma unroll
@@ -1983,6 +2035,14 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
     // output stores (+ 2 record stores), which stay in flight
     if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if constexpr (PRO) {
+      // the pieces this wave DMA'd for this iteration's new rows (prologue: rows hb - 1 ..
+      // hb + 4; later: rows h0 + 1 .. h0 + 4, issued in the previous iteration)
+      // iteration 0: the prologue rows hb - 1 .. hb + 4; later iterations' rows were transformed
+      // under the previous iteration's MFMAs (below)
+      if (it == 0)
+        for (int j0 = 0; wave + 8 * j0 < 66; j0 += 2) xform_batch(hb - 1, 66, j0, std::integral_constant<int, 2>{});
+    }
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -2006,6 +2066,15 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
         fb[pf] = *reinterpret_cast<const bf16x8*>(smem + sb[r] + (pf * 16 + s) * C64_PXB + ch * 64);
       // the next iteration's rows h0 + 5 .. h0 + 8: pieces wave, wave + 8, ... < 44
       if (ks < 6 && more && wave + 8 * ks < 44) issue_piece(h0 + 5, wave + 8 * ks);
+      if constexpr (PRO) {
+        // ... and their BN-apply + activation once landed, one piece per k-step under this
+        // iteration's MFMAs (they go to ring slots this iteration does not read; the barrier
+        // at the next iteration's top publishes them)
+        if (ks >= C64_XK && ks < C64_XK + 6 && more) {
+          if (ks == C64_XK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (wave + 8 * (ks - C64_XK) < 44) xform_batch(h0 + 5, 44, ks - C64_XK, std::integral_constant<int, 1>{});
+        }
+      }
 #pragma unroll
       for (int pf = 0; pf < 4; ++pf)
 #pragma unroll
@@ -2025,7 +2094,7 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
       for (int cf = 0; cf < 2; ++cf)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          v[cf][i] = acc[pf][cf][i] + bv[cf][i];
+          v[cf][i] = acc[pf][cf][i] + sbias[cg * 32 + cf * 16 + lh * 4 + i];
           st[cf][i] += v[cf][i];
           sq[cf][i] += v[cf][i] * v[cf][i];
         }
@@ -4001,7 +4070,9 @@ bool use_h3w(const fv_conv_desc* d) {
     g_h3w_all = (e && e[0] == '0') ? 0 : 1;
   }
   const bool cin_ok = d->cin == 64 || (g_h3w_all && d->cin % 64 == 0);
-  if (d->pro_act && !pro3_ok(d)) return false;      // the staged BN prologue: NAC convs only
+  // the staged BN prologue: the NAC convs, and AFE.down1 (64 input channels: the in_conv BN
+  // applied in its operand staging, fv_conv2d_pro_staged)
+  if (d->pro_act && !pro3_ok(d) && d->cin != 64) return false;
   return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && cin_ok &&
          d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
 }
@@ -4024,6 +4095,7 @@ int check_desc(const fv_conv_desc* d) {
   FV_REQUIRE(!d->upsample || (d->h % 2 == 0 && d->w % 2 == 0), "upsample needs even h, w");
   FV_REQUIRE(!d->upsample || d->ksize == 3, "upsample only with 3x3");
   FV_REQUIRE(!d->pro_act || d->ksize != 7, "BN prologue not supported for 7x7");
+  FV_REQUIRE(!d->pro_act || fv_slope_ok(d->pro_slope), "prologue slope must be in [0, 1] (got %g)", (double)d->pro_slope);
   return FV_OK;
 }
 
@@ -4284,9 +4356,12 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   return rows * kpad_of(d->ksize, cin_t);
 }
 
+static bool use_c64(const fv_conv_desc* fd);
 int fv_conv2d_pro_staged(const fv_conv_desc* d) {
-  if (check_desc(d) != FV_OK) return 0;
-  return pro3_ok(d) ? 1 : 0;
+  if (check_desc(d) != FV_OK || !d->pro_act) return 0;
+  // the NAC halo convs, or a 64-channel band conv (conv3c64_fwd<true>) whose weight gradient
+  // runs the sliding-row kernel's PRO variant
+  return (pro3_ok(d) || (use_c64(d) && plan_wgrad(d).v2 == 5)) ? 1 : 0;
 }
 
 int fv_conv2d_dgrad_lowres(const fv_conv_desc* d) {
@@ -4315,7 +4390,7 @@ static bool use_c74(const fv_conv_desc* fd) {
 // the launch of forward-conv descriptor fd runs conv3c64_fwd (64 input channels, sliding band,
 // weights in registers; plain [co][Kpad] weights)
 static bool use_c64(const fv_conv_desc* fd) {
-  return fd->dtype == FV_BF16 && fd->ksize == 3 && !fd->upsample && !fd->pro_act && fd->cin == 64 &&
+  return fd->dtype == FV_BF16 && fd->ksize == 3 && !fd->upsample && fd->cin == 64 &&
          fd->cin_valid == 64 && fd->cout % 64 == 0 && fd->ldy % 8 == 0 && !fd->epi_sigmoid && !fd->out_nchw_f32 &&
          fd->w % 64 == 0 && fd->h % 32 == 0 && (long)fd->n * fd->h * fd->w * 64 * 2 < (1L << 31) &&
          (long)fd->n * fd->h * fd->w * fd->ldy * 2 < (1L << 31);
@@ -4620,7 +4695,12 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     const int nb = c64_bands(d);
     const int nblk = d->n * (d->w / 64) * (d->cout / 64) * nb;
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
-    hipLaunchKernelGGL(conv3c64_fwd, dim3(nblk), dim3(512), 0, s, a, xb, nb);
+    if (d->pro_act) {
+      FV_REQUIRE(psc && psh, "64-channel band conv: prologue needs scale / shift");
+      hipLaunchKernelGGL(conv3c64_fwd<true>, dim3(nblk), dim3(512), 0, s, a, xb, nb);
+    } else {
+      hipLaunchKernelGGL(conv3c64_fwd<false>, dim3(nblk), dim3(512), 0, s, a, xb, nb);
+    }
     return fv_check_launch("conv2d_fwd_c64");
   }
   if (use_c74(d)) {

@@ -113,10 +113,11 @@ int fv_conv2d_dgrad_lowres(const fv_conv_desc* d);
  * (d->pro_act): the ResBlock2D NAC convs (modules.py:13,31-39,119-125: BN -> act -> conv3x3),
  * whose pre-BN input is staged and transformed in LDS, so act(BN(x)) is never materialised
  * (forward: fv_conv2d_fwd / fv_conv2d_fwd_pro_sr; weight gradient: fv_conv2d_bwd_weight with
- * the same scale / shift; the data gradient is w.r.t. act(BN(x)) as before).  0: other
- * descriptors take the prologue on the generic register-staged kernels (slow).  Measured on
- * MI355X (DESIGN.md §4 "Round 4, measured"): slower than materialising act(BN(x)) with
- * fv_bn_act_fwd, so the host side only uses it on request. */
+ * the same scale / shift; the data gradient is w.r.t. act(BN(x)) as before), and the 64-input-
+ * channel 3x3 convs (AFE.down1 consuming the in_conv CNA block's pre-BN output:
+ * models.py:935-940).  0: other descriptors take the prologue on the generic register-staged
+ * kernels (slow).  Measured on MI355X: the NAC variant is slower than
+ * materialising act(BN(x)) with fv_bn_act_fwd, so the host side only uses it on request. */
 int fv_conv2d_pro_staged(const fv_conv_desc* d);
 
 /* weight gradient w.r.t. the effective (post-SN) weight, split over pixels:
@@ -328,8 +329,11 @@ int fv_grid_sample3d_fwd(int dtype, const void* in, const float* grid, int B, in
 int fv_grid_sample3d_bwd(int dtype, const void* in, const float* grid, const void* gout, int B, int Di, int Hi,
                          int Wi, int Do, int Ho, int Wo, int C, int group, float* gin, float* ggrid, void* stream);
 /* gin (dtype, input layout, every element written) = dL/din without float atomics: the output
- * voxels are bucketed by their base input cell (count, scan, fill in ws) and each input cell sums
- * the buckets whose corner it is.  ws: fv_grid_sample3d_bwd_input_ws_bytes bytes. */
+ * voxels are bucketed by their base input cell (count, scan, fill in ws), each bucket is ordered
+ * by voxel index, and each input cell sums the buckets whose corner it is (bit-reproducible).
+ * ws: fv_grid_sample3d_bwd_input_ws_bytes bytes = 4 B per input cell key + 24 B per OUTPUT voxel
+ * (key/rank + record): for create_deformed_source_image (group K+1, B = N (K+1) grids) at N = 8,
+ * K = 15, 16x64x64 that is ~200 MB per backward. */
 size_t fv_grid_sample3d_bwd_input_ws_bytes(int B, int Di, int Hi, int Wi, int Do, int Ho, int Wo, int group);
 int fv_grid_sample3d_bwd_input(int dtype, const float* grid, const void* gout, int B, int Di, int Hi, int Wi, int Do,
                                int Ho, int Wo, int C, int group, void* gin, void* ws, void* stream);

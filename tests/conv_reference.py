@@ -203,7 +203,15 @@ class LaunchChecker:
         name = self.names.get(id(bn), "?")
         rl2, worst = compare(t["out"], z, out_bf16=self.dtype == torch.bfloat16)
         self._addbn(name, "bn_fwd", y.shape, rl2, worst)
+        self.bn_stat(bn, t)
+
+    def bn_stat(self, bn, t):
+        """Batch statistics of a training-mode BN (also for a BN whose apply runs in its consumer
+        conv's operand staging, ops.CNAPairFn: that apply is checked by the conv's fwd row)."""
+        r = t["r"]
+        name = self.names.get(id(bn), "?")
         if r.count or r.stats is not None:              # training: batch statistics
+            y = t["y"]
             yd = t["y"].double()
             m = yd.mean((0, 2, 3))
             sd = yd.var((0, 2, 3), unbiased=False).add(bn.eps).sqrt()
@@ -251,9 +259,9 @@ class LaunchChecker:
                           "cout": shape[1], "k": 0, "ups": 0, "rel_l2": rl2, "worst": worst})
 
     def __call__(self, kind, cs, **t):
-        if kind in ("bn_fwd", "bn_bwd"):
+        if kind in ("bn_fwd", "bn_bwd", "bn_stat"):
             with torch.no_grad():
-                return (self.bn_fwd if kind == "bn_fwd" else self.bn_bwd)(cs, t)
+                return {"bn_fwd": self.bn_fwd, "bn_bwd": self.bn_bwd, "bn_stat": self.bn_stat}[kind](cs, t)
         d = cs.d
         name = self.names.get(id(cs.conv), "?")
         k = d.ksize

@@ -55,6 +55,9 @@ def run_conv3d(x, w, b, res=None, dtype=torch.bfloat16, stats=False):
 
 @pytest.mark.parametrize("shape,dtype", [((2, 32, 4, 8, 64), torch.bfloat16),     # MFMA kernels
                                          ((1, 32, 16, 16, 64), torch.bfloat16),
+                                         # N (H / 4) >= 256 at D = 16: one 16-slice depth chunk, the
+                                         # 18-slice walk of the B = 32 trunk
+                                         ((64, 32, 16, 16, 64), torch.bfloat16),
                                          ((1, 32, 7, 4, 64), torch.bfloat16),     # depth walk of 7 (+2 halo)
                                          ((2, 32, 2, 8, 64), torch.bfloat16),     # no 3k-2 chunk: conv3d_c32_fwd
                                          ((2, 16, 3, 5, 8), torch.float32),       # direct kernels
