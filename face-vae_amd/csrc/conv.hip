@@ -648,6 +648,10 @@ __device__ __forceinline__ void wait_lgkm0() {
 }
 
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff, unsigned soff) {
+  // lds / soff are wave-uniform at every call site (the "s" operands); readfirstlane states it
+  // for values the compiler merges across uniform branches into a VGPR phi (a no-op on an SGPR)
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  soff = __builtin_amdgcn_readfirstlane(soff);
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
                :
                : "v"(voff), "s"(r), "s"(lds), "s"(soff)
@@ -3126,6 +3130,222 @@ conv3_halo_wgrad2(H3Wg2Args a) {
 }
 
 // ----------------------------------------------------------------------------------------
+// Sub-pixel weight gradient of the UpBlock2D convs (nearest x2 upsample + 3x3, modules.py:78-89;
+// VERDICT r4 item 2) on the sliding-row structure of conv3_halo_wgrad2: output row Y = 2h + pa,
+// column X = 2w + pb reads the low-res rows h + pa + rr - 1 and columns w + pb + ss - 1
+// (rr, ss in {0, 1}), so the gradient of the 4 phases' 2x2 weights is
+//   D[pa pb][co][(rr ss), ci] = sum_{h, w} dy[2h + pa][2w + pb][co] * x[h + pa + rr - 1][w + pb + ss - 1][ci]
+// (4/9 of the MACs of the upsampled 3x3; wgrad_reduce_subpix folds the phases back).  A block
+// owns 64 co x 64 ci x all 16 (phase, tap) pairs and walks the low-res rows of `spb` consecutive
+// (image, 64-column output strip) units.  Step h = output rows 2h, 2h + 1 (one dy group, 2 x 8
+// KB) and the low-res x rows h - 1 .. h + 1 (a ring; one new 34-pixel row per step).  The dy
+// rows land PHASE-MAJOR in LDS -- LDS row pb * 32 + w holds output pixel 2w + pb (the per-lane
+// DMA source chooses the pixel) -- so a phase's A fragment (16 co x 32 pixels) is one
+// transposed read pair, like every x fragment (16 ci x 32 low-res pixels at column shift
+// pb + ss).  Wave (pa, pb, rr) = wave bits (0, 1, 2): 4 co tiles x 2 ss x 4 ci tiles = 32
+// accumulators, 4 A + 8 B fragments per 32 MFMAs.  Output: the sub-pixel slab layout of
+// conv_wgrad_v2 <SUB> ([phase][split][co][(rr * 2 + ss) * Cin + ci]) and the per-phase bias slab
+// (dy sums by an all-ones operand, the rr = 0 waves of ci tile 0).
+// ----------------------------------------------------------------------------------------
+struct UpWgArgs {
+  const void* x;
+  const void* dy;
+  float* slab;
+  float* bslab;
+  int Hin, Win, Cout, Cin, ldd;
+  int nct, nci, units, spb, nsplit;     // units = images x output strips; spb units per block
+  unsigned xbytes, dybytes;
+};
+
+template <int AHEAD>
+__global__ void __launch_bounds__(512, 1)
+conv3_up_wgrad(UpWgArgs a) {
+  // a step = 2 low-res rows (4 dy rows): 64 MFMAs per wave between barriers (one low-res row per
+  // step measured 170 us per UpBlock2D conv at B = 32: the per-step barrier, waits and DMA issue
+  // were not amortised over 32 MFMAs)
+  constexpr int RPS = 2;
+  constexpr int BC = 64, NSD = AHEAD + 1, NSX = (AHEAD + 1) * RPS + 2;
+  constexpr int DYR = 64 * BC * 2, DYB = 2 * RPS * DYR; // one dy row 8 KB (8 pieces), a group 32 KB
+  constexpr int XQ = 5, XB = XQ * 1024;               // x row: 34 px x 128 B = 4352 B -> 5 pieces
+  constexpr int NDY = 16 * RPS, NPC = NDY + XQ * RPS; // pieces per group: dy rows, then x rows
+  __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB];
+  char* const dyr = smem;
+  char* const xr_ = smem + NSD * DYB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pa = wave & 1, pb = (wave >> 1) & 1, rr = wave >> 2;
+  const int li = lane & 15, g = lane >> 4;
+  // XCD-aware order: the nct x nci tiles of one split (the same dy and x rows) are consecutive
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int blk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int ntile = a.nct * a.nci;
+  const int tile = blk % ntile, tc = tile % a.nct, tci = tile / a.nct;
+  const int split = blk / ntile;
+  const int co0 = tc * BC, ci0 = tci * 64;
+  const int Wo = 2 * a.Win, strips = Wo >> 6;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.dy), 0, (int)a.dybytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+
+  // this wave's pieces of a group: piece `wave` of each of the 2 RPS dy rows (one lane offset
+  // for all of them: the lane's source pixel / channel within the strip row), and x pieces
+  // xq = wave (+ 8 for waves 0, 1) of the group's RPS x rows (row xq / XQ, piece xq % XQ).  Few
+  // wave-uniform values: per-piece conditions and offsets kept in SGPRs spilled 169 of them
+  static_assert(NDY == 8 * 2 * RPS && XQ * RPS <= 16, "piece assignment");
+  constexpr int NXP = XQ * RPS;
+  const int nxw = (NXP - wave + 7) / 8;               // x pieces of this wave (1 or 2)
+  const int npw = 2 * RPS + nxw;
+  unsigned dyoff;
+  {
+    const int o = wave * 1024 + lane * 16;
+    const int rho = o >> 7, b = o & 127;
+    const int co = (((b >> 5) ^ tswz<BC>(rho)) << 4) | (((b >> 4) & 1) << 3);
+    const int px = 2 * (rho & 31) + (rho >> 5);       // phase-major rows
+    dyoff = (unsigned)((px * a.ldd + co0 + co) * 2);
+  }
+  int xrho[2], xci[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int xq = wave + 8 * m;
+    const int o = (xq % XQ) * 1024 + lane * 16;
+    const int rho = o >> 7, b = o & 127;
+    xci[m] = ci0 + ((((b >> 5) ^ tswz<64>(rho)) << 4) | (((b >> 4) & 1) << 3));
+    xrho[m] = rho;                                    // < 34: a pixel of the row
+  }
+
+  // lane constants of the transposed reads (rows: the phase's 32 pixels; x rows shifted by
+  // pb + ss), as conv3_halo_wgrad2's lcd / lcx
+  unsigned lcd[4][2], lcx[2][4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int rl = 8 * g + 4 * h + (li >> 2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lcd[q][h] = (unsigned)timg_off<BC>(pb * 32 + rl, q * 16 + 4 * (li & 3));
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) lcx[ss][u][h] = (unsigned)timg_off<64>(pb + ss + rl, u * 16 + 4 * (li & 3));
+  }
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  auto frag2 = [](const char* base, unsigned l0, unsigned l1) {
+    FV_LDS char* lb = (FV_LDS char*)(base);
+    const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + l0));
+    const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(lb + l1));
+    const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  f32x4 acc[4][2][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[q][ss][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) accb[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bslab && tci == 0 && rr == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+
+  const int u0 = split * a.spb, u1 = min(a.units, u0 + a.spb);
+  const int nstep = a.Hin / RPS;
+  for (int un = u0; un < u1; ++un) {
+    const int n = un / strips, w0 = (un % strips) * 64, wl0 = w0 >> 1;
+    if (un > u0) __syncthreads();                    // the previous unit's last reads of the rings
+    // per unit: the x pieces' source offsets with the strip's column validity (0x80000000 =
+    // zero fill: halo columns outside the image, LDS rows past the 34 pixels)
+    unsigned xv[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int col = wl0 - 1 + xrho[m];
+      xv[m] = (xrho[m] < 34 && col >= 0 && col < a.Win) ? (unsigned)((col * a.Cin + xci[m]) * 2) : 0x80000000u;
+    }
+    // x row y (low-res; -1 and Hin are the zero padding) -> ring slot (y + 1) % NSX
+    auto issue_x = [&](int y, int m) {
+      const int xq = wave + 8 * m;
+      const bool rok = y >= 0 && y < a.Hin;
+      dma16s(xr, sbase + NSD * DYB + ((y + 1) % NSX) * XB + (xq % XQ) * 1024, rok ? xv[m] : 0x80000000u,
+             rok ? (unsigned)((n * a.Hin + y) * a.Win) * (unsigned)a.Cin * 2u : 0u);
+    };
+    // group i: dy rows 2 RPS i .. + 2 RPS - 1, x rows RPS i + 1 .. RPS i + RPS
+    auto issue_group = [&](int i) {
+      const unsigned rb = (unsigned)(((n * 2 * a.Hin + 2 * RPS * i) * Wo + w0) * a.ldd) * 2u;
+      const unsigned rs = (unsigned)(Wo * a.ldd) * 2u;
+#pragma unroll
+      for (int k = 0; k < 2 * RPS; ++k)
+        dma16s(dr, sbase + (i % NSD) * DYB + k * DYR + wave * 1024, dyoff, rb + k * rs);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        if (m < nxw) issue_x(RPS * i + 1 + (wave + 8 * m) / XQ, m);
+    };
+    // prologue: x rows -1 .. RPS - 2 = "group -1"'s x rows
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      if (m < nxw) issue_x(1 - RPS + (wave + 8 * m) / XQ, m);
+#pragma unroll
+    for (int i = 0; i < AHEAD; ++i)
+      if (i < nstep) issue_group(i);
+
+    for (int i = 0; i < nstep; ++i) {
+      // group i landed; the younger groups issued so far (up to AHEAD - 1) may stay in flight
+      const int younger = min(AHEAD - 1, nstep - 1 - i);
+      wait_vm_dyn(younger * npw);
+      wait_lgkm0();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (i + AHEAD < nstep) issue_group(i + AHEAD);
+#pragma unroll
+      for (int hh = 0; hh < RPS; ++hh) {
+        const int h = RPS * i + hh;
+        const char* dys = dyr + (i % NSD) * DYB + (2 * hh + pa) * DYR;   // dy row 2h + pa
+        const char* xs = xr_ + ((h + pa + rr) % NSX) * XB;              // low-res row h + pa + rr - 1
+        bf16x8 af[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) af[q] = frag2(dys, lcd[q][0], lcd[q][1]);
+        bf16x8 bcur = frag2(xs, lcx[0][0][0], lcx[0][0][1]);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int ss = t >> 2, u = t & 3;
+          bf16x8 bnext = bcur;
+          if (t + 1 < 8) bnext = frag2(xs, lcx[(t + 1) >> 2][(t + 1) & 3][0], lcx[(t + 1) >> 2][(t + 1) & 3][1]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q][ss][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], bcur, acc[q][ss][u], 0, 0, 0);
+          bcur = bnext;
+        }
+        if (do_bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) accb[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[q], ones, accb[q], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // slab[(phase * nsplit + split)][co][(rr * 2 + ss) * Cin + ci]: lane holds D[co = 4g + jj][ci = li]
+  const int ph = pa * 2 + pb;
+  const long KW = 4L * a.Cin;
+  float* sl = a.slab + (long)(ph * a.nsplit + split) * a.Cout * KW;
+#pragma unroll
+  for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kcol = (rr * 2 + ss) * a.Cin + ci0 + u * 16 + li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) sl[(long)(co0 + q * 16 + 4 * g + jj) * KW + kcol] = acc[q][ss][u][jj];
+    }
+  if (do_bias && li == 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) a.bslab[(long)(ph * a.nsplit + split) * a.Cout + co0 + q * 16 + 4 * g + jj] = accb[q][jj];
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // Weight gradient of the 7x7 64 -> <= 4 channel conv (Generator.out_conv), "row taps in N":
 //   D[(s, ci)][(r, co)] = sum_{x row h, column w} x[h][w + s - 3][ci] * dy[h - r + 3][w][co]
 //                      = dW[co][ci][r][s]
@@ -3725,6 +3945,66 @@ __global__ void wgrad_reduce_subpix_kernel(const float* __restrict__ slab, const
   }
 }
 
+// Sub-pixel slabs of many splits (conv3_up_wgrad: ~one block per CU, 4 x 128 splits at
+// 256^2), in two passes instead of the gather above (whose 9 (r, s) neighbours read 4 rows a
+// cin apart: 117 us for the two UpBlock2D convs at B = 32):
+// pass 1 sums each phase's splits over 64 consecutive slab elements x 4 split lanes (coalesced,
+// fixed order) and writes the sum in place into the phase's split-0 row (every element is read
+// by its own block only); blocks >= nb_main do the same for the bias slab.
+__global__ void subpix_split_sum_kernel(float* __restrict__ slab, float* __restrict__ bslab, int nsplit, long rowlen,
+                                        int CW, int nb_main) {
+  const int sg = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __shared__ float red[4][64];
+  float g = 0.f;
+  float* base = nullptr;
+  long stride = 0, e = -1;
+  if ((int)blockIdx.x < nb_main) {
+    e = (long)blockIdx.x * 64 + l;                   // element of the [phase][rowlen] sums
+    if (e < 4 * rowlen) {
+      const long ph = e / rowlen, k = e - ph * rowlen;
+      base = slab + ph * nsplit * rowlen + k;
+      stride = rowlen;
+    }
+  } else {
+    e = (long)((int)blockIdx.x - nb_main) * 64 + l;
+    if (e < 4L * CW) {
+      const long ph = e / CW, co = e - ph * CW;
+      base = bslab + ph * nsplit * CW + co;
+      stride = CW;
+    }
+  }
+  if (base)
+    for (int sp = sg; sp < nsplit; sp += 4) g += base[sp * stride];
+  red[sg][l] = g;
+  __syncthreads();
+  if (sg == 0 && base) base[0] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+}
+
+// pass 2: dW[co][ci][r][s] = sum over the 4 phases of the phase tap (rr, ss) that (r, s) maps to
+// (the map of wgrad_reduce_subpix_kernel), db = the 4 phase sums
+__global__ void subpix_fold_kernel(const float* __restrict__ slab, const float* __restrict__ bslab, float* dw, float* db,
+                                   int nsplit, int CW, int KW, int cout, int cin_valid, int lgCin, int nb_main) {
+  const long rowlen = (long)CW * KW;
+  if ((int)blockIdx.x < nb_main) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (long)cout * cin_valid * 9) return;
+    const int rs = (int)(e % 9), ci = (int)((e / 9) % cin_valid), co = (int)(e / (9L * cin_valid));
+    const int r = rs / 3, sc = rs % 3;
+    float g = 0.f;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int pa = ph >> 1, pb = ph & 1;
+      const int rr = pa ? (r == 2) : (r > 0), ss = pb ? (sc == 2) : (sc > 0);
+      g += slab[(long)ph * nsplit * rowlen + (long)co * KW + (((rr * 2 + ss) << lgCin) + ci)];
+    }
+    dw[e] = g;
+  } else {
+    const int co = ((int)blockIdx.x - nb_main) * blockDim.x + threadIdx.x;
+    if (co >= cout) return;
+    db[co] = (bslab[co] + bslab[(long)nsplit * CW + co]) + (bslab[2L * nsplit * CW + co] + bslab[3L * nsplit * CW + co]);
+  }
+}
+
 // sum of the per-split slabs -> dW in the reference layout [co][ci][r][s] (+ db).  Block =
 // 64 consecutive outputs x 4 split lanes (4 independent partial sums each), so that large
 // split counts do not serialise on load latency; blocks >= nb_main reduce the bias slab.
@@ -4147,6 +4427,17 @@ int wg2_cfg(const fv_conv_desc* d, int K) {
   if (bc == 256) return K % 256 == 0 ? 0 : (d->ksize == 3 && d->w % 32 == 0 ? 6 : 1);
   return k256 ? 2 : 3;
 }
+// UpBlock2D weight gradient on conv3_up_wgrad: bf16 nearest-x2 + 3x3, 64-channel multiples,
+// 64-column output strips (FV_UPW=0: the conv_wgrad_v2 sub-pixel path, A/B)
+static bool use_upw(const fv_conv_desc* d) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("FV_UPW");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on && d->dtype == FV_BF16 && d->upsample && d->ksize == 3 && !d->pro_act && d->cin % 64 == 0 &&
+         d->cin_valid == d->cin && d->cout % 64 == 0 && d->w % 64 == 0 && d->h % 4 == 0;
+}
 WgPlan plan_wgrad(const fv_conv_desc* d) {
   WgPlan p{};
   const int K = d->ksize * d->ksize * d->cin;
@@ -4205,6 +4496,25 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
     p.sps = fv_cdiv(p.nsteps, p.nsplit);
     p.KW = p.bkt;
     p.CW = p.bc;
+    return p;
+  }
+  if (fits && use_upw(d)) {
+    // sub-pixel sliding-row weight gradient (v2 == 6, conv3_up_wgrad): blocks = (co tile, ci
+    // tile) x splits of `sps` consecutive (image, 64-column output strip) units, ~one block per
+    // CU; slab [phase][split][co][4 cin] as the v2 sub-pixel path
+    p.sub = 1;
+    p.v2 = 6;
+    p.ntc = d->cout / 64;
+    p.ntk = d->cin / 64;
+    const int units = d->n * (d->w / 64), tiles = p.ntc * p.ntk;
+    p.sps = (units * tiles + 128) / 256;
+    // FV_UPW_SPB=k: k units per block (tests: ragged last split at small shapes)
+    if (const char* e = getenv("FV_UPW_SPB")) p.sps = atoi(e);
+    if (p.sps < 1) p.sps = 1;
+    p.nsteps = units;
+    p.nsplit = fv_cdiv(units, p.sps);
+    p.CW = d->cout;
+    p.KW = 4 * d->cin;
     return p;
   }
   if (p.v2 && use_subpix(d) && (d->w / 2) % 64 == 0) {
@@ -5017,6 +5327,18 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
       hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
     return fv_check_launch("conv2d_bwd_weight_halo3s");
   }
+  if (t.v2 == 6) {
+    FV_REQUIRE(P * ldy_dy * 2 < (1L << 31) && (long)d->n * Hin * Win * d->cin * 2 < (1L << 31),
+               "wgrad: operand larger than 2 GB");
+    UpWgArgs a{};
+    a.x = x; a.dy = dy; a.slab = slab; a.bslab = bias_slab;
+    a.Hin = Hin; a.Win = Win; a.Cout = d->cout; a.Cin = d->cin; a.ldd = ldy_dy;
+    a.nct = t.ntc; a.nci = t.ntk; a.units = t.nsteps; a.spb = t.sps; a.nsplit = t.nsplit;
+    a.xbytes = (unsigned)((long)d->n * Hin * Win * d->cin * 2);
+    a.dybytes = (unsigned)(P * ldy_dy * 2);
+    hipLaunchKernelGGL(conv3_up_wgrad<2>, dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    return fv_check_launch("conv2d_bwd_weight_up");
+  }
   if (t.v2 == 3) {
     FV_REQUIRE(ldy_dy == 8, "wgrad (out_conv 7x7): dy channel stride must be 8 (got %d)", ldy_dy);
     W7Args a{};
@@ -5133,6 +5455,18 @@ int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float
     hipLaunchKernelGGL(w7_reduce2_kernel, dim3(fv_cdiv(ncol, 256)), dim3(256), 0, (hipStream_t)stream,
                        const_cast<float*>(slab), const_cast<float*>(bias_slab), t.nsplit, rpg, d->cout, dw_param, db);
     return fv_check_launch("wgrad_reduce_c7");
+  }
+  if (t.sub && t.v2 == 6) {
+    // many splits: split sums (in place), then the phase fold
+    const long rowlen = (long)t.CW * t.KW;
+    const int nb1 = (int)fv_cdiv(4 * rowlen, 64), nbb1 = db ? fv_cdiv(4L * t.CW, 64) : 0;
+    hipLaunchKernelGGL(subpix_split_sum_kernel, dim3(nb1 + nbb1), dim3(256), 0, (hipStream_t)stream,
+                       const_cast<float*>(slab), const_cast<float*>(bias_slab), t.nsplit, rowlen, t.CW, nb1);
+    if ((st = fv_check_launch("wgrad_reduce_subpix_splits"))) return st;
+    const int nb2 = fv_cdiv((long)d->cout * d->cin_valid * 9, 256), nbb2 = db ? fv_cdiv(d->cout, 256) : 0;
+    hipLaunchKernelGGL(subpix_fold_kernel, dim3(nb2 + nbb2), dim3(256), 0, (hipStream_t)stream, slab, bias_slab,
+                       dw_param, db, t.nsplit, t.CW, t.KW, d->cout, d->cin_valid, fv_ilog2(d->cin), nb2);
+    return fv_check_launch("wgrad_reduce_subpix_fold");
   }
   if (t.sub) {
     const int nb_main = fv_cdiv((long)d->cout * d->cin_valid * 9, 64);

@@ -484,3 +484,34 @@ def test_conv3x3_64ch_with_residual(res):
     xq = xb.float().cpu()
     ref = F.conv2d(xq, w, b, padding=1) + (rb.float().cpu() if res else 0)
     assert rel(y.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("spb", [1, 4])
+def test_up_wgrad_splits(spb, monkeypatch):
+    """UpBlock2D weight gradient (conv3_up_wgrad: sub-pixel phases on the sliding-row structure)
+    at 3 images x 2 output strips = 6 units, 1 or 4 units per block (the last split ragged), vs
+    torch fp32 (the CONV_CASES cover it at N = 2 and the full UpBlock2D sizes)."""
+    monkeypatch.setenv("FV_UPW_SPB", str(spb))
+    N, cin, cout, Hi, Wi = 3, 128, 64, 8, 64
+    g = gen(777)
+    x = torch.randn(N, cin, Hi, Wi, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    wr = w.clone().requires_grad_(True)
+    br = torch.zeros(cout, requires_grad=True)
+    out = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), wr, br, padding=1)
+    gy = torch.randn(out.shape, generator=g)
+    (out * gy).sum().backward()
+    d, xb, wk, wt, shp = conv_setup(x, w, 3, torch.bfloat16, True, need_wt=True)
+    gyb = gy.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    slab = torch.empty(L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)), device="cuda")
+    bslab = torch.empty(L.query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), device="cuda")
+    L.call("fv_conv2d_bwd_weight", ctypes.byref(d), xb.data_ptr(), None, None, gyb.data_ptr(), cout,
+           slab.data_ptr(), bslab.data_ptr(), L.stream())
+    dw = torch.empty(cout, cin, 3, 3, device="cuda")
+    db = torch.empty(cout, device="cuda")
+    L.call("fv_conv2d_wgrad_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(), dw.data_ptr(),
+           db.data_ptr(), L.stream())
+    torch.cuda.synchronize()
+    assert L.query("fv_conv2d_wgrad_nsplit", ctypes.byref(d)) == (6 + spb - 1) // spb
+    assert rel(dw, wr.grad) < TOL[torch.bfloat16] * 1.5
+    assert rel(db, br.grad) < TOL[torch.bfloat16] * 1.5

@@ -38,7 +38,7 @@ def main():
             continue
         g = lambda k: (re.search(r"\." + k + r":\s+(\S+)", blk) or [None, "?"])[1]
         print(f"{m.group(1)[:90]:90s} vgpr {g('vgpr_count'):>3} agpr {blk.split(chr(10))[0].strip():>3} "
-              f"spill {g('vgpr_spill_count'):>3} priv {g('private_segment_fixed_size'):>4} lds {g('group_segment_fixed_size')}")
+              f"spill {g('vgpr_spill_count'):>3} sgpr {g('sgpr_count'):>3}/{g('sgpr_spill_count'):>3} priv {g('private_segment_fixed_size'):>4} lds {g('group_segment_fixed_size')}")
 
 
 if __name__ == "__main__":
