@@ -1923,6 +1923,9 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
   __shared__ __attribute__((aligned(1024))) char smem[C64_NR * C64_ROWB];
   __shared__ __attribute__((aligned(16))) float sst[PRO ? 128 : 4];     // PRO: [scale 64][shift 64]
   __shared__ __attribute__((aligned(16))) float sbias[64];              // the block's 64 biases
+  // per-lane BN partial sums of the current 8-iteration record group, [wave][16][lane] (kept
+  // in LDS: their 16 registers double-buffer the B fragments instead)
+  __shared__ __attribute__((aligned(16))) float sacc[8 * 16 * 64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cg = wave & 1, rw = wave >> 1;
@@ -2020,11 +2023,7 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
   }
   __syncthreads();
 
-  float st[2][4], sq[2][4];
-#pragma unroll
-  for (int cf = 0; cf < 2; ++cf)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) st[cf][i] = sq[cf][i] = 0.f;
+  float* const sa = sacc + wave * 16 * 64 + lane;         // element e at sa[e * 64]
   const int niter = BAND >> 2, ng = niter / C64_G;
   const int rec0 = ((n * strips + strip) * nbands + band) * (4 * ng);
   const int loff = lr * C64_PXB + lh * 16;
@@ -2061,13 +2060,19 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
     for (int pf = 0; pf < 4; ++pf)
 #pragma unroll
       for (int cf = 0; cf < 2; ++cf) acc[pf][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 18; ++ks) {
+    // B fragments double-buffered: k-step ks + 1's are read before k-step ks's MFMAs
+    auto ldb = [&](bf16x8 (&fb)[4], int ks) {
       const int tap = ks >> 1, r = tap / 3, s = tap - (tap / 3) * 3, ch = ks & 1;
-      bf16x8 fb[4];
 #pragma unroll
       for (int pf = 0; pf < 4; ++pf)
         fb[pf] = *reinterpret_cast<const bf16x8*>(smem + sb[r] + (pf * 16 + s) * C64_PXB + ch * 64);
+    };
+    bf16x8 fbq[2][4];
+    ldb(fbq[0], 0);
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      if (ks + 1 < 18) ldb(fbq[(ks + 1) & 1], ks + 1);
+      const bf16x8 (&fb)[4] = fbq[ks & 1];
       // the next iteration's rows h0 + 5 .. h0 + 8: pieces wave, wave + 8, ... < 44
       if (ks < 6 && more && wave + 8 * ks < 44) issue_piece(h0 + 5, wave + 8 * ks);
       if constexpr (PRO) {
@@ -2091,6 +2096,15 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
     // contiguous channels (lh & 1) * 16 + (lh >> 1) * 8 .. + 7
     bf16* yp = reinterpret_cast<bf16*>(a.y) + ((long)(n * a.H + orow) * a.W + w0 + lr) * a.ldy + cw +
                (lh & 1) * 16 + (lh >> 1) * 8;
+    float st[2][4], sq[2][4];
+    const bool g0 = (it % C64_G) == 0;                    // the record group's first iteration
+#pragma unroll
+    for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        st[cf][i] = g0 ? 0.f : sa[(cf * 4 + i) * 64];
+        sq[cf][i] = g0 ? 0.f : sa[(8 + cf * 4 + i) * 64];
+      }
 #pragma unroll
     for (int pf = 0; pf < 4; ++pf) {
       float v[2][4];
@@ -2106,7 +2120,15 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
       const auto s1 = __builtin_amdgcn_permlane16_swap(pk(v[0][2], v[0][3]), pk(v[1][2], v[1][3]), false, false);
       *reinterpret_cast<uint4*>(yp + (long)pf * 16 * a.ldy) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
     }
-    if (a.stats && (it % C64_G) == C64_G - 1) {
+    if ((it % C64_G) != C64_G - 1) {
+#pragma unroll
+      for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sa[(cf * 4 + i) * 64] = st[cf][i];
+          sa[(8 + cf * 4 + i) * 64] = sq[cf][i];
+        }
+    } else if (a.stats) {
       // record (block, 8-iteration group, wave row): lanes 0-3 of a 16-lane row store the 4
       // channel sums, lanes 4-7 the squares (conv_epilogue's record layout)
       const int rec = rec0 + (it / C64_G) * 4 + rw;
@@ -2117,7 +2139,6 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
         for (int i = 0; i < 4; ++i) {
           sv[i] = row16_sum(st[cf][i]);
           qv[i] = row16_sum(sq[cf][i]);
-          st[cf][i] = sq[cf][i] = 0.f;
         }
         const int cb = cw + cf * 16 + lh * 4, ii = lr & 3;
         const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
