@@ -3658,37 +3658,81 @@ conv_halo_wgrad(HaloWgArgs a) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
 
-  auto compute = [&](int buf) {
-    const char* halo = smem + buf * BUF;
+  // fragments of k-group kg (B: dy[32 px][16 co] of every n-tile; A: the halo at each m-tile's
+  // tap shift), all reads issued together before the k-group's MFMAs (one m-tile's 2 reads
+  // right before its 4 MFMAs left the LDS latency exposed: AFE.in_conv 140.7 -> 131.4 us; the
+  // k-groups double-buffered as well spill at 256 registers: 145.7)
+  auto load_kg = [&](const char* halo, int kg, bf16x8 (&bfr)[NT], bf16x8 (&afr)[RMW]) {
     const char* dys = halo + HB;
     FV_LDS char* hl = (FV_LDS char*)(halo);
-    for (int kg = 0; kg < NKG; ++kg) {
-      // B: dy[32 px][16 co] of every n-tile
-      bf16x8 bfr[NT];
 #pragma unroll
-      for (int n = 0; n < NT; ++n) bfr[n] = tfrag<LDD>(dys, kg * 32, n * 16, lane);   // co >= LDD lanes: ignored
-      // pixel rows 8g+q4 and 8g+4+q4 of this k-group -> halo pixel at tap (0,0)
-      const int p0 = kg * 32 + 8 * g + q4, p1 = p0 + 4;
-      const int hb0 = (p0 / TW) * HW + (p0 % TW), hb1 = (p1 / TW) * HW + (p1 % TW);
+    for (int n = 0; n < NT; ++n) bfr[n] = tfrag<LDD>(dys, kg * 32, n * 16, lane);   // co >= LDD lanes: ignored
+    // pixel rows 8g+q4 and 8g+4+q4 of this k-group -> halo pixel at tap (0,0)
+    const int p0 = kg * 32 + 8 * g + q4, p1 = p0 + 4;
+    const int hb0 = (p0 / TW) * HW + (p0 % TW), hb1 = (p1 / TW) * HW + (p1 % TW);
 #pragma unroll
-      for (int j = 0; j < RMW; ++j) {
-        bf16x8 af = bf16x8{};
-        if (aok[j]) {
-          const int ha = hb0 + aoff[j], hb = hb1 + aoff[j];
-          const int ca = ((akx[j] >> 3) ^ (ha & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
-          const int cb = ((akx[j] >> 3) ^ (hb & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
-          const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + ha * CIN * 2 + ca));
-          const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + hb * CIN * 2 + cb));
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
-          const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-          af = __builtin_bit_cast(bf16x8, v);
-        }
-#pragma unroll
-        for (int n = 0; n < NT; ++n) acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[n], acc[j][n], 0, 0, 0);
+    for (int j = 0; j < RMW; ++j) {
+      afr[j] = bf16x8{};
+      if (aok[j]) {
+        const int ha = hb0 + aoff[j], hb = hb1 + aoff[j];
+        const int ca = ((akx[j] >> 3) ^ (ha & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
+        const int cb = ((akx[j] >> 3) ^ (hb & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
+        const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + ha * CIN * 2 + ca));
+        const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + hb * CIN * 2 + cb));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+        afr[j] = __builtin_bit_cast(bf16x8, v);
       }
-      if (do_bias) {
+    }
+  };
+  auto mfma_kg = [&](const bf16x8 (&bfr)[NT], const bf16x8 (&afr)[RMW]) {
 #pragma unroll
-        for (int n = 0; n < NT; ++n) accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[n], accb[n], 0, 0, 0);
+    for (int j = 0; j < RMW; ++j)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[j], bfr[n], acc[j][n], 0, 0, 0);
+    if (do_bias) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[n], accb[n], 0, 0, 0);
+    }
+  };
+  auto compute = [&](int buf) {
+    const char* halo = smem + buf * BUF;
+    if constexpr (RMW * NT <= 16) {
+      for (int kg = 0; kg < NKG; ++kg) {
+        bf16x8 b0[NT], a0[RMW];
+        load_kg(halo, kg, b0, a0);
+        mfma_kg(b0, a0);
+      }
+    } else {
+      // many m-tiles per wave (64-channel input): each A fragment read right before its MFMAs
+      const char* dys = halo + HB;
+      FV_LDS char* hl = (FV_LDS char*)(halo);
+      for (int kg = 0; kg < NKG; ++kg) {
+        bf16x8 bfr[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) bfr[n] = tfrag<LDD>(dys, kg * 32, n * 16, lane);
+        const int p0 = kg * 32 + 8 * g + q4, p1 = p0 + 4;
+        const int hb0 = (p0 / TW) * HW + (p0 % TW), hb1 = (p1 / TW) * HW + (p1 % TW);
+#pragma unroll
+        for (int j = 0; j < RMW; ++j) {
+          bf16x8 af = bf16x8{};
+          if (aok[j]) {
+            const int ha = hb0 + aoff[j], hb = hb1 + aoff[j];
+            const int ca = ((akx[j] >> 3) ^ (ha & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
+            const int cb = ((akx[j] >> 3) ^ (hb & (CPP - 1))) * 16 + (akx[j] & 7) * 2;
+            const s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + ha * CIN * 2 + ca));
+            const s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((FV_LDS s16x4*)(hl + hb * CIN * 2 + cb));
+            typedef short s16x8 __attribute__((ext_vector_type(8)));
+            const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+            af = __builtin_bit_cast(bf16x8, v);
+          }
+#pragma unroll
+          for (int n = 0; n < NT; ++n) acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[n], acc[j][n], 0, 0, 0);
+        }
+        if (do_bias) {
+#pragma unroll
+          for (int n = 0; n < NT; ++n) accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[n], accb[n], 0, 0, 0);
+        }
       }
     }
   };
