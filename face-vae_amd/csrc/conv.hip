@@ -2151,6 +2151,170 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
 }
 
 // ----------------------------------------------------------------------------------------
+// conv3up_band_fwd: the UpBlock2D forward (nearest x2 upsample + 3x3 as 4 sub-pixel phases of a
+// 2x2 conv over the low-res input, modules.py:78-89) for a 128-channel input, as a sliding band
+// like conv3c64_fwd: a block owns (image, 32-column low-res strip = 64 output columns, 64 output
+// channels, band of low-res rows); wave (phase pa pb, 32-channel group cg) keeps its phase's
+// 32 co x K = 4 taps x 128 ci weights as MFMA A fragments in registers (128 VGPRs) for the whole
+// band, so the only LDS traffic is the input: low-res rows (34 pixels incl. the column halo) land
+// ONCE by LDS-DMA in a 6-row ring (272-B pixels: 16 consecutive pixels read by ds_read_b128 are
+// conflict-free) -- the halo kernel (MODE 1) restaged a 4-row halo per 32-channel chunk for only
+// 4 taps of work, bandwidth-bound.  An iteration = 2 low-res rows (4 output rows); wave (pa, pb)
+// writes output rows 2h + pa, columns 2w + pb.  Epilogue: bias, BN records of 256 pixels
+// (4 iterations x 2 rows x 32 columns of one phase; the two channel-group waves of the phase fill
+// the record's 64 channels), 16-B stores (v_permlane16_swap pairs the 16-channel fragments).
+// Weights: the sub-pixel layout of weight_prep_subpix_kernel, wk [4][rows][Kpad = 512].
+// ----------------------------------------------------------------------------------------
+constexpr int UPB_PXB = 272, UPB_ROWB = 10 * 1024, UPB_NR = 6, UPB_G = 4;
+__global__ void __launch_bounds__(512, 1)
+conv3up_band_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
+  __shared__ __attribute__((aligned(1024))) char smem[UPB_NR * UPB_ROWB];
+  __shared__ __attribute__((aligned(16))) float sbias[64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cg = wave & 1, ph = wave >> 1, pa = ph >> 1, pb = ph & 1;
+  const int lr = lane & 15, lh = lane >> 4;
+  // XCD-aware order: consecutive local ids (the co groups of one strip) share an XCD
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nblk / 8, r8 = nblk % 8, xcd = bid % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int nco = a.Cout >> 6, strips = a.Win >> 5;
+  const int cgrp = lid % nco, rest = lid / nco;
+  const int band = rest % nbands, strip = (rest / nbands) % strips, n = rest / (nbands * strips);
+  const int BAND = a.Hin / nbands, hb = band * BAND, wl0 = strip * 32;
+  const int cw = cgrp * 64 + cg * 32;                        // this wave's first output channel
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+  // DMA slots of a row: 16-B chunk k = piece * 64 + lane -> LDS pixel k / 17 (low-res column
+  // wl0 - 1 + k / 17), chunk k % 17 (chunk 16: the pad)
+  auto poff_of = [&](int p, int ln) {
+    const int k = p * 64 + ln, px = k / 17, ch = k - px * 17;
+    const int iw = wl0 - 1 + px;
+    return (px < 34 && ch < 16 && iw >= 0 && iw < a.Win) ? (unsigned)((iw * 128 + ch * 8) * 2) : 0x80000000u;
+  };
+  auto row_slot = [&](int y) { return (y - hb + 1) % UPB_NR; };
+  // piece q (0 .. 10 * rows - 1) of the rows starting at y0: row y0 + q / 10, piece q % 10
+  auto issue_piece = [&](int y0, int q) {                  // rows outside the image -> zeros
+    const int y = y0 + q / 10, p = q % 10;
+    const bool rok = y >= 0 && y < a.Hin;
+    dma16s(xr, sbase + row_slot(y) * UPB_ROWB + p * 1024, rok ? poff_of(p, lane) : 0x80000000u,
+           rok ? (unsigned)((n * a.Hin + y) * a.Win) * 256u : 0u);
+  };
+
+  // the wave's weights: A fragment (cf, ks) = 16 channels x 32 k, k = (rr * 2 + ss) * 128 + ci
+  bf16x8 wf[2][16];
+  const bf16* wk = reinterpret_cast<const bf16*>(a.w) + (long)ph * a.wphase;
+#pragma unroll
+  for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks)
+      wf[cf][ks] = *reinterpret_cast<const bf16x8*>(wk + (long)(cw + cf * 16 + lr) * a.Kpad + ks * 32 + lh * 8);
+
+  // prologue: low-res rows hb - 1 .. hb + 2 (40 pieces)
+  for (int q = wave; q < 40; q += 8) issue_piece(hb - 1, q);
+  if (tid < 64) sbias[tid] = a.bias ? a.bias[cgrp * 64 + tid] : 0.f;
+  __syncthreads();
+
+  float st[2][4], sq[2][4];
+#pragma unroll
+  for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[cf][i] = sq[cf][i] = 0.f;
+  const int niter = BAND >> 1, ng = niter / UPB_G;
+  const int rec0 = ((n * strips + strip) * nbands + band) * (4 * ng);
+  auto pk = [](float lo, float hi) {
+    const bf16 t[2] = {(bf16)lo, (bf16)hi};
+    return *reinterpret_cast<const unsigned*>(t);
+  };
+
+  for (int it = 0; it < niter; ++it) {
+    const int h0 = hb + 2 * it;
+    // this iteration's rows landed; younger than them are at most the previous iteration's 4
+    // output stores (+ record stores), which stay in flight
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const bool more = it + 1 < niter;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int h = h0 + hh;
+      // input rows h + pa - 1 + rr, LDS pixel of output column w: w + pb + ss (halo offset 1)
+      unsigned sb[2];
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) sb[rr] = (unsigned)(row_slot(h + pa - 1 + rr) * UPB_ROWB + (lr + pb) * UPB_PXB + lh * 16);
+      auto ldb = [&](bf16x8 (&fb)[2], int ks) {
+        const int tap = ks >> 2, rr = tap >> 1, ss = tap & 1, cc = ks & 3;
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          fb[m] = *reinterpret_cast<const bf16x8*>(smem + sb[rr] + (m * 16 + ss) * UPB_PXB + cc * 64);
+      };
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int cf = 0; cf < 2; ++cf) acc[m][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 fbq[2][2];
+      ldb(fbq[0], 0);
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        if (ks + 1 < 16) ldb(fbq[(ks + 1) & 1], ks + 1);
+        // the next iteration's rows h0 + 3, h0 + 4: pieces wave, wave + 8, wave + 16 < 20
+        if (hh == 0 && ks < 3 && more && wave + 8 * ks < 20) issue_piece(h0 + 3, wave + 8 * ks);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int cf = 0; cf < 2; ++cf)
+            acc[m][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cf][ks], fbq[ks & 1][m], acc[m][cf], 0, 0, 0);
+      }
+      // epilogue of output row 2h + pa: lane (lr, lh) holds channels cf * 16 + lh * 4 .. + 3 of
+      // column w = m * 16 + lr (output column 2 (wl0 + w) + pb)
+      const int Y = 2 * h + pa;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        float v[2][4];
+#pragma unroll
+        for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            v[cf][i] = acc[m][cf][i] + sbias[cg * 32 + cf * 16 + lh * 4 + i];
+            st[cf][i] += v[cf][i];
+            sq[cf][i] += v[cf][i] * v[cf][i];
+          }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(pk(v[0][0], v[0][1]), pk(v[1][0], v[1][1]), false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(pk(v[0][2], v[0][3]), pk(v[1][2], v[1][3]), false, false);
+        const int X = 2 * (wl0 + m * 16 + lr) + pb;
+        bf16* yp = reinterpret_cast<bf16*>(a.y) + ((long)(n * a.Ho + Y) * a.Wo + X) * a.ldy + cw + (lh & 1) * 16 +
+                   (lh >> 1) * 8;
+        *reinterpret_cast<uint4*>(yp) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    }
+    if (a.stats && (it % UPB_G) == UPB_G - 1) {
+      // record (block, 4-iteration group, phase): lanes 0-3 of a 16-lane row store the 4 channel
+      // sums, lanes 4-7 the squares (conv_epilogue's record layout)
+      const int rec = rec0 + (it / UPB_G) * 4 + ph;
+#pragma unroll
+      for (int cf = 0; cf < 2; ++cf) {
+        float sv[4], qv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sv[i] = row16_sum(st[cf][i]);
+          qv[i] = row16_sum(sq[cf][i]);
+          st[cf][i] = sq[cf][i] = 0.f;
+        }
+        const int cb = cw + cf * 16 + lh * 4, ii = lr & 3;
+        const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
+        const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
+        const float val = lr < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
+        if (lr < 8) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // 7x7 conv with a 64-channel input and <= 4 output channels (Generator.out_conv 64 -> 3,
 // models.py:1099 + sigmoid 1110), "column taps in N": for every input pixel w' of a row the
 // block computes D[h][w'][(co, s)] = sum_{r, ci} x[h + r - 3][w'][ci] * W[co][ci][r][s]
@@ -4357,8 +4521,22 @@ static bool up_halo_on() {
   const char* e = getenv("FV_UP_HALO");
   return !(e && e[0] == '0');
 }
+// UpBlock2D forward with a 128-channel input on the sliding-band kernel (conv3up_band_fwd;
+// FV_UPBAND=0: the halo kernel's MODE 1, A/B).  Its weights are the plain sub-pixel layout.
+static bool use_upband(const fv_conv_desc* d) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("FV_UPBAND");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!on || d->dtype != FV_BF16 || !use_subpix(d)) return false;
+  const int hl = d->h / 2, wl = d->w / 2;
+  return d->cin == 128 && d->cin_valid == 128 && d->cout % 64 == 0 && wl % 32 == 0 && hl % 8 == 0 &&
+         !d->out_nchw_f32 && !d->epi_sigmoid && !d->pro_act && d->ldy % 8 == 0 &&
+         (long)d->n * hl * wl * 128 * 2 < (1L << 31) && (long)d->n * d->h * d->w * d->ldy * 2 < (1L << 31);
+}
 static bool use_subpix_halo(const fv_conv_desc* d) {
-  if (!up_halo_on() || !use_subpix(d)) return false;
+  if (!up_halo_on() || !use_subpix(d) || use_upband(d)) return false;
   const int hl = d->h / 2, wl = d->w / 2;
   return d->cout % 64 == 0 && d->cin % 32 == 0 && d->cin >= 64 && d->cin_valid == d->cin && wl % 64 == 0 &&
          hl % 4 == 0 && !d->out_nchw_f32 && !d->epi_sigmoid && !d->pro_act && d->ldy % 8 == 0 &&
@@ -4786,6 +4964,7 @@ static FwdTile plan_tile(const fv_conv_desc* d) {
 // pixels per BN-statistics record = the pixels of one wave row of the tile (BM / WM)
 static int stats_record_pixels(const fv_conv_desc* d) {
   if (use_c7n(d)) return 64;
+  if (use_upband(d)) return UPB_G * 2 * 32;                  // (block, 4 iterations, phase)
   if (use_subpix_halo(d)) return 128;                         // (tile, wave row, phase): RM * 16                                  // one 64-pixel row segment
   if (use_c74(d)) return C74_TR * 64;                         // one record per tile
   if (use_c64(d)) return C64_G * 64;                          // 8 iterations x one wave's row
@@ -5095,6 +5274,21 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     else
       hipLaunchKernelGGL((conv_halo_fwd<7, 64, 1, 2, false, true>), dim3(nblk), dim3(512), 0, s, a, xb);
     return fv_check_launch("conv2d_fwd_halo");
+  }
+  if (use_upband(d)) {
+    FV_REQUIRE(!res && !a.spm, "sub-pixel band conv: no residual / store-pass records");
+    a.Ho = d->h; a.Wo = d->w;
+    a.Kpad = kpad_of(2, d->cin);
+    a.wphase = wrows(d->cout) * a.Kpad;
+    if ((st = wext(4L * wrows(d->cout), a.Kpad, "upband"))) return st;
+    const int hl = d->h / 2, wl = d->w / 2;
+    const long base = (long)d->n * (wl / 32) * (d->cout / 64);
+    int nb = 1;
+    while (base * nb < 256 && hl % (nb * 16) == 0) nb *= 2;      // bands of a multiple of 8 rows
+    const int nblk = (int)(base * nb);
+    const unsigned xb = (unsigned)((long)d->n * hl * wl * 128 * 2);
+    hipLaunchKernelGGL(conv3up_band_fwd, dim3(nblk), dim3(512), 0, s, a, xb, nb);
+    return fv_check_launch("conv2d_fwd_upband");
   }
   if (use_subpix_halo(d)) {
     FV_REQUIRE(!res && !a.spm, "sub-pixel conv: no residual / store-pass records");
