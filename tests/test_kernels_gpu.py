@@ -77,6 +77,8 @@ CONV_CASES = [
     # ... with low-res width 64: the sub-pixel weight gradient too
     (3, 128, 64, 8, 64, True, False),
     (3, 256, 128, 4, 64, True, False),
+    # the 128-channel-input forward on the sliding band (conv3up_band_fwd): 2 co groups, 2 bands
+    (3, 128, 128, 32, 64, True, False),
     # the full-size UpBlock2D convs (Generator.up at 256x256): fp32 parity of the large-P paths
     (3, 128, 64, 128, 128, True, False),
     (3, 256, 128, 64, 64, True, False),
