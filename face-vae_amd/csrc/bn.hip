@@ -466,7 +466,7 @@ __global__ void __launch_bounds__(NTH) act_fwd_q8_kernel(const T* __restrict__ y
     for (int q = 0; q < 8; ++q) o[q] = fv_act(f[q] * sc[q] + sh[q], slope);
     Chunk8<T> ch;
     ch.set8(o);
-    ch.store(out + (size_t)e * 8);
+    if (out) ch.store(out + (size_t)e * 8);             // (NULL: the e4m3 copy only)
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = ch.get(q);
     *reinterpret_cast<uint2*>(out8 + (size_t)e * 8) = q8_pack(o, s, m);
@@ -758,7 +758,7 @@ __global__ void __launch_bounds__(NTH) act_bwd_apply_q8_kernel(
     }
     Chunk8<T> ch;
     ch.set8(o);
-    ch.store(dx + (size_t)p * C + c);
+    if (dx) ch.store(dx + (size_t)p * C + c);           // (NULL: the e4m3 copy only)
 #pragma unroll
     for (int q = 0; q < 8; ++q) o[q] = ch.get(q);
     *reinterpret_cast<uint2*>(dx8 + (size_t)p * C + c) = q8_pack(o, s, m);
@@ -1035,7 +1035,7 @@ int fv_bn_act_fwd_q8(int dtype, const void* y, int n, int h, int w, int c, const
   FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, c);
   if (st) return st;
-  FV_REQUIRE(y && scale && shift && out && out8 && site, "bn_act_fwd_q8: null pointer");
+  FV_REQUIRE(y && scale && shift && out8 && site, "bn_act_fwd_q8: null pointer");
   const long n8 = (long)n * h * w * (c / 8);
   FV_REQUIRE(n8 * 8 < (1L << 31), "bn: tensor too large for 32-bit indexing");
   const int lgcpc = fv_ilog2(c / 8);
@@ -1057,7 +1057,7 @@ int fv_bn_act_bwd_apply_q8(int dtype, const void* dout, const void* y, int n, in
   FV_REQUIRE(fv_slope_ok(slope), "activation slope must be in [0, 1] (got %g)", (double)slope);
   int st = check_c(c, c);
   if (st) return st;
-  FV_REQUIRE(dout && y && mean && invstd && gamma && beta && k && dx && dx8 && site,
+  FV_REQUIRE(dout && y && mean && invstd && gamma && beta && k && dx8 && site,
              "bn_act_bwd_apply_q8: null pointer");
   FV_REQUIRE((long)n * h * w * c < (1L << 31), "bn: tensor too large for 32-bit indexing");
   const long work = (long)n * h * w * (c / 8);

@@ -661,17 +661,33 @@ def _q8_ok(site, y, pool, bn=None):
             and (bn is None or (bn.weight is not None and bn.bias is not None)))
 
 
-def bn_act_forward_q8(y, r: BNResult, slope, bn, site):
+_Q8_ONLY = os.environ.get("FV_Q8_ONLY", "1") == "1"   # tests/test_fp8_gpu.py flips it to compare with the bf16-writing passes
+
+
+def q8_only(cs: ConvState) -> bool:
+    """True when conv cs reads its input x (or its output gradient dy) ONLY as the e4m3 copy:
+    fp8 forward, fp8 data gradient and fp8 weight gradient (fv_conv2d_wgrad_fp8_supported), no
+    checker attached.  The producing BN pass then writes the e4m3 copy alone, not the bf16
+    tensor beside it (one bf16 write of the activation less per pass)."""
+    return _Q8_ONLY and CHECK is None and cs.fp8 and bool(query("fv_conv2d_wgrad_fp8_supported", ctypes.byref(cs.d)))
+
+
+def bn_act_forward_q8(y, r: BNResult, slope, bn, site, only8=False):
     """bn_act_forward for an fp8 consumer: -> (out, (e4m3 copy, dq) or None).  With a seeded
     delayed-scaling site the pass writes the consumer's fp8 operand beside `out`
-    (fv_bn_act_fwd_q8), so the conv needs no quantize pass of its own."""
+    (fv_bn_act_fwd_q8), so the conv needs no quantize pass of its own.  only8 (q8_only(consumer)):
+    the e4m3 copy alone -- `out` is then a 0-element placeholder of the right dtype / device."""
     if not _q8_ok(site, y, False):
         return bn_act_forward(y, r, slope, False, bn), None
     N, C, H, W = y.shape
-    out = torch.empty((N, C, H, W), dtype=y.dtype, device=y.device, memory_format=CL)
-    out8 = _empty(out.numel(), torch.uint8, y.device)
+    n = N * C * H * W
+    if only8:
+        out = torch.empty(0, dtype=y.dtype, device=y.device)
+    else:
+        out = torch.empty((N, C, H, W), dtype=y.dtype, device=y.device, memory_format=CL)
+    out8 = _empty(n, torch.uint8, y.device)
     call("fv_bn_act_fwd_q8", L.dtype_code(y.dtype), ptr(y), N, H, W, C, ptr(r.scale), ptr(r.shift), float(slope),
-         ptr(out), ptr(out8), ptr(site[0]), stream())
+         None if only8 else ptr(out), ptr(out8), ptr(site[0]), stream())
     if CHECK is not None:
         CHECK("bn_fwd", bn, y=y, r=r, slope=slope, pool=False, out=out)
     return out, (out8, site[0][18:19].view(F32))
@@ -686,11 +702,13 @@ def bn_backward_is_local(r: BNResult, comm) -> bool:
     return comm is None or (r.count == 0 and r.stats is None)
 
 
-def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True, recs=None, q8=None):
+def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, need_dx=True, recs=None, q8=None,
+                    only8=False):
     """-> (dx of the BN input, dgamma, dbeta).  recs: the BN-backward sums already reduced by
     the dgrad that produced dout (BNRecords), replacing the reduce pass.  q8: the delayed-scaling
     site of an fp8 data gradient consuming dx -> (dx, dgamma, dbeta, (e4m3 copy of dx, dq) or
-    None), the copy written by the apply pass itself (fv_bn_act_bwd_apply_q8)."""
+    None), the copy written by the apply pass itself (fv_bn_act_bwd_apply_q8); only8
+    (q8_only(consumer)): that copy alone, dx a 0-element placeholder."""
     N, C, H, W = y.shape
     dev = y.device
     dc = L.dtype_code(y.dtype)
@@ -735,12 +753,16 @@ def bn_act_backward(dout, y, bn, r: BNResult, slope, pool, comm, addend=None, ne
             call("fv_bn_bwd_finalize_dev", ptr(red), C, ptr(r.stats), None, None, ptr(k), stream())
     dx = q = None
     if need_dx:
-        dx = torch.empty((N, C, H, W), dtype=y.dtype, device=dev, memory_format=CL)
-        if _q8_ok(q8, y, pool, bn):
-            dx8 = _empty(dx.numel(), torch.uint8, dev)
+        q8ok = _q8_ok(q8, y, pool, bn)
+        if q8ok and only8:
+            dx = torch.empty(0, dtype=y.dtype, device=dev)
+        else:
+            dx = torch.empty((N, C, H, W), dtype=y.dtype, device=dev, memory_format=CL)
+        if q8ok:
+            dx8 = _empty(N * C * H * W, torch.uint8, dev)
             call("fv_bn_act_bwd_apply_q8", dc, ptr(dout), ptr(y), N, H, W, C, ptr(r.mean), ptr(r.invstd),
-                 ptr(bn.weight), ptr(bn.bias), float(slope), ptr(k), ptr(addend), ptr(dx), ptr(dx8), ptr(q8[0]),
-                 stream())
+                 ptr(bn.weight), ptr(bn.bias), float(slope), ptr(k), ptr(addend), None if only8 else ptr(dx),
+                 ptr(dx8), ptr(q8[0]), stream())
             q = (dx8, q8[0][18:19].view(F32))
         else:
             call("fv_bn_act_bwd_apply", dc, ptr(dout), ptr(y), N, H, W, C, C, ptr(r.mean), ptr(r.invstd),
@@ -949,13 +971,15 @@ class ResBlockFn(torch.autograd.Function):
         d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size)
         cs1 = ConvState(c1, d1, dtype, x.device, training, True, fp8=mode == FP8)
         # fp8 convs: the BN pass writes the conv's e4m3 operand beside its bf16 output
-        a1, q1 = bn_act_forward_q8(xb, r1, 0.0, blk.bn1, fp8_site(c1, "x", x.device) if cs1.fp8 else None)
+        a1, q1 = bn_act_forward_q8(xb, r1, 0.0, blk.bn1, fp8_site(c1, "x", x.device) if cs1.fp8 else None,
+                                   only8=q8_only(cs1))
         t1 = torch.empty_like(xb)
         part = conv_forward(cs1, a1, b1, y=t1, stats=training, x8=q1)
         r2 = bn_from_partials(blk.bn2, part, cs1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
         d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size)
         cs2 = ConvState(c2, d2, dtype, x.device, training, True, fp8=mode == FP8)
-        a2, q2 = bn_act_forward_q8(t1, r2, 0.0, blk.bn2, fp8_site(c2, "x", x.device) if cs2.fp8 else None)
+        a2, q2 = bn_act_forward_q8(t1, r2, 0.0, blk.bn2, fp8_site(c2, "x", x.device) if cs2.fp8 else None,
+                                   only8=q8_only(cs2))
         out = torch.empty_like(xb)
         geo = sr_records(d2, False) if training and not cs2.fp8 else None
         if geo is not None:
@@ -1050,7 +1074,8 @@ class ResBlockFn(torch.autograd.Function):
         # pass: step 12.46 -> 12.67 ms in r4, as in r2 -- DESIGN.md §4)
         da2, dw2, db2 = conv_backward(cs2, a2, dout, C, dy8=dy8)
         site1 = fp8_site(cs1.conv, "dy", xb.device) if cs1.fp8 else None
-        dt1, dg2, dbe2, *q = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, q8=site1)
+        dt1, dg2, dbe2, *q = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm, q8=site1,
+                                             only8=site1 is not None and q8_only(cs1))
         da1, dw1, db1 = conv_backward(cs1, a1, dt1, C, dy8=q[0] if q else None)
         prev = ctx.q8_prev
         dxb, dg1, dbe1, *q = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout,

@@ -467,7 +467,9 @@ int fv_bn_act_bwd_apply(int dtype, const void* dout, const void* y, int n, int h
  * conv that consumes it: out8 / dx8 [n][h][w][c] bytes = the bf16 output quantized with the
  * delayed scale of `site` (the consumer's fv_fp8_site_bytes site, already seeded), bit-identical
  * to fv_quantize_fp8_site over the output; the site's in-flight amax and dq are updated the
- * same way.  Replaces the separate quantize pass (one read of the output) */
+ * same way.  Replaces the separate quantize pass (one read of the output).  out / dx may be NULL:
+ * then only the e4m3 copy is written (its values are still the bf16-rounded outputs) -- for a
+ * consumer whose forward, data gradient and weight gradient all run on the e4m3 operands. */
 int fv_bn_act_fwd_q8(int dtype, const void* y, int n, int h, int w, int c, const float* scale,
                      const float* shift, float slope, void* out, void* out8, void* site, void* stream);
 int fv_bn_act_bwd_apply_q8(int dtype, const void* dout, const void* y, int n, int h, int w, int c,

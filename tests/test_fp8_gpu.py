@@ -206,6 +206,68 @@ def test_bn_passes_write_the_fp8_operand(addend):
     torch.cuda.synchronize()
     assert q is not None and torch.equal(dx, dx2)
     assert torch.equal(q[0], rq) and q[1].item() == rdq.item() and torch.equal(sa[0], sb[0])
+    # only8: the e4m3 copy alone, bit-identical, the bf16 output a 0-element placeholder
+    sa, sb = seeded_site(), seeded_site()
+    out, q = ops.bn_act_forward_q8(y, r, 0.0, bn, sa, only8=True)
+    _, rq = ops.bn_act_forward_q8(y, r, 0.0, bn, sb)
+    torch.cuda.synchronize()
+    assert out.numel() == 0 and out.dtype == y.dtype
+    assert torch.equal(q[0], rq[0]) and q[1].item() == rq[1].item() and torch.equal(sa[0], sb[0])
+    sa, sb = seeded_site(), seeded_site()
+    dx, _, _, q = ops.bn_act_backward(dout, y, bn, r, 0.0, False, None, addend=add, q8=sa, only8=True)
+    _, _, _, rq = ops.bn_act_backward(dout, y, bn, r, 0.0, False, None, addend=add, q8=sb)
+    torch.cuda.synchronize()
+    assert dx.numel() == 0 and dx.dtype == y.dtype
+    assert torch.equal(q[0], rq[0]) and q[1].item() == rq[1].item() and torch.equal(sa[0], sb[0])
+
+
+def test_resblock_fp8_only8_matches_bf16_copies():
+    """q8_only: the ResBlock's fp8 BN passes (a1, a2 forward; dt1 backward) write the e4m3 copy
+    alone when the consuming conv's forward, dgrad and wgrad all run on e4m3.  Output and every
+    gradient equal the run that also writes the bf16 tensors, and the placeholders are taken."""
+    from facevae_amd.modules import ResBlock2D
+    N, C, H, W = 2, 256, 8, 64
+    g = torch.Generator().manual_seed(41)
+    x0 = torch.randn(N, C, H, W, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    g1 = torch.randn(N, C, H, W, generator=g).cuda()
+    torch.manual_seed(7)
+    blk = ResBlock2D(C, True).cuda().train().set_compute_dtype(torch.float8_e4m3fn)
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+    seen = []
+    orig = ops.bn_act_forward_q8
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        seen.append(r[0].numel() == 0)
+        return r
+
+    def run(only8):
+        blk.load_state_dict(sd)
+        for m in (blk, blk.conv1, blk.conv2):
+            m.__dict__.pop("_fv_fp8_sites", None)
+            m.__dict__.pop("_fv_fp8_pending", None)
+        ops._Q8_ONLY = only8
+        ops.bn_act_forward_q8 = spy
+        seen.clear()
+        try:
+            for _ in range(2):                        # step 1 seeds the delayed-scaling sites
+                x = x0.clone().requires_grad_(True)
+                for p in blk.parameters():
+                    p.grad = None
+                out = blk(x)
+                (out.float() * g1).sum().backward()
+            torch.cuda.synchronize()
+            return out.detach().clone(), x.grad.clone(), [p.grad.clone() for p in blk.parameters()], list(seen)
+        finally:
+            ops._Q8_ONLY = True
+            ops.bn_act_forward_q8 = orig
+
+    o_on, dx_on, gr_on, seen_on = run(True)
+    o_off, dx_off, gr_off, seen_off = run(False)
+    assert torch.equal(o_on, o_off) and torch.equal(dx_on, dx_off)
+    for a, b in zip(gr_on, gr_off):
+        assert torch.equal(a, b)
+    assert seen_on[-2:] == [True, True] and not any(seen_off)
 
 
 @pytest.mark.parametrize("two_consumers", [False, True])
