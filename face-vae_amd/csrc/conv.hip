@@ -265,7 +265,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     }
   }
 
-  if (a.stats) {
+  // (a wave row wholly past the last pixel -- the tail of a partial pixel tile -- has no record:
+  // the caller sized the buffer with cdiv(P, RM*16) of them, fv_conv2d_stats_blocks)
+  if (a.stats && (long)(tm * WM + wm) * (RM * 16) < a.P) {
     // BN statistics partials, one record per wave row (RM*16 pixels, record index
     // tm*WM + wm): per output channel (sum, sum of squares) over the record's valid pixels,
     // reduced over the 16 pixel lanes of each m-tile by shuffles -- no LDS, no barrier.
