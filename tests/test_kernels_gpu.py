@@ -112,10 +112,15 @@ def test_conv_fwd(case, dtype, monkeypatch):
         y = torch.empty(shp, dtype=dtype, device="cuda", memory_format=CL)
     scd, shd = sc.cuda(), sh.cuda()
     nb = L.query("fv_conv2d_stats_blocks", ctypes.byref(d))
-    part = torch.empty(nb * 2 * cout, device="cuda")
+    # records + a guard region: no launch writes a record past the nb the query sized (a partial
+    # pixel tile's empty wave rows once did, an illegal address when the buffer ended a mapping)
+    guard = 4 * 2 * cout
+    pbuf = torch.full((nb * 2 * cout + guard,), 1234.5, device="cuda")
+    part = pbuf[:nb * 2 * cout]
     L.call("fv_conv2d_fwd", ctypes.byref(d), xb.data_ptr(), wk.data_ptr(), b.cuda().data_ptr(),
            L.ptr(scd if pro else None), L.ptr(shd if pro else None), None, y.data_ptr(), part.data_ptr(), L.stream())
     torch.cuda.synchronize()
+    assert bool((pbuf[nb * 2 * cout:] == 1234.5).all()), "BN records written past fv_conv2d_stats_blocks"
     assert rel(y.float(), ref) < TOL[dtype] * (1 if dtype == torch.float32 else 1.5)
     # block partials -> exact batch statistics
     if cout % 8 == 0:
