@@ -265,9 +265,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
     }
   }
 
-  // (a wave row wholly past the last pixel -- the tail of a partial pixel tile -- has no record:
-  // the caller sized the buffer with cdiv(P, RM*16) of them, fv_conv2d_stats_blocks)
-  if (a.stats && (long)(tm * WM + wm) * (RM * 16) < a.P) {
+  // (records past cdiv(output pixels, RM*16) -- the empty wave rows of a partial last pixel
+  // tile -- are not written: the caller sized the buffer with that many, fv_conv2d_stats_blocks;
+  // the sub-pixel launches number records over the 4 phases of a low-res a.P, hence Ho x Wo)
+  const long pout = a.Ho ? (long)a.N * a.Ho * a.Wo : (long)a.P;
+  if (a.stats && (long)(tm * WM + wm) < (pout + RM * 16 - 1) / (RM * 16)) {
     // BN statistics partials, one record per wave row (RM*16 pixels, record index
     // tm*WM + wm): per output channel (sum, sum of squares) over the record's valid pixels,
     // reduced over the 16 pixel lanes of each m-tile by shuffles -- no LDS, no barrier.
