@@ -22,9 +22,10 @@ item's `driving`; `source` is not decoded -- the FaceVAE step never reads it).
 `to_device_frames` turns a collated uint8 batch into the float32 NCHW [0, 1] tensor on the
 GPU -- x times fp32(1/255), bit-identical to img_as_float32 on the CPU (`u8_to_float`).
 
-`PairedDataset` is dataset.py:154-193 (source / driving pairs for animation), and
 `SyntheticFramesDataset` produces VoxCeleb-shaped frames x ~ U[0, 1) deterministically per
-index (the benchmark / test input when no dataset is on disk).
+index (the benchmark / test input when no dataset is on disk).  The reference's
+`PairedDataset` (dataset.py:154-193: source / driving pairs for the animation evaluation) is
+not on the FaceVAE training path and is not provided.
 """
 from __future__ import annotations
 
@@ -188,43 +189,6 @@ class DatasetRepeater(Dataset):
 
     def __getitem__(self, idx):
         return self.dataset[idx % len(self.dataset)]
-
-
-class PairedDataset(Dataset):
-    """dataset.py:154-193: (driving, source) index pairs over an initial dataset -- random
-    distinct pairs (seeded) or the rows of a pairs csv (`source`, `driving` video names)."""
-
-    def __init__(self, initial_dataset, number_of_pairs, seed=0):
-        self.initial_dataset = initial_dataset
-        pairs_list = self.initial_dataset.pairs_list
-        np.random.seed(seed)
-        if pairs_list is None:
-            max_idx = min(number_of_pairs, len(initial_dataset))
-            nx, ny = max_idx, max_idx
-            xy = np.mgrid[:nx, :ny].reshape(2, -1).T
-            number_of_pairs = min(xy.shape[0], number_of_pairs)
-            self.pairs = xy.take(np.random.choice(xy.shape[0], number_of_pairs, replace=False), axis=0)
-        else:
-            import pandas as pd
-            videos = self.initial_dataset.videos
-            name_to_index = {name: index for index, name in enumerate(videos)}
-            pairs = pd.read_csv(pairs_list)
-            pairs = pairs[np.logical_and(pairs["source"].isin(videos), pairs["driving"].isin(videos))]
-            number_of_pairs = min(pairs.shape[0], number_of_pairs)
-            self.pairs = [(name_to_index[pairs["driving"].iloc[i]], name_to_index[pairs["source"].iloc[i]])
-                          for i in range(number_of_pairs)]
-            self.start_frames = []
-
-    def __len__(self):
-        return len(self.pairs)
-
-    def __getitem__(self, idx):
-        pair = self.pairs[idx]
-        first = self.initial_dataset[pair[0]]
-        second = self.initial_dataset[pair[1]]
-        first = {"driving_" + key: value for key, value in first.items()}
-        second = {"source_" + key: value for key, value in second.items()}
-        return {**first, **second}
 
 
 class SyntheticFramesDataset(Dataset):
