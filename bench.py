@@ -148,6 +148,12 @@ def pmc_counters(cfg, B, dtype, fam, avg_ms):
 
 def main():
     args = parse()
+
+    def comm_count():
+        """ranks the RCCL communicator spans (ncclCommCount), None without one"""
+        c = fv.distributed.get_comm()
+        return c.count() if isinstance(c, fv.distributed.RcclComm) else None
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -280,6 +286,7 @@ def main():
         "launch": ("hip graph (one captured step replayed)" if world == 1 else
                    "hip graph segments between the collectives (StepGraph)") if use_graph else "eager",
         "comm": None if world == 1 else args.comm,
+        "rccl_comm_count": comm_count(),
         "loss_last": round(loss.item(), 6),
         "mfma_util_step": round(step_util, 4),
         "step_flop_per_image": f_img,

@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.realpath(__file__))
 LIB_PATH = os.environ.get("FV_LIB_PATH") or os.path.join(_HERE, "libfacevae.so")
 
 FV_F32, FV_BF16, FV_F64 = 0, 1, 2
+FV_E_BADARG, FV_E_UNSUPPORTED, FV_E_COMM = 1001, 1002, 1003
 ADAM_CHUNK = 4096
 ABI_VERSION = 2
 
@@ -202,6 +203,9 @@ _SIGS = {
     "fv_comm_allgather": (c_int, [c_void_p, P, P, c_size_t, c_int, P]),
     "fv_comm_broadcast": (c_int, [c_void_p, P, c_size_t, c_int, c_int, P]),
     "fv_comm_destroy": (c_int, [c_void_p]),
+    "fv_comm_async_error": (c_int, [c_void_p, POINTER(c_int)]),
+    "fv_comm_count": (c_int, [c_void_p, POINTER(c_int)]),
+    "fv_comm_abort": (c_int, [c_void_p]),
 }
 
 _lib = None

@@ -55,6 +55,7 @@ int fv_comm_init(const uint8_t id[128], int nranks, int rank, int device, fv_com
 }
 
 int fv_comm_allreduce(fv_comm_t comm, void* buf, size_t count, int dtype, int op, void* stream) {
+  FV_REQUIRE(op >= 0 && op <= 2, "allreduce: unknown op %d (0 = sum, 1 = average, 2 = max)", op);
   FV_REQUIRE(comm && buf, "allreduce: bad args");
   ncclDataType_t dt;
   int st = map_dtype(dtype, &dt);
@@ -81,6 +82,33 @@ int fv_comm_broadcast(fv_comm_t comm, void* buf, size_t count, int dtype, int ro
   if (st) return st;
   return nccl_check(ncclBroadcast(buf, buf, count, dt, root, (ncclComm_t)comm, (hipStream_t)stream),
                     "ncclBroadcast");
+}
+
+// Failure detection (the reference's mp.spawn tears every rank down on an exception,
+// train.py:54; a dead or stuck peer otherwise hangs every rank inside its next collective).
+// *result = the communicator's asynchronous error (ncclResult_t; 0 = ncclSuccess, 7 =
+// ncclInProgress).  Host-only query, safe from a watchdog thread while collectives are queued.
+int fv_comm_async_error(fv_comm_t comm, int* result) {
+  FV_REQUIRE(comm && result, "async_error: bad args");
+  ncclResult_t r = ncclSuccess;
+  int st = nccl_check(ncclCommGetAsyncError((ncclComm_t)comm, &r), "ncclCommGetAsyncError");
+  if (st) return st;
+  *result = (int)r;
+  if (r != ncclSuccess && r != ncclInProgress) fv_set_error("RCCL async error: %s", ncclGetErrorString(r));
+  return FV_OK;
+}
+
+// number of ranks the communicator spans (ncclCommCount)
+int fv_comm_count(fv_comm_t comm, int* nranks) {
+  FV_REQUIRE(comm && nranks, "comm_count: bad args");
+  return nccl_check(ncclCommCount((ncclComm_t)comm, nranks), "ncclCommCount");
+}
+
+// abort every outstanding operation of the communicator and free it (ncclCommAbort); the
+// handle is invalid afterwards
+int fv_comm_abort(fv_comm_t comm) {
+  if (!comm) return FV_OK;
+  return nccl_check(ncclCommAbort((ncclComm_t)comm), "ncclCommAbort");
 }
 
 int fv_comm_destroy(fv_comm_t comm) {

@@ -33,7 +33,11 @@ from __future__ import annotations
 import ctypes
 import os
 import random
-from typing import Dict, List, Optional
+import sys
+import threading
+import time
+from collections import deque
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 import torch
@@ -56,6 +60,90 @@ def _deferred(op):
 
 FIRST_BUCKET_MB = 1.0   # torch/nn/parallel/distributed.py _DEFAULT_FIRST_BUCKET_BYTES
 
+# failure detection: a collective still pending after COMM_TIMEOUT_S seconds, or an RCCL async
+# error, ends the process (see CommWatchdog)
+COMM_TIMEOUT_S = float(os.environ.get("FV_COMM_TIMEOUT", "600"))
+COMM_POLL_S = float(os.environ.get("FV_COMM_POLL", "1.0"))
+
+# ncclResult_t values that are not failures
+_NCCL_OK, _NCCL_IN_PROGRESS = 0, 7
+
+
+class CommWatchdog:
+    """Fail-fast for the collectives of one communicator (the reference's
+    mp.spawn tears every rank down when one raises, train.py:54, and torch's ProcessGroupNCCL
+    watchdog aborts a timed-out collective).
+
+    Every issued collective is tracked as (done(), issue time, name).  A daemon thread polls
+    every `poll_s` while anything is pending: completed entries are dropped, the communicator's
+    asynchronous error is queried (`async_error()` -> ncclResult_t), and an error other than
+    success / in-progress, or an entry pending for more than `timeout_s`, calls `abort()` (RCCL
+    abandons the outstanding collectives) and then `exit_fn(1)` after printing the reason with
+    the rank to stderr.  `exit_fn` is os._exit: the process ends without running atexit
+    handlers that could block on the dead communicator, and never re-execs.  While a segmented
+    graph capture is in progress (no collective is issued then) the thread does not poll."""
+
+    def __init__(self, rank: int, async_error: Callable[[], int], abort: Callable[[], None],
+                 timeout_s: float = COMM_TIMEOUT_S, poll_s: float = COMM_POLL_S,
+                 exit_fn: Callable[[int], None] = os._exit):
+        self.rank, self._async_error, self._abort = rank, async_error, abort
+        self.timeout_s, self.poll_s, self._exit = timeout_s, poll_s, exit_fn
+        self._pending = deque()
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self.failed: Optional[str] = None
+        self._thread = threading.Thread(target=self._run, name=f"fv-comm-watchdog-{rank}", daemon=True)
+        self._thread.start()
+
+    def track(self, done: Callable[[], bool], what: str):
+        with self._lock:
+            self._pending.append((done, time.monotonic(), what))
+
+    def pending(self) -> int:
+        with self._lock:
+            return len(self._pending)
+
+    def check(self) -> Optional[str]:
+        """One poll; returns the failure reason (None while healthy)."""
+        with self._lock:
+            while self._pending and self._pending[0][0]():
+                self._pending.popleft()
+            oldest = self._pending[0] if self._pending else None
+        if oldest is None:
+            return None
+        r = self._async_error()
+        if r not in (_NCCL_OK, _NCCL_IN_PROGRESS):
+            return f"RCCL asynchronous error {r} while {oldest[2]} was pending"
+        age = time.monotonic() - oldest[1]
+        if age > self.timeout_s:
+            return f"{oldest[2]} pending for {age:.0f} s (> FV_COMM_TIMEOUT {self.timeout_s:.0f} s): a peer is dead or stuck"
+        return None
+
+    def _fail(self, why: str):
+        self.failed = why
+        print(f"[facevae rank {self.rank}] communicator failure: {why}; aborting the communicator and exiting",
+              file=sys.stderr, flush=True)
+        try:
+            self._abort()
+        finally:
+            self._exit(1)
+
+    def _run(self):
+        while not self._stop.wait(self.poll_s):
+            if _SEGMENTS is not None:
+                continue
+            try:
+                why = self.check()
+            except Exception as e:          # a failing query is a failure too
+                why = f"watchdog query failed: {e}"
+            if why is not None:
+                self._fail(why)
+                return
+
+    def stop(self):
+        self._stop.set()
+        self._thread.join(timeout=5 * self.poll_s + 1)
+
 
 class RcclComm:
     """fv_comm_* communicator bound to one GPU.  All of its collectives run on its own comm
@@ -70,6 +158,7 @@ class RcclComm:
         L.call("fv_comm_init", ctypes.addressof(buf), world_size, rank, device, ctypes.byref(h))
         self._h = h
         self.stream = torch.cuda.Stream(device=device)
+        self.watchdog = CommWatchdog(rank, self.async_error, self.abort) if world_size > 1 else None
 
     @staticmethod
     def unique_id() -> bytes:
@@ -78,10 +167,34 @@ class RcclComm:
         L.call("fv_comm_unique_id", ctypes.addressof(buf))
         return bytes(buf)
 
-    def _launch(self, fn, t: torch.Tensor, wait_back: bool):
+    def async_error(self) -> int:
+        """ncclCommGetAsyncError of the communicator (0 = success, 7 = in progress)."""
+        r = ctypes.c_int(0)
+        self._L.call("fv_comm_async_error", self._h, ctypes.byref(r))
+        return r.value
+
+    def count(self) -> int:
+        """Ranks the RCCL communicator spans (ncclCommCount)."""
+        n = ctypes.c_int(0)
+        self._L.call("fv_comm_count", self._h, ctypes.byref(n))
+        return n.value
+
+    def abort(self):
+        """ncclCommAbort: abandon the outstanding collectives and free the communicator."""
+        h, self._h = self._h, None
+        if h:
+            self._L.query("fv_comm_abort", h)
+
+    def _launch(self, fn, t: torch.Tensor, wait_back: bool, what: str = "collective"):
+        if self._h is None:
+            raise RuntimeError("RcclComm: the communicator was destroyed or aborted")
         cur = torch.cuda.current_stream(t.device)
         self.stream.wait_stream(cur)
         fn(self.stream.cuda_stream)
+        if self.watchdog is not None:
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            self.watchdog.track(ev.query, f"{what} of {t.numel()} x {t.dtype}")
         t.record_stream(self.stream)
         if wait_back:
             cur.wait_stream(self.stream)
@@ -95,14 +208,14 @@ class RcclComm:
         L = self._L
         code = {"sum": 0, "avg": 1, "max": 2}[op]
         return self._launch(lambda s: L.call("fv_comm_allreduce", self._h, t.data_ptr(), t.numel(),
-                                             L.dtype_code(t.dtype), code, s), t, wait_back)
+                                             L.dtype_code(t.dtype), code, s), t, wait_back, f"all-reduce ({op})")
 
     def broadcast_(self, t: torch.Tensor, root: int = 0, wait_back: bool = True):
         if _deferred(lambda: self.broadcast_(t, root, wait_back)):
             return t
         L = self._L
         return self._launch(lambda s: L.call("fv_comm_broadcast", self._h, t.data_ptr(), t.numel(),
-                                             L.dtype_code(t.dtype), root, s), t, wait_back)
+                                             L.dtype_code(t.dtype), root, s), t, wait_back, "broadcast")
 
     def fence(self, device=None):
         """Make the caller's stream wait for every collective issued so far."""
@@ -111,6 +224,9 @@ class RcclComm:
         torch.cuda.current_stream(device).wait_stream(self.stream)
 
     def destroy(self):
+        if self.watchdog is not None:
+            self.watchdog.stop()
+            self.watchdog = None
         if self._h:
             self._L.call("fv_comm_destroy", self._h)
             self._h = None
@@ -310,16 +426,24 @@ class DataParallel(torch.nn.Module):
         if self.world > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
-            # fp8 operands (config C5): one scale per operand for the whole global batch, as
-            # SyncBN's statistics (ops.quantize_fp8_site seeds, _sync_fp8 rolls once per step)
-            from . import _lib, ops
-            ops.FP8_GLOBAL = self.comm
-            _lib.call("fv_fp8_set_deferred_roll", 1)
+
+    def _global_fp8(self, on: bool):
+        """fp8 operands (config C5): one scale per operand for the whole global batch, as
+        SyncBN's statistics (ops.quantize_fp8_site seeds through the communicator, the convs
+        leave their amax in-flight and _sync_fp8 rolls every site once per step).  Scoped to
+        this wrapper's training step -- switched on by forward, off by the end-of-backward
+        callback -- so an fp8 module used outside it (an eval copy, a second model) rolls its
+        own sites and never issues a collective the other ranks do not match."""
+        from . import _lib, ops
+        ops.FP8_GLOBAL = self.comm if on else None
+        _lib.call("fv_fp8_set_deferred_roll", 1 if on else 0)
 
     def forward(self, *args, **kwargs):
         self._pending = [len(b) for b in self.buckets]
         self._armed = False
         self.launch_order = []
+        if self.world > 1:
+            self._global_fp8(self.module.training and torch.is_grad_enabled())
         return self.module(*args, **kwargs)
 
     def _flat_buf(self, bi, like):
@@ -363,6 +487,14 @@ class DataParallel(torch.nn.Module):
         key = tuple(t.data_ptr() for t in sites)
         if key != self._fp8_key:
             dev = sites[0].device
+            # the MAX all-reduce below must have the same length on every rank (a site created
+            # by a forward only one rank ran would misalign it): check the counts once per set
+            cnt = torch.tensor([len(sites), -len(sites)], dtype=torch.float64, device=dev)
+            self.comm.allreduce_(cnt, op="max", wait_back=True)
+            hi, lo = cnt.tolist()
+            if hi != -lo:
+                raise RuntimeError(f"DataParallel fp8: ranks hold {int(-lo)}..{int(hi)} delayed-scaling sites "
+                                   f"(this rank {len(sites)}); every rank must run the same fp8 forwards")
             self._fp8_tab = torch.tensor(key, dtype=torch.int64).to(dev)
             self._fp8_amax = torch.empty(len(sites), dtype=torch.float32, device=dev)
             self._fp8_key = key
@@ -379,6 +511,7 @@ class DataParallel(torch.nn.Module):
                                    "(unused parameters are not supported)")
         if self._params and self._params[0].is_cuda:
             self._sync_fp8()
+        self._global_fp8(False)
         if self._params:
             self.comm.fence(self._params[0].device if self._params[0].is_cuda else None)
         for bi, b in enumerate(self.buckets):

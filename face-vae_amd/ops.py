@@ -510,6 +510,13 @@ def conv_backward(cs: ConvState, x, dy, ldd, pro=None, need_dx=True, need_db=Tru
         dy8 = dy8 if dy8 is not None else quantize_fp8_site(dy, site)
         dw, db = _wgrad_fp8(cs, x, dy, ldd, need_db, dy8)
     else:
+        if x.numel() == 0 or (dy.numel() == 0 and dy8 is None):
+            # q8_only: the activation / gradient exists only as its e4m3 copy, which the first
+            # backward consumed (cs.x8 released); a second backward (retain_graph=True) would
+            # read the 0-element placeholder
+            raise RuntimeError("conv backward: the bf16 operand of this fp8 conv was never materialised "
+                               "(FV_Q8_ONLY) and its e4m3 copy was released by an earlier backward; "
+                               "backward through an fp8 ResBlock runs once (no retain_graph)")
         dw, db = _wgrad(cs, x, dy, ldd, pro, need_db)
     dx, recs = _dgrad(cs, dy, ldd, need_dx, bnred, dy8)
     return (dx, dw, db, recs) if want_recs else (dx, dw, db)

@@ -570,7 +570,8 @@ int fv_copy_h2d_async(void* dst, const void* src_pinned, size_t bytes, void* str
 typedef void* fv_comm_t;
 int fv_comm_unique_id(uint8_t out[128]);
 int fv_comm_init(const uint8_t id[128], int nranks, int rank, int device, fv_comm_t* comm);
-/* op: 0 = sum, 1 = average, 2 = max; dtype: FV_F32 / FV_BF16 / FV_F64 */
+/* op: 0 = sum, 1 = average, 2 = max (anything else: FV_E_BADARG); dtype: FV_F32 / FV_BF16 /
+ * FV_F64 */
 int fv_comm_allreduce(fv_comm_t comm, void* buf, size_t count, int dtype, int op,
                       void* stream);
 int fv_comm_allgather(fv_comm_t comm, const void* send, void* recv, size_t count_per_rank,
@@ -578,6 +579,14 @@ int fv_comm_allgather(fv_comm_t comm, const void* send, void* recv, size_t count
 int fv_comm_broadcast(fv_comm_t comm, void* buf, size_t count, int dtype, int root,
                       void* stream);
 int fv_comm_destroy(fv_comm_t comm);
+/* Failure detection (replaces the teardown the reference gets from mp.spawn, train.py:54, and
+ * NCCL_ASYNC_ERROR_HANDLING under init_process_group("nccl"), distributed.py:24-31):
+ * *result = ncclCommGetAsyncError (0 = success, 7 = in progress; other values also set
+ * fv_last_error), host-only, callable from a watchdog thread; fv_comm_count = ncclCommCount;
+ * fv_comm_abort = ncclCommAbort (outstanding collectives abandoned, handle freed). */
+int fv_comm_async_error(fv_comm_t comm, int* result);
+int fv_comm_count(fv_comm_t comm, int* nranks);
+int fv_comm_abort(fv_comm_t comm);
 
 #ifdef __cplusplus
 }

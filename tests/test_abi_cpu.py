@@ -127,3 +127,65 @@ def test_full_size_afe_generator_state_dicts_match_reference():
     for name, mod in (("afe", fv.AFE()), ("generator", fv.Generator())):
         got = [[k, list(v.shape)] for k, v in mod.state_dict().items()]
         assert got == gold[name], name
+
+
+def test_comm_entry_points_reject_bad_arguments(lib_built):
+    """fv_comm_allreduce returns FV_E_BADARG for an op outside {sum, average, max} (VERDICT r5
+    weak 8: it used to map any op to ncclSum) -- checked before the communicator is touched,
+    so no GPU is needed -- and the failure-detection entries refuse a NULL communicator."""
+    import ctypes
+    import fvamd  # noqa: F401
+    from facevae_amd import _lib
+    lib = _lib.load()
+    for op in (3, -1, 99):
+        st = lib.fv_comm_allreduce(None, None, 0, _lib.FV_F32, op, None)
+        assert st == _lib.FV_E_BADARG, st
+        assert b"unknown op" in lib.fv_last_error()
+    r = ctypes.c_int(-5)
+    assert lib.fv_comm_async_error(None, ctypes.byref(r)) == _lib.FV_E_BADARG and r.value == -5
+    assert lib.fv_comm_count(None, ctypes.byref(r)) == _lib.FV_E_BADARG
+    assert lib.fv_comm_abort(None) == 0                # nothing to abort
+
+
+def test_comm_watchdog_fails_fast():
+    """distributed.CommWatchdog (SURVEY.md §5 fail-fast): a collective pending past the
+    deadline, or an RCCL asynchronous error while one is pending, aborts the communicator and
+    exits the process (os._exit, never a re-exec); completed collectives are dropped and a
+    healthy communicator is left alone."""
+    import threading
+    import time
+    import fvamd  # noqa: F401
+    from facevae_amd import distributed as D
+
+    def make(err=0, timeout=0.3):
+        calls = []
+        done = threading.Event()
+        wd = D.CommWatchdog(0, lambda: err, lambda: calls.append("abort"), timeout_s=timeout, poll_s=0.02,
+                            exit_fn=lambda code: (calls.append(("exit", code)), done.set()))
+        return wd, calls, done
+
+    wd, calls, done = make()
+    flag = {"v": False}
+    wd.track(lambda: flag["v"], "all-reduce (avg) of 8 x torch.float32")
+    assert wd.check() is None and wd.pending() == 1
+    flag["v"] = True
+    assert wd.check() is None and wd.pending() == 0
+    time.sleep(0.5)
+    assert calls == [] and wd.failed is None
+    wd.stop()
+
+    wd, calls, done = make(timeout=0.2)
+    wd.track(lambda: False, "all-reduce (sum) of 3 x torch.float64")
+    assert done.wait(5)
+    assert calls == ["abort", ("exit", 1)] and "pending for" in wd.failed and "all-reduce (sum)" in wd.failed
+
+    wd, calls, done = make(err=3, timeout=100)            # ncclInternalError
+    wd.track(lambda: False, "broadcast of 1 x torch.float32")
+    assert done.wait(5)
+    assert calls == ["abort", ("exit", 1)] and "asynchronous error 3" in wd.failed
+
+    wd, calls, done = make(err=7, timeout=100)            # ncclInProgress is not a failure
+    wd.track(lambda: False, "x")
+    time.sleep(0.3)
+    assert calls == []
+    wd.stop()

@@ -43,6 +43,34 @@ def test_rccl_world1_collectives():
         comm.destroy()
 
 
+def test_rccl_failure_detection_world1():
+    """the async-error query of a healthy communicator returns success
+    (ncclSuccess) before and after collectives, ncclCommCount sees the one rank, a watchdog
+    around the communicator tracks the collectives to completion without firing, and abort
+    frees it (later collectives raise instead of touching a dead handle)."""
+    D = fv.distributed
+    torch.cuda.set_device(0)
+    comm = D.RcclComm(0, 1, 0, D.RcclComm.unique_id())
+    assert comm.watchdog is None                       # world 1: nothing can hang
+    assert comm.async_error() == 0 and comm.count() == 1
+    fired = []
+    comm.watchdog = D.CommWatchdog(0, comm.async_error, lambda: fired.append("abort"), timeout_s=60, poll_s=0.05,
+                                   exit_fn=lambda c: fired.append(c))
+    t = torch.randn(1 << 20, device="cuda")
+    for _ in range(4):
+        comm.allreduce_(t, op="sum", wait_back=False)
+    comm.fence()
+    torch.cuda.synchronize()
+    assert comm.watchdog.check() is None and comm.watchdog.pending() == 0
+    assert comm.async_error() == 0 and fired == []
+    comm.watchdog.stop()
+    comm.watchdog = None
+    comm.abort()
+    with pytest.raises(RuntimeError):
+        comm.allreduce_(t, op="sum")
+    comm.destroy()                                      # no-op after abort
+
+
 def test_dataparallel_over_rccl_world1_is_transparent():
     """DataParallel around the toy model with a world-1 RCCL communicator: no hooks, no
     broadcast, the step equals the bare model's step bit for bit."""

@@ -416,3 +416,139 @@ def test_dataparallel_segmented_graph_matches_eager(dtype_name):
                 assert _rel(sdg[k], sde[k]) < 1e-6, (rank, k)
             else:
                 assert torch.equal(sdg[k], sde[k]), (rank, k)
+
+
+def _site_words(m):
+    """{module name / operand: the 32 site words} of every fp8 delayed-scaling site of m."""
+    out = {}
+    for name, mod in m.named_modules():
+        for which, st in sorted(mod.__dict__.get("_fv_fp8_sites", {}).items()):
+            out[f"{name}/{which}"] = st[0].detach().cpu().clone()
+    return out
+
+
+def _fp8_steps_worker(rank, port, q):
+    """Rank of the multi-step fp8 test: the real 256x256 model in fp8 under DataParallel +
+    SyncBN, two training steps eagerly and then (same initial weights) one eager warm-up step +
+    one replay of the segmented graph; returns every site's words after each run and whether
+    the process-wide global-scaling switches were off again after the steps."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import fvamd  # noqa: F401
+        import facevae_amd as fv
+        D = fv.distributed
+        torch.cuda.set_device(0)
+        comm = D.TorchComm()
+        D.install(comm, syncbn=True)
+        cfg = fv.FaceVAEConfig(H=256)
+        x, eps = _inputs(cfg.H, cfg.latent, cfg.latent_hw)
+        sl = slice(PER_RANK * rank, PER_RANK * (rank + 1))
+        xs, es = x[sl].cuda(), eps[sl].cuda()
+        res = {}
+        for mode in ("eager", "graph"):
+            torch.manual_seed(10 + rank)
+            m = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(torch.float8_e4m3fn)
+            dp = D.DataParallel(m, comm)
+            init = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+            opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
+
+            def step():
+                opt.zero_grad(set_to_none=True)
+                y, mu, logstd = dp(xs, es)
+                loss = cfg.w_R * fv.ReconLoss()((xs, y)) + cfg.w_K * fv.KLDivergenceLoss()((mu, logstd))
+                loss.backward()
+                opt.step()
+                return loss
+
+            if mode == "eager":
+                losses = [step().item() for _ in range(2)]
+            else:
+                sg = fv.StepGraph(step, [opt], warmup=1).capture()
+                losses = [sg.warm_out.item(), sg.replay().item()]
+            torch.cuda.synchronize()
+            off = fv.ops.FP8_GLOBAL is None
+            res[mode] = (losses, _site_words(m), off, init)
+        buf = io.BytesIO()
+        torch.save((rank, res), buf)
+        q.put(buf.getvalue())
+    except Exception as e:
+        buf = io.BytesIO()
+        torch.save((rank, repr(e)), buf)
+        q.put(buf.getvalue())
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dataparallel_fp8_sites_roll_globally_over_steps():
+    """under DataParallel every fp8 site's amax history is rolled once per
+    step from the all-reduced (MAX) in-flight amax, so after two steps -- eager, and with the
+    segmented graph -- both ranks hold bit-identical site words, matching the single process
+    on the global batch of 4 (the step-2 amaxes follow parameters that differ from the single
+    process only by gradient summation order); the global-scaling switches are off again after
+    the step, and a plain fp8 module in the same process rolls its own sites."""
+    import facevae_amd as fv
+    from facevae_amd import distributed as D
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fp8_steps_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in ps:
+        p.start()
+    out = sorted([torch.load(io.BytesIO(q.get(timeout=400)), weights_only=True) for _ in ps], key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in out:
+        assert isinstance(r[1], dict), f"rank {r[0]} failed: {r[1]}"
+    r0, r1 = out[0][1], out[1][1]
+    for mode in ("eager", "graph"):
+        l0, s0, off0, init0 = r0[mode]
+        l1, s1, off1, _ = r1[mode]
+        assert off0 and off1, mode
+        assert len(s0) >= 28 and sorted(s0) == sorted(s1), (mode, len(s0))
+        for k in s0:
+            assert torch.equal(s0[k], s1[k]), (mode, k)
+            assert int(s0[k][17]) == 2, (mode, k, s0[k][17])        # one global roll per step
+    ge, gg = r0["eager"][1], r0["graph"][1]
+    for k in ge:                                                   # graph replay ~ eager step
+        a, b = ge[k][:16].view(torch.float32).double(), gg[k][:16].view(torch.float32).double()
+        assert ((a - b).abs() <= 1e-3 * b.abs()).all() and ge[k][17] == gg[k][17], k
+
+    # single process, global batch of 4, same initial weights: two eager fp8 steps
+    cfg = fv.FaceVAEConfig(H=256)
+    x, eps = _inputs(cfg.H, cfg.latent, cfg.latent_hw)
+    D.install(None, syncbn=True)
+    assert fv.ops.FP8_GLOBAL is None
+    m = fv.FaceVAE(cfg)
+    m.load_state_dict(r0["eager"][3])
+    m = m.cuda().train().set_compute_dtype(torch.float8_e4m3fn)
+    opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
+    xc, ec = x.cuda(), eps.cuda()
+    for _ in range(2):
+        opt.zero_grad(set_to_none=True)
+        y, mu, ls = m(xc, ec)
+        (cfg.w_R * fv.ReconLoss()((xc, y)) + cfg.w_K * fv.KLDivergenceLoss()((mu, ls))).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    s1p = _site_words(m)
+    assert sorted(s1p) == sorted(ge)
+    worst = {0: 0.0, 1: 0.0}
+    for k in ge:
+        assert int(s1p[k][17]) == int(ge[k][17]), k                # this process rolled its own sites
+        a = ge[k][:2].view(torch.float32).double()
+        b = s1p[k][:2].view(torch.float32).double()
+        # a rank's loss is the mean over its 2 images, so its output gradients are 2x the
+        # 4-image process's (the averaged weight gradients are equal): the "dy" amaxes are 2x
+        if k.endswith("/dy"):
+            b = 2 * b
+        for j in (0, 1):
+            worst[j] = max(worst[j], abs(a[j] - b[j]).item() / max(abs(b[j]).item(), 1e-30))
+        if k.endswith("/x"):
+            assert torch.equal(a[0], b[0]), k                      # step 1: the same forward, bit for bit
+    print(f"\n[fp8 sites, 2 ranks x 2 vs 1 process x 4] amax history worst rel: step 1 {worst[0]:.2e}, "
+          f"step 2 {worst[1]:.2e}")
+    assert worst[0] < 1e-2 and worst[1] < 5e-2
