@@ -292,14 +292,18 @@ class _Staging:
     layers, Adam tensors).  Eager: a fresh pinned buffer per copy, copied with torch's
     non_blocking copy (torch's pinned allocator keeps it until the copy has run).  Under HIP-
     graph capture (graph.StepGraph): persistent pinned buffers, one per copy in issue order,
-    reserved from the sizes recorded during the last eager step before the capture; the
-    captured memcpy nodes re-read them on every replay, so they live as long as the graph."""
+    reserved from the sizes recorded during the last eager step before the capture, with their
+    device tables allocated before the capture and written once when it ends (end()); both live
+    as long as the graph."""
 
     def __init__(self):
         self.mode = "eager"          # "eager" | "record" | "capture"
         self.sizes = []
         self.bufs = []
         self.i = 0
+        self.devs = []               # the captured tables' device buffers (allocated before the capture)
+        self.deferred = []           # (device table, pinned buffer, bytes) filled at capture end
+        self.keep = []               # the captured tables, alive as long as the graph
 
     def begin_record(self):
         self.mode, self.sizes = "record", []
@@ -308,10 +312,25 @@ class _Staging:
         if self.mode != "record":
             raise RuntimeError("staging: capture without a recorded eager step")
         self.bufs = [torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True) for n in self.sizes]
+        # the device tables are allocated HERE, before the capture, from the ordinary pool: a
+        # table allocated inside the capture may reuse the block of a tensor the step freed
+        # earlier, which every replay overwrites before the table's reader runs (the copy node
+        # of the old scheme re-wrote the table after it; a copy done once at capture end does not)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.devs = [torch.empty(max(n, 1), dtype=torch.uint8, device=dev) for n in self.sizes]
         self.mode, self.i = "capture", 0
         return self.bufs
 
     def end(self):
+        """End of a capture: the tables are constant for every replay (their bytes were frozen at
+        capture), so they are copied into their pre-allocated device buffers ONCE here instead of
+        by a memcpy node in every replay (3 dependent ~5 us copy kernels per replayed step)."""
+        if self.mode == "capture" and self.deferred:
+            for dev, hb, n in self.deferred:
+                dev.copy_(hb[:n])
+            torch.cuda.synchronize()
+            self.keep = self.deferred
+        self.deferred = []
         self.mode = "eager"
 
 
@@ -325,11 +344,15 @@ def h2d_table(data: bytes, device):
         if staging.i >= len(staging.bufs) or staging.bufs[staging.i].numel() < n:
             raise RuntimeError("staging: the captured step issues other table copies than the recorded one")
         hb = staging.bufs[staging.i]
+        dev = staging.devs[staging.i]
         staging.i += 1
+        want = torch.device(device)
+        if want.type != "cuda" or (want.index is not None and want.index != dev.device.index):
+            raise RuntimeError("staging: the captured table's device differs from the current device")
         hb[:n].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
-        dev = torch.empty(n, dtype=torch.uint8, device=device)
-        call("fv_copy_h2d_async", dev.data_ptr(), hb.data_ptr(), n, stream())
-        return dev, hb
+        # filled once by end(); referenced as long as the graph (staging.keep -> StepGraph)
+        staging.deferred.append((dev, hb, n))
+        return dev[:n], hb
     if staging.mode == "record":
         staging.sizes.append(n)
     hb = torch.frombuffer(bytearray(data), dtype=torch.uint8).pin_memory()

@@ -1878,11 +1878,17 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
         *reinterpret_cast<uint4*>(yp + (2 * q + (g & 1)) * 16 + (g >> 1) * 8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
       }
     }
-    // the next tile's halo was issued a whole tile earlier; younger than it are the previous
-    // tile's >= 4 stores, this tile's DMA (if any) and this tile's >= 4 stores, so vmcnt(8)
-    // has it landed (in-order counting); the barrier publishes it to all waves and releases
-    // this tile's buffer (raw barrier: __syncthreads() would also drain the stores)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // the next tile's halo was issued a whole tile earlier; younger than it are exactly the
+    // previous tile's 4 stores, this tile's BN record store (waves 0-1), its halo DMA pieces
+    // (2 / 1 per wave, when the tile two ahead exists) and its 4 stores: waiting for that count
+    // leaves all of them in flight (vmcnt(8) made every tile wait for half of the previous
+    // tile's stores); the barrier publishes it to all waves and releases this tile's buffer
+    // (raw barrier: __syncthreads() would also drain the stores)
+    {
+      const int dpieces = ahead < ntiles ? (wave + 8 < C74_HQ ? 2 : 1) : 0;
+      const int recst = (a.stats && it > 0 && wave < 2) ? 1 : 0;
+      wait_vm_dyn(8 + dpieces + recst);
+    }
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -2319,6 +2325,168 @@ conv3up_band_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
 }
 
 // ----------------------------------------------------------------------------------------
+// 1x1 conv as a pixel stream: AFE.mid_conv 256 -> 512 (models.py:934) and Generator.mid_conv
+// 256 -> 256 (models.py:1096) forward, and their data gradients (the same GEMM with the
+// transposed weights, K = Cout).  out[p][co] = bias[co] + sum_k x[p][k] W[co][k]: per output
+// pixel 2 K bytes in and 2 Cout bytes out for 2 K Cout FLOP, so at K <= 512 the launch is
+// HBM-bound (conv_fwd_v2's 256 x 256 tile, one block per CU, alternated load -> MFMA -> store
+// phases across the whole chip: 3.4 TB/s).
+// A block owns 256 output channels; wave w keeps rows [32 w, 32 w + 32) of W for the whole
+// launch as MFMA A fragments in registers (K / 4 VGPRs) and the block walks pixel tiles of
+// BP = 16384 / K pixels (32 KB of x) persistently.  The x tiles land by LDS-DMA in a 4-slot
+// ring, 3 tiles in flight while one is computed (with 2 slots of 64 KB only one tile was in
+// flight per CU: 3.3 TB/s); the staged epilogue's stores of tile t drain under the DMA of
+// tile t + 4, issued into the slot tile t just freed.  LDS rows are K * 2 bytes with the 16-B chunks XOR-swizzled by (pixel & 15)
+// through the per-lane DMA source, so a fragment read (16 pixels at one k) is conflict-free.
+// Co groups of one pixel stream are neighbouring blocks of one XCD (x read once into its L2).
+// Requires P % BP == 0, Cout % 256 == 0, dense NHWC (ldy = Cout), no residual / statistics.
+// ----------------------------------------------------------------------------------------
+template <int K, int BPX>
+__global__ void __launch_bounds__(512, 1)
+conv1x1_stream(ConvArgs a, unsigned x_bytes) {
+  constexpr int ROWB = K * 2, BP = BPX, RM = BP / 16, RN = 2, NKS = K / 32;
+  constexpr int SLOT = BP * ROWB;                   // 32 / 64 KB
+  constexpr int NSL = 131072 / SLOT;                // ring slots in 128 KB: NSL - 1 tiles in flight
+  constexpr int PPW = SLOT / 1024 / 8;              // DMA pieces per wave per tile
+  constexpr int RPP = 1024 / ROWB;                  // pixel rows per piece (2 / 1)
+  constexpr int NST = RM;                           // 16-B output stores per lane per tile
+  static_assert(K == 256 || K == 512, "conv1x1_stream: K of 256 or 512");
+  static_assert(NSL >= 2 && NSL <= 4 && (NSL - 1) * PPW + NSL * NST <= 63, "conv1x1_stream: ring / vmcnt");
+  __shared__ __attribute__((aligned(1024))) char smem[NSL * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lh = lane >> 4;
+  const int ncg = a.Cout / 256;
+  const int bid = blockIdx.x, G = gridDim.x;
+  const int cg = (bid / 8) % ncg;                   // the co groups of a stream share an XCD
+  const int stream = bid % 8 + 8 * ((bid / 8) / ncg), nstream = G / ncg;
+  const int co0 = cg * 256;
+  const int ntp = a.P / BP;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.x), 0, (int)x_bytes, 0x00020000);
+  const unsigned sbase = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_ptr_t)smem);
+  // lane part of a DMA piece: byte l * 16 of the piece = (row l / (64 / RPP), physical chunk);
+  // the source is logical chunk (physical ^ (pixel & 15)); the piece's pixel offset & 15 is
+  // RPP * (wave + 8 i) & 15: constant over i for RPP = 2, alternating for RPP = 1
+  unsigned voff[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int rip = lane / (64 / RPP), pc = lane % (64 / RPP);
+    const int prow = (RPP * (wave + 8 * par) + rip) & 15;
+    voff[par] = (unsigned)((rip * K + ((pc ^ prow) << 3)) * 2);
+  }
+  // tile t into `slot`; t >= ntp issues the same pieces out of range (zero fill, no branch:
+  // a branch here made the compiler keep live arrays in scratch across it)
+  auto issue = [&](int t, int slot) {
+    const unsigned base = sbase + slot * SLOT;
+    const bool ok = t < ntp;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int q = wave + 8 * i;
+      dma16s(xr, base + q * 1024, ok ? voff[RPP == 2 ? 0 : (i & 1)] : 0x80000000u,
+             ok ? (unsigned)(((t * BP + q * RPP) * K) * 2) : 0u);
+    }
+  };
+  // this wave's weights: rows co0 + 32 wave + 16 n + lr, k = 32 s + 8 lh .. + 7
+  Frag<bf16> wa[NKS][RN];
+  {
+    const bf16* w = reinterpret_cast<const bf16*>(a.w);
+#pragma unroll
+    for (int ss = 0; ss < NKS; ++ss)
+#pragma unroll
+      for (int n = 0; n < RN; ++n)
+        wa[ss][n].v = *reinterpret_cast<const bf16x8*>(w + (long)(co0 + 32 * wave + 16 * n + lr) * a.Kpad + 32 * ss + 8 * lh);
+  }
+  // this lane's biases (channels co0 + 32 wave + 16 n + 4 lh + i), for every tile
+  float bv[RN][4];
+#pragma unroll
+  for (int n = 0; n < RN; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[n][i] = a.bias ? a.bias[co0 + 32 * wave + 16 * n + 4 * lh + i] : 0.f;
+  // fragment read of k-step s, m-tile m: pixel m * 16 + lr, physical chunk (4 s + lh) ^ lr
+  unsigned foff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) foff[q] = (unsigned)(lr * ROWB + (((4 * q + lh) ^ lr) << 4));
+  auto pk = [](float lo, float hi) {
+    const bf16 t2[2] = {(bf16)lo, (bf16)hi};
+    return *reinterpret_cast<const unsigned*>(t2);
+  };
+  bf16* const yw = reinterpret_cast<bf16*>(a.y) + co0 + 32 * wave + (lh & 1) * 16 + (lh >> 1) * 8;
+
+  int t = stream;
+  if (t >= ntp) return;
+#pragma unroll
+  for (int j = 0; j < NSL; ++j) issue(t + j * nstream, j);
+  for (int i = 0; t < ntp; t += nstream, ++i) {
+    const int slot = i % NSL;
+    // tile t landed: every wave waits for its own pieces, the barrier publishes them.  Issued
+    // after tile t's pieces, in order: the prologue's later tiles, then per finished tile u the
+    // pieces of tile u + NSL (zero-fill past the last tile) and u's stores -- exactly
+    // (NSL - 1) x PPW pieces and min(i, NSL) x NST stores
+    const int ni = i < NSL ? i : NSL;
+    if (ni == 0) wait_vm<(NSL - 1) * PPW>();
+    else if (ni == 1) wait_vm<(NSL - 1) * PPW + NST>();
+    else if (ni == 2) wait_vm<(NSL - 1) * PPW + 2 * NST>();
+    else if (ni == 3) wait_vm<(NSL - 1) * PPW + 3 * NST>();
+    else wait_vm<(NSL - 1) * PPW + 4 * NST>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    f32x4 acc[RN][RM];
+#pragma unroll
+    for (int n = 0; n < RN; ++n)
+#pragma unroll
+      for (int m = 0; m < RM; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* xs = smem + slot * SLOT;
+    // two fragment sets: k-step ss + 1's reads under k-step ss's MFMAs; the scheduling
+    // barriers keep the compiler from hoisting every k-step's reads (all of them in flight
+    // spilled ~54 registers beside the resident weights)
+    Frag<bf16> f0[RM], f1[RM];
+    auto rd = [&](Frag<bf16> (&f)[RM], int ss) {
+#pragma unroll
+      for (int m = 0; m < RM; ++m) f[m].lds(xs + foff[ss & 3] + (ss >> 2) * 256 + m * 16 * ROWB);
+    };
+    auto mm = [&](const Frag<bf16> (&f)[RM], int ss) {
+#pragma unroll
+      for (int m = 0; m < RM; ++m)
+#pragma unroll
+        for (int n = 0; n < RN; ++n) acc[n][m] = mma(wa[ss][n], f[m], acc[n][m]);
+    };
+    rd(f0, 0);
+#pragma unroll
+    for (int ss = 0; ss < NKS; ss += 2) {
+      rd(f1, ss + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(f0, ss);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ss + 2 < NKS) rd(f0, ss + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(f1, ss + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // every wave's fragment reads of the slot are done: refill it with tile t + NSL at once,
+    // then the stores of tile t straight from the accumulators -- + bias, bf16, the two
+    // 16-channel n-tiles paired by v_permlane16_swap so lane (lr, lh) holds 8 contiguous
+    // channels ((lh & 1) * 16 + (lh >> 1) * 8 of the wave's 32) of pixel m * 16 + lr: one
+    // 16-B store per m-tile (4 lanes = one 64-B channel run of a pixel)
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(t + NSL * nstream, slot);
+#pragma unroll
+    for (int m = 0; m < RM; ++m) {
+      const f32x4 va = acc[0][m], vb = acc[1][m];
+      const auto s0 = __builtin_amdgcn_permlane16_swap(pk(va[0] + bv[0][0], va[1] + bv[0][1]),
+                                                       pk(vb[0] + bv[1][0], vb[1] + bv[1][1]), false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(pk(va[2] + bv[0][2], va[3] + bv[0][3]),
+                                                       pk(vb[2] + bv[1][2], vb[3] + bv[1][3]), false, false);
+      *reinterpret_cast<uint4*>(yw + (long)(t * BP + m * 16 + lr) * a.ldy) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+  wait_vm<0>();      // the zero-fill pieces of the last tiles land before the workgroup's LDS is freed
+}
+
+// ----------------------------------------------------------------------------------------
 // 7x7 conv with a 64-channel input and <= 4 output channels (Generator.out_conv 64 -> 3,
 // models.py:1099 + sigmoid 1110), "column taps in N": for every input pixel w' of a row the
 // block computes D[h][w'][(co, s)] = sum_{r, ci} x[h + r - 3][w'][ci] * W[co][ci][r][s]
@@ -2395,10 +2563,24 @@ conv7_n3_fwd2(ConvArgs a, unsigned x_bytes, int band) {
   const int pn[5] = {half ? 1 : 0, half ? 0 : 1, half ? 1 : 0, half ? 0 : 1, half ? 1 : 0};
   const int HWo = a.H * a.W;
   const int ngroups = band / C7_TR;
+  float bias4[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) bias4[c] = (a.bias && c < a.Cout) ? a.bias[c] : 0.f;
+  // the epilogue's store instructions per group of this wave (lane 0's two record stores per
+  // output too when statistics are on): the wait at the next group's top leaves them in flight
+  // (it was vmcnt(0): every group waited for the previous group's output stores)
+  const int nout = C7_TR * 64 * a.Cout;
+  const int nst = (nout > wave * 64 ? (nout - wave * 64 + 511) / 512 : 0) * (a.stats ? 3 : 1);
 
   for (int j = 0; j < ngroups; ++j) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();                           // group j's rows landed; group j-1's D reads done
+    // group j's rows (issued at group j - 1's top; only this wave's stores of group j - 1 are
+    // younger) landed for this wave; the barrier publishes every wave's and retires group
+    // j - 1's D reads
+    if (j == 0) wait_vm<0>();
+    else wait_vm_dyn(nst);
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     if (j + 1 < ngroups) issue_rows(4 * j + 10, 4);
     f32x4 acc[5];
 #pragma unroll
@@ -2440,11 +2622,13 @@ conv7_n3_fwd2(ConvArgs a, unsigned x_bytes, int band) {
         }
       }
     }
-    __syncthreads();
+    wait_lgkm0();                              // D written (LDS only: the row DMA stays in flight)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     const int h0 = hb + 4 * j;
-    for (int o = tid; o < C7_TR * 64 * a.Cout; o += 512) {
+    for (int o = tid; o < nout; o += 512) {
       const int co = o / (C7_TR * 64), rr = (o / 64) % C7_TR, w = o % 64;
-      float v = a.bias ? a.bias[co] : 0.f;
+      float v = co == 0 ? bias4[0] : co == 1 ? bias4[1] : co == 2 ? bias4[2] : bias4[3];
 #pragma unroll
       for (int s7 = 0; s7 < 7; ++s7) v += Dl[(rr * 70 + w + s7) * C7B_DLD + co * 7 + s7];
       if (a.stats) {
@@ -3742,9 +3926,15 @@ struct HaloWgArgs {
   unsigned xbytes, dybytes;
 };
 
-template <int KS, int CIN, int NT, int TR>
+// PK (AFE.in_conv, <= 4 valid input channels of the 8 staged per pixel): k packed as
+// k = r * 32 + s * 4 + ci (s = 7 a padding column, ci = 3 the zero channel), the weight layout
+// conv7c4_fwd's forward reads -- 14 m-tiles instead of 25 (49 taps x 8 padded channels): a
+// lane's 4 k are ci 0..3 of one tap = the first 8 B of the halo pixel at that tap's shift.
+// The slab rows are these k (KW = 224); wgrad_reduce_kernel maps them back (KSL = 8).
+template <int KS, int CIN, int NT, int TR, bool PK = false>
 __global__ void __launch_bounds__(512, 2)
 conv_halo_wgrad(HaloWgArgs a) {
+  static_assert(!PK || (CIN == 8 && KS == 7), "packed 7x7 weight gradient: 8 staged channels");
   constexpr int PAD = KS / 2, TW = 64;
   constexpr int HR = TR + KS - 1, HW = TW + KS - 1;
   constexpr int CPP = CIN / 8;
@@ -3754,7 +3944,7 @@ conv_halo_wgrad(HaloWgArgs a) {
   constexpr int DCH = TR * TW * LDD / 8;
   constexpr int DQ = (DCH + 63) / 64;
   constexpr int HB = HQ * 1024, DB = DQ * 1024, BUF = HB + DB;
-  constexpr int KT = KS * KS * CIN;                 // valid k
+  constexpr int KT = PK ? KS * 32 : KS * KS * CIN;  // valid k
   constexpr int MTT = (KT + 15) / 16;               // m-tiles (16 k rows)
   // every wave owns m-tiles {wave, wave + 8, ...} and ALL NT n-tiles: the A fragment of an
   // m-tile (two transposed 8-B halo reads) feeds NT MFMAs.  (One n-tile per wave, as before,
@@ -3807,11 +3997,18 @@ conv_halo_wgrad(HaloWgArgs a) {
   for (int j = 0; j < RMW; ++j) {
     const int mt = mw + j * 8;
     const int k = mt * 16 + 4 * pp;                 // first of this lane's 4 k (same tap, same chunk)
-    const int tap = k / CIN, ci = k - (k / CIN) * CIN;
-    const int r = tap / KS, s = tap - (tap / KS) * KS;
     aok[j] = mt < MTT;                              // wave-uniform (transposed reads need EXEC = all)
-    aoff[j] = k < KT ? r * HW + s : 0;              // k >= K rows: finite junk, never stored
-    akx[j] = k < KT ? ci : 0;
+    if constexpr (PK) {
+      // s = 7 reads one column past the tap window (the next halo row's first pixel, or the
+      // dy image after the last row): finite junk in rows the reduce never maps
+      aoff[j] = k < KT ? (k >> 5) * HW + ((k >> 2) & 7) : 0;
+      akx[j] = 0;
+    } else {
+      const int tap = k / CIN, ci = k - (k / CIN) * CIN;
+      const int r = tap / KS, s = tap - (tap / KS) * KS;
+      aoff[j] = k < KT ? r * HW + s : 0;            // k >= K rows: finite junk, never stored
+      akx[j] = k < KT ? ci : 0;
+    }
   }
   f32x4 acc[RMW][NT];
 #pragma unroll
@@ -4241,9 +4438,11 @@ __global__ void subpix_fold_kernel(const float* __restrict__ slab, const float* 
 // sum of the per-split slabs -> dW in the reference layout [co][ci][r][s] (+ db).  Block =
 // 64 consecutive outputs x 4 split lanes (4 independent partial sums each), so that large
 // split counts do not serialise on load latency; blocks >= nb_main reduce the bias slab.
+// KSL: taps per row in the slab's k layout (KS, or 8 for the packed 7x7 rows of conv_halo_wgrad
+// PK, whose s = 7 column is padding)
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
                                     float* dw, float* db, int nsplit, int CW, int KW, int K,
-                                    int cout, int cin_valid, int lgCin, int KS, int nb_main) {
+                                    int cout, int cin_valid, int lgCin, int KS, int nb_main, int KSL) {
   const int sg = threadIdx.x >> 6, l = threadIdx.x & 63;
   __shared__ float red[4][64];
   float g = 0.f;
@@ -4255,8 +4454,8 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float*
     const long e = (long)blockIdx.x * 64 + l;
     const int co = (int)(e / K), k = (int)(e - (e / K) * K);
     const int tap = k >> lgCin, c = k & ((1 << lgCin) - 1);
-    valid = e < (long)cout * K && c < cin_valid;
-    const int r = tap / KS, sx = tap - (tap / KS) * KS;
+    const int r = tap / KSL, sx = tap - (tap / KSL) * KSL;
+    valid = e < (long)cout * K && c < cin_valid && sx < KS;
     dst = (((long)co * cin_valid + c) * KS + r) * KS + sx;
     p = slab + (long)co * KW + k;
     stride = (long)CW * KW;
@@ -4629,6 +4828,13 @@ int check_desc(const fv_conv_desc* d) {
 int kpad_of(int ks, int cin) { return fv_cdiv((long)ks * ks * cin, BK) * BK; }
 
 // 7x7 halo wgrad: in_conv (cin 8 -> 64, dy stride 64) or out_conv (cin 64 -> cout <= 8, dy stride 8)
+// the in_conv weight gradient in the packed k layout (conv_halo_wgrad PK); FV_WG7_PACK=0 keeps
+// the 8-channel padded layout (A/B).  Read per call.
+static bool halo_wg_pk(const fv_conv_desc* d) {
+  const char* e = getenv("FV_WG7_PACK");
+  if (e && e[0] == '0') return false;
+  return d->ksize == 7 && d->cin == 8 && d->cin_valid <= 4;
+}
 static int halo_wg_tr(const fv_conv_desc* d) {
   if (d->ksize != 7 || d->upsample || d->pro_act || d->w % 64) return 0;
   int tr = 0;
@@ -4663,6 +4869,14 @@ constexpr Wg2Cfg kWg2Cfg[] = {
 constexpr int kNumWg2Cfg = sizeof(kWg2Cfg) / sizeof(kWg2Cfg[0]);
 int wg2_cfg(const fv_conv_desc* d, int K) {
   const int bc = d->cout > 128 ? 256 : d->cout > 64 ? 128 : d->cout > 16 ? 64 : 16;
+  // FV_WG1_CFG=c: tile config c (0..5) for the 1x1 weight gradients (A/B; read per call)
+  if (d->ksize == 1) {
+    const char* e = getenv("FV_WG1_CFG");
+    if (e && e[0] >= '0' && e[0] <= '5') {
+      const int c = e[0] - '0';
+      if (d->cout % kWg2Cfg[c].bc == 0 && K % kWg2Cfg[c].bkt == 0) return c;
+    }
+  }
   // defaults from the FaceVAE-shape tile sweep (r1): 384 x 64 tiles for the
   // 64-channel layers (K = 1152 splits exactly), 32-pixel stages 3-deep when K is not a
   // multiple of 256 at 256 channels
@@ -4733,7 +4947,7 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   if (p.v2 && htr) {
     const int nt = d->cin == 8 ? 4 : 1;
     p.v2 = 2;
-    p.bkt = fv_cdiv(K, 16) * 16;
+    p.bkt = halo_wg_pk(d) ? 7 * 32 : fv_cdiv(K, 16) * 16;
     p.bc = nt * 16;
     p.px = htr * 64;
     p.ntk = 1;
@@ -5197,6 +5411,18 @@ static void launch_h3(int ntiles, hipStream_t s, const ConvArgs& a, unsigned xb)
 }
 }  // extern "C++"
 
+// 1x1 convs with K = 256 / 512 input channels and whole 256-channel output groups (the mid
+// convs and their data gradients) on the pixel-stream kernel conv1x1_stream; FV_C1S=0 keeps
+// conv_fwd_v2 (A/B).  Read per call.
+static bool use_c1s(const fv_conv_desc* d) {
+  const char* e = getenv("FV_C1S");
+  if (e && e[0] == '0') return false;
+  if (!use_v2(d) || d->ksize != 1 || d->upsample || d->pro_act) return false;
+  if ((d->cin != 256 && d->cin != 512) || d->cout % 256 || d->ldy != d->cout) return false;
+  const long P = (long)d->n * d->h * d->w;
+  return P % (32768 / d->cin) == 0 && P * d->cout * 2 < (1L << 31);   // (both tile sizes)
+}
+
 static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
                     const float* psc, const float* psh, const void* res, void* y, float* stats,
                     hipStream_t s, const fv_store_reduce* sr = nullptr) {
@@ -5388,6 +5614,25 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
       hipLaunchKernelGGL((conv3_halo_fwd2<1, 4, 4, 4, 3>), dim3(nblk), dim3(256), 0, s, a, xb);
     }
     return fv_check_launch("conv2d_fwd_halo3");
+  }
+  if (use_c1s(d) && !res && !stats && !a.spm) {
+    if ((st = wext(d->cout, a.Kpad, "c1s"))) return st;
+    FV_REQUIRE(a.Kpad == d->cin, "1x1 stream conv: K %d != Kpad %d", d->cin, a.Kpad);
+    const int ncg = d->cout / 256;
+    const int grid = std::max(8 * ncg, cu_count() / (8 * ncg) * (8 * ncg));
+    const unsigned xb = (unsigned)((long)a.P * d->cin * 2);
+    // FV_C1S_BP=64 / 128: pixels per tile for K = 256 (halved for K = 512): 4 slots of 32 KB
+    // or 2 of 64 KB (A/B; read per call)
+    const char* e = getenv("FV_C1S_BP");
+    const bool big = e && atoi(e) == 128;
+    if (d->cin == 256) {
+      if (big) hipLaunchKernelGGL((conv1x1_stream<256, 128>), dim3(grid), dim3(512), 0, s, a, xb);
+      else hipLaunchKernelGGL((conv1x1_stream<256, 64>), dim3(grid), dim3(512), 0, s, a, xb);
+    } else {
+      if (big) hipLaunchKernelGGL((conv1x1_stream<512, 64>), dim3(grid), dim3(512), 0, s, a, xb);
+      else hipLaunchKernelGGL((conv1x1_stream<512, 32>), dim3(grid), dim3(512), 0, s, a, xb);
+    }
+    return fv_check_launch("conv2d_fwd_c1s");
   }
   if (use_v2(d)) {
     FV_REQUIRE(!(res && stats), "conv v2: residual and BN statistics in one call are not supported");
@@ -5622,7 +5867,10 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.KW = t.KW; a.CW = t.CW; a.ntiles = t.nsteps; a.cout = d->cout;
     a.xbytes = (unsigned)(P * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
-    if (d->cin == 8)
+    FV_REQUIRE(t.KW == (halo_wg_pk(d) ? 224 : fv_cdiv(a.K, 16) * 16), "7x7 halo wgrad: slab row length");
+    if (d->cin == 8 && halo_wg_pk(d))
+      hipLaunchKernelGGL((conv_halo_wgrad<7, 8, 4, 4, true>), dim3(t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    else if (d->cin == 8)
       hipLaunchKernelGGL((conv_halo_wgrad<7, 8, 4, 4>), dim3(t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
     else
       hipLaunchKernelGGL((conv_halo_wgrad<7, 64, 1, 2>), dim3(t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
@@ -5738,13 +5986,15 @@ int fv_conv2d_wgrad_reduce(const fv_conv_desc* d, const float* slab, const float
                        bias_slab, dw_param, db, t.nsplit, t.CW, t.KW, d->cout, d->cin_valid, fv_ilog2(d->cin), nb_main);
     return fv_check_launch("wgrad_reduce_subpix");
   }
-  const int K = d->ksize * d->ksize * d->cin;
+  // (the packed 7x7 slab rows: k = r * 32 + s * 4 + ci, i.e. 4 "channels" x 8 "taps" per row)
+  const bool pk = t.v2 == 2 && halo_wg_pk(d);
+  const int K = pk ? 7 * 32 : d->ksize * d->ksize * d->cin;
   const long tot = (long)d->cout * K;
   const int nb_main = fv_cdiv(tot, 64);
   const int nb_bias = db ? fv_cdiv(d->cout, 64) : 0;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb_main + nb_bias), dim3(256), 0, (hipStream_t)stream, slab,
-                     bias_slab, dw_param, db, t.nsplit, t.CW, t.KW, K, d->cout, d->cin_valid, fv_ilog2(d->cin),
-                     d->ksize, nb_main);
+                     bias_slab, dw_param, db, t.nsplit, t.CW, t.KW, K, d->cout, d->cin_valid, pk ? 2 : fv_ilog2(d->cin),
+                     d->ksize, nb_main, pk ? 8 : d->ksize);
   return fv_check_launch("wgrad_reduce");
 }
 

@@ -9,8 +9,9 @@ hipGraphLaunch.  Everything the step does on the host is frozen into the graph a
 
 * kernel arguments (device pointers of weights, activations and workspaces from the graph
   pool, shapes) -- fixed shapes, fixed parameter storage;
-* descriptor tables (spectral-norm layers, Adam tensors) -- copied from pinned buffers that
-  `_lib.staging` reserves for the capture from the sizes of the last eager step;
+* descriptor tables (spectral-norm layers, Adam tensors) -- written once into graph-pool
+  tensors at the end of the capture (`_lib.staging`, sized from the last eager step), not
+  re-copied by every replay;
 * the Adam step count -- moved to a device counter (`Adam.prepare_graph`,
   fv_adam_step_dev), so bias corrections advance on every replay.
 
@@ -157,6 +158,7 @@ class StepGraph:
                     self.out = self.step_fn()
         finally:
             L.staging.end()
+        self._tables = L.staging.keep           # the captured descriptor tables (filled once)
         if L.staging.i != len(self._bufs):
             raise RuntimeError("StepGraph: the captured step issued fewer table copies than the recorded one")
         return self

@@ -131,7 +131,7 @@ def conv3d_backward(cs: Conv3dState, x, dy, need_dx=True):
     dw = torch.empty_like(cs.w)
     db = torch.empty(d.cout, dtype=F32, device=dev)
     nws = query("fv_conv3d_wgrad_ws_bytes", ctypes.byref(d))
-    ws = torch.empty(max(nws, 4) // 4, dtype=F32, device=dev)
+    ws = ops._empty(max(nws, 4) // 4, F32, dev)
     call("fv_conv3d_bwd_weight", ctypes.byref(d), ptr(x), ptr(dy), ptr(dw), ptr(db), ptr(ws) if nws else None,
          stream())
     dx = None

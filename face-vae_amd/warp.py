@@ -87,7 +87,7 @@ class GridSample3dFn(torch.autograd.Function):
             gd = F32 if ctx.in_dtype == F32 else ctx.dtype
             gsrc = go if gd == ctx.dtype else go.to(gd)
             nws = L.query("fv_grid_sample3d_bwd_input_ws_bytes", B, Di, Hi, Wi, Do, Ho, Wo, ctx.group)
-            ws = torch.empty(nws, dtype=torch.uint8, device=xb.device)
+            ws = ops._empty(nws, torch.uint8, xb.device)
             gin = torch.empty((Bi, C, Di, Hi, Wi), dtype=gd, device=xb.device, memory_format=CL3)
             call("fv_grid_sample3d_bwd_input", L.dtype_code(gd), ptr(g32), ptr(gsrc), B, Di, Hi, Wi, Do, Ho, Wo,
                  C, ctx.group, ptr(gin), ptr(ws), stream())

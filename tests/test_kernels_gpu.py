@@ -522,3 +522,81 @@ def test_up_wgrad_splits(spb, monkeypatch):
     assert L.query("fv_conv2d_wgrad_nsplit", ctypes.byref(d)) == (6 + spb - 1) // spb
     assert rel(dw, wr.grad) < TOL[torch.bfloat16] * 1.5
     assert rel(db, br.grad) < TOL[torch.bfloat16] * 1.5
+
+
+# 1x1 convs on the pixel-stream kernel (conv.hip conv1x1_stream): the mid convs' forward and
+# data-gradient shapes -- one tile per stream, several tiles per stream (the t + 2 DMA under the
+# stores), 2 co groups -- bit-identical to conv_fwd_v2's 256 x 256 tile (same k order, same
+# epilogue: FV_C1S=0) and within bf16 tolerance of the torch fp32 conv
+C1S_CASES = [
+    # cin, cout, N, H, W
+    (256, 512, 2, 16, 64),      # 16 pixel tiles, 2 co groups
+    (256, 256, 16, 64, 64),     # 512 tiles: 2 per stream
+    (512, 256, 8, 64, 64),      # K = 512 (AFE.mid_conv's data gradient shape): 64-pixel tiles
+    (256, 512, 24, 64, 64),     # 768 tiles, 2 co groups: 6 per stream
+]
+
+
+@pytest.mark.parametrize("bp", ["64", "128"])
+@pytest.mark.parametrize("case", C1S_CASES)
+def test_conv1x1_stream(case, bp, monkeypatch):
+    cin, cout, N, H, W = case
+    monkeypatch.setenv("FV_C1S_BP", bp)         # 4 slots of 32 KB / 2 slots of 64 KB
+    g = gen(300 + cin + N)
+    x = torch.randn(N, cin, H, W, generator=g)
+    w = torch.randn(cout, cin, 1, 1, generator=g) / cin ** 0.5
+    b = torch.randn(cout, generator=g)
+    d, xb, wk, wt, shp = conv_setup(x, w, 1, torch.bfloat16, need_wt=True)
+    bc = b.cuda()
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FV_C1S", mode)
+        y = torch.empty(shp, dtype=torch.bfloat16, device="cuda", memory_format=CL)
+        L.call("fv_conv2d_fwd", ctypes.byref(d), xb.data_ptr(), wk.data_ptr(), bc.data_ptr(), None, None, None,
+               y.data_ptr(), None, L.stream())
+        gy = torch.randn(shp, generator=gen(7)).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+        dx = torch.empty((N, cin, H, W), dtype=torch.bfloat16, device="cuda", memory_format=CL)
+        L.call("fv_conv2d_bwd_data", ctypes.byref(d), gy.data_ptr(), cout, wt.data_ptr(), dx.data_ptr(), L.stream())
+        torch.cuda.synchronize()
+        outs[mode] = (y, dx, gy)
+    (y1, dx1, gy), (y0, dx0, _) = outs["1"], outs["0"]
+    assert torch.equal(y1, y0) and torch.equal(dx1, dx0)
+    xq = xb.float().cpu()
+    wq = w.cuda().to(torch.bfloat16).float().cpu()
+    ref = F.conv2d(xq, wq, b)
+    assert rel(y1.float().cpu(), ref) < TOL[torch.bfloat16]
+    dref = F.conv_transpose2d(gy.float().cpu(), wq)
+    assert rel(dx1.float().cpu(), dref) < TOL[torch.bfloat16]
+
+
+@pytest.mark.parametrize("shape", [(2, 16, 64), (4, 32, 128)])
+def test_in_conv_wgrad_packed_layout(shape, monkeypatch):
+    """AFE.in_conv's weight gradient (7x7, 3 -> 64) with k packed as (row, 4 taps x 4 channels)
+    -- 14 m-tiles instead of 25 -- is bit-identical to the 8-channel padded layout (the same
+    pixel sums per output element; FV_WG7_PACK=0) and matches torch fp32 at bf16 tolerance."""
+    N, H, W = shape
+    g = gen(41 + H)
+    x = torch.rand(N, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) / 147 ** 0.5
+    gy = torch.randn(N, 64, H, W, generator=g)
+    d, xb, wk, _, shp = conv_setup(x, w, 7, torch.bfloat16)
+    gyb = gy.cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FV_WG7_PACK", mode)
+        slab = torch.full((L.query("fv_conv2d_wgrad_slab_elems", ctypes.byref(d)),), float("nan"), device="cuda")
+        bslab = torch.empty(L.query("fv_conv2d_wgrad_bias_slab_elems", ctypes.byref(d)), device="cuda")
+        L.call("fv_conv2d_bwd_weight", ctypes.byref(d), xb.data_ptr(), None, None, gyb.data_ptr(), 64,
+               slab.data_ptr(), bslab.data_ptr(), L.stream())
+        dw = torch.empty(64, 3, 7, 7, device="cuda")
+        db = torch.empty(64, device="cuda")
+        L.call("fv_conv2d_wgrad_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(), dw.data_ptr(),
+               db.data_ptr(), L.stream())
+        torch.cuda.synchronize()
+        res[mode] = (dw.cpu(), db.cpu())
+    assert torch.equal(res["1"][0], res["0"][0]) and torch.equal(res["1"][1], res["0"][1])
+    xq = xb[:, :3].float().cpu()
+    wr = w.clone().requires_grad_(True)
+    (F.conv2d(xq, wr, padding=3) * gyb.float().cpu()).sum().backward()
+    assert rel(res["1"][0], wr.grad) < TOL[torch.bfloat16]
+    assert torch.isfinite(res["1"][0]).all()
