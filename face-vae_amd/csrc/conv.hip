@@ -111,6 +111,8 @@ struct ConvArgs {
   float bns;
   int wus;        // halo 3x3 kernels: bytes per tap unit of the stage-major weights (rows * 64)
   unsigned* roll; // fp8: the operand's delayed-scaling site, rolled by block 0 (fp8_site_roll)
+  int nrec;       // BN records the caller sized `stats` for (fv_conv2d_stats_blocks / fp8): every
+                  // record write is bounded by it (not only by the kernel's own tiling)
 };
 
 // output pixel of tile-space pixel p (identity unless a sub-pixel phase is set)
@@ -269,7 +271,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[RN
   // tile -- are not written: the caller sized the buffer with that many, fv_conv2d_stats_blocks;
   // the sub-pixel launches number records over the 4 phases of a low-res a.P, hence Ho x Wo)
   const long pout = a.Ho ? (long)a.N * a.Ho * a.Wo : (long)a.P;
-  if (a.stats && (long)(tm * WM + wm) < (pout + RM * 16 - 1) / (RM * 16)) {
+  if (a.stats && (long)(tm * WM + wm) < (pout + RM * 16 - 1) / (RM * 16) && tm * WM + wm < a.nrec) {
     // BN statistics partials, one record per wave row (RM*16 pixels, record index
     // tm*WM + wm): per output channel (sum, sum of squares) over the record's valid pixels,
     // reduced over the 16 pixel lanes of each m-tile by shuffles -- no LDS, no barrier.
@@ -1153,7 +1155,7 @@ __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[
       const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
       const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
       const float val = lr < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
-      if (lr < 8) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
+      if (lr < 8 && rec < a.nrec) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
     }
   }
   __syncthreads();
@@ -1741,8 +1743,8 @@ conv_halo_fwd(ConvArgs a, unsigned x_bytes) {
 // Tile: 4 rows x 64 columns x 64 co; wave w owns pixels [32w, 32w + 32) x all 64 co.
 // ----------------------------------------------------------------------------------------
 constexpr int C74_TR = 4, C74_HW = 71, C74_HR = C74_TR + 6;          // halo row: 64 + 6 + 1 (zero) px
-constexpr int C74_K = 224, C74_WROW = C74_K / 8 + 1;                 // 16-B chunks per LDS weight row
-constexpr int C74_WQ = (64 * C74_WROW + 63) / 64;                    // 1-KB weight pieces
+constexpr int C74_K = 224, C74_WCOL = C74_K / 8;                     // 16-B chunks (k columns) per weight row
+constexpr int C74_WQ = 64 * C74_WCOL / 64;                           // 1-KB weight pieces (28)
 constexpr int C74_HQ = (C74_HR * C74_HW + 63) / 64;                  // 1-KB halo pieces (16 B / px)
 __global__ void __launch_bounds__(512, 4)
 conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
@@ -1770,11 +1772,14 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
       dma16s(xr, sbase + WB + buf * HB + q * 1024, ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * 8) * 2) : 0x80000000u, 0u);
     }
   };
+  // weight image [n-tile][k column][16 rows] of 16-B chunks: the 16 lanes of every ds_read_b128
+  // lane group read 16 different rows of one column = 16 different bank slots (the padded
+  // [row][29] image put 2 lanes of a group on one slot: 50 % of the LDS cycles were bank
+  // conflicts, profiles/r6/r6_convpmc_7x7.txt)
   for (int q = wave; q < C74_WQ; q += 8) {
     const int L = q * 64 + lane;
-    const int row = L / C74_WROW, ch = L - (L / C74_WROW) * C74_WROW;
-    const bool ok = row < 64 && ch < C74_K / 8;
-    dma16s(wr, sbase + q * 1024, ok ? (unsigned)((row * C74_K + ch * 8) * 2) : 0x80000000u, 0u);
+    const int li = L & 15, t = L >> 4, col = t % C74_WCOL, row = (t / C74_WCOL) * 16 + li;
+    dma16s(wr, sbase + q * 1024, (unsigned)((row * C74_K + col * 8) * 2), 0u);
   }
   int tile = blockIdx.x;
   if (tile < ntiles) issue_halo(tile, 0);
@@ -1803,7 +1808,7 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) v += sp[w * 128];
-      a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
+      if (tile - (int)gridDim.x < a.nrec) a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
     }
     // the halo two tiles ahead goes into the buffer the previous tile released at its barrier
     const int ahead = tile + 2 * gridDim.x;
@@ -1819,7 +1824,7 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
       bf16x8 bfr[4], afr[2];
 #pragma unroll
       for (int nn = 0; nn < 4; ++nn)
-        bfr[nn] = *reinterpret_cast<const bf16x8*>(smem + ((nn * 16 + li) * C74_WROW + r * 4 + g) * 16);
+        bfr[nn] = *reinterpret_cast<const bf16x8*>(smem + ((nn * C74_WCOL + r * 4 + g) * 16 + li) * 16);
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         const char* p = hs + (hbase[m] + r * C74_HW + 2 * g) * 16;
@@ -1899,7 +1904,7 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < 8; ++w) v += sp[w * 128];
-    a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
+    if (tile - (int)gridDim.x < a.nrec) a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
   }
 }
 
@@ -2154,7 +2159,7 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
         const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
         const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
         const float val = lr < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
-        if (lr < 8) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
+        if (lr < 8 && rec < a.nrec) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
       }
     }
   }
@@ -2318,7 +2323,7 @@ conv3up_band_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
         const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
         const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
         const float val = lr < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
-        if (lr < 8) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
+        if (lr < 8 && rec < a.nrec) a.stats[(long)(rec * 2 + (lr >> 2)) * a.Cout + cb + ii] = val;
       }
     }
   }
@@ -2539,7 +2544,9 @@ conv7_n3_fwd2(ConvArgs a, unsigned x_bytes, int band) {
       const int px = L >> 3, ch = L & 7;
       const int ww = w0 - 3 + px;
       const bool ok = px < 70 && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-      const unsigned off = ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * 64 + ((ch ^ (px & 7)) << 3)) * 2)
+      // 16-B chunk swizzle by (px >> 1) & 7: 16 consecutive pixels (one fragment read) land on 16
+      // different bank slots (by px & 7, pixels 8 apart shared one: 14 % bank conflicts)
+      const unsigned off = ok ? (unsigned)((((n * a.H + hh) * a.W + ww) * 64 + ((ch ^ ((px >> 1) & 7)) << 3)) * 2)
                               : 0x80000000u;
       dma16(xr, smem + (rel % C7B_SLOTS) * C7B_ROWB + pc * 1024, off);
     }
@@ -2594,7 +2601,7 @@ conv7_n3_fwd2(ConvArgs a, unsigned x_bytes, int band) {
         bf16x8 afr[3];
 #pragma unroll
         for (int t = 0; t < 3; ++t)
-          afr[t] = *reinterpret_cast<const bf16x8*>(slot + (apix[t] * 8 + (c ^ (apix[t] & 7))) * 16);
+          afr[t] = *reinterpret_cast<const bf16x8*>(slot + (apix[t] * 8 + (c ^ ((apix[t] >> 1) & 7))) * 16);
         if (half == 0) {
           acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bw[ks][0], acc[0], 0, 0, 0);
           acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[0], bw[ks][1], acc[1], 0, 0, 0);
@@ -2634,7 +2641,7 @@ conv7_n3_fwd2(ConvArgs a, unsigned x_bytes, int band) {
       if (a.stats) {
         const float sv = wave_sum(v), qv = wave_sum(v * v);
         const int rec = ((n * a.H + h0 + rr) * a.W + w0) >> 6;
-        if (lane == 0) {
+        if (lane == 0 && rec < a.nrec) {
           a.stats[(long)(rec * 2) * a.Cout + co] = sv;
           a.stats[(long)(rec * 2 + 1) * a.Cout + co] = qv;
         }
@@ -5441,6 +5448,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
   const FwdTile t = fwd_tile(d->cout);
   a.x = x; a.w = wk; a.bias = bias; a.psc = psc; a.psh = psh; a.slope = d->pro_slope;
   a.res = res; a.y = y; a.stats = stats;
+  a.nrec = stats ? fv_conv2d_stats_blocks(d) : 0;
   a.N = d->n; a.H = d->h; a.W = d->w;
   a.Hin = d->upsample ? d->h / 2 : d->h;
   a.Win = d->upsample ? d->w / 2 : d->w;
@@ -6795,6 +6803,7 @@ int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, co
                  unsigned* roll = nullptr) {
   ConvArgs a{};
   a.x = x8; a.w = w8; a.bias = bias; a.res = res; a.y = y; a.stats = stats;
+  a.nrec = stats ? fv_conv2d_fp8_stats_blocks(d) : 0;
   a.dq0 = dq_x; a.dq1 = dq_w;
   a.roll = roll;
   a.N = d->n; a.H = d->h; a.W = d->w; a.Hin = d->h; a.Win = d->w;
