@@ -1207,18 +1207,6 @@ __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[
 // per-lane base and the fragments of the step are immediate offsets from it (measured in the
 // asm: 4 non-MFMA VALU per 64-MFMA step against 88).  LDS: [NSB weight stages][2 halo buffers].
 //
-// PRO (NAC blocks: BN-apply + activation of the conv INPUT, modules.py:13,31-39,119-125): the
-// halo is staged pre-BN and transformed IN LDS, once per 32-channel chunk, by the waves that
-// DMA'd it: slot -> bf16(act(fma(v, scale[c], shift[c]))), the exact arithmetic of the separate
-// act_fwd pass (bn.hip), which this removes together with its output tensor.  Out-of-image
-// slots (the zero padding of the ACTIVATED input) are skipped, so they stay 0.  Chunks 0 / 1
-// are transformed after the prologue barrier (+1 barrier); chunk c >= 2 lands by the barrier of
-// the step after its issue and is transformed at the end of that step by waves 0-3 and of the
-// next by waves 4-7 (the SIMD partners of 0-3: one wave of a SIMD transforms while the other
-// runs MFMAs), published by the following barrier, before its first fragment read (the first
-// read needs it published by barrier floor(9c / 2) - 1 (c even) / (9c - 3) / 2 (c odd), the
-// later half publishes at barrier 9c / 2 - 2 / (9c - 5) / 2).
-//
 // SCH (schedule of the two waves of a SIMD, waves w and w + NW / 2): bit 0 = one static
 // s_setprio 1 for waves NW/2 .. NW-1 before the main loop instead of prio flips around every
 // MFMA cluster; bit 1 = stagger: waves NW/2 .. NW-1 pass each step's barrier before the MFMAs
@@ -1245,11 +1233,9 @@ __device__ __forceinline__ void subpix_epilogue(const ConvArgs& a, f32x4 (&acc)[
 // prologue DMA (weight stage 0, halo chunks 0 / 1) is issued and THEN the stores: every CU
 // reaches its epilogue at the same time, so a tile's 128 KB of stores (HBM-bound as a burst)
 // drain under the next tile's prologue instead of after it.
-template <int WN, int WM, int RN, int RM, int NSB, bool PRO = false, int SCH = 0, int MODE = 0, bool PERS = false>
+template <int WN, int WM, int RN, int RM, int NSB, int SCH = 0, int MODE = 0, bool PERS = false>
 __global__ void __launch_bounds__(64 * WN * WM, (WN * RN * 16 >= 256 || WN == 1) ? 1 : 2)
 conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
-  static_assert(!(PERS && PRO), "persistent tiles: no staged prologue");
-  static_assert(MODE == 0 || !PRO, "phase modes: no prologue");
   static_assert(MODE != 1 || (WN == 4 && RN == 4), "sub-pixel forward: one phase of 64 channels per wave column");
   constexpr int UPC = MODE ? 4 : 9;                        // tap units per 32-channel chunk
   constexpr int NW = WN * WM;
@@ -1263,8 +1249,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
   constexpr int QB = BN / 16, JB = QB >= NW ? QB / NW : 1;
   static_assert(QB % NW == 0 || NW % QB == 0, "weight pieces per wave");
   constexpr int BST = BN * 64, STG = 2 * BST, WOFF = NSB * STG;
-  constexpr int PROB = PRO ? 2 * 256 * 4 : 0;              // scale / shift of <= 256 input channels
-  constexpr int MAIN = WOFF + 2 * HALO + PROB, EPI = BM * BN * 2;
+  constexpr int MAIN = WOFF + 2 * HALO, EPI = BM * BN * 2;
   static_assert(MAIN <= 163840, "LDS");
   static_assert(STG * (NSB - 1) + BST + (BN - 16) * 64 < 65536, "weight fragment immediates");
   __shared__ __attribute__((aligned(1024))) char smem[MAIN > EPI ? MAIN : EPI];
@@ -1313,10 +1298,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
   };
   // halo slots of this wave: slot k = 16-B chunk k % 6 of halo pixel k / 6 (chunks 4, 5 pad)
   unsigned hoff[JH];
-  unsigned hval = 0;             // PRO: bit j = slot j holds image data (a transform target)
-  int hcb[PRO ? JH : 1];         // PRO: the slot's channel offset in a 32-channel chunk
   auto mk_hoff = [&](const Tile& t) {
-    hval = 0;
 #pragma unroll
     for (int j = 0; j < JH; ++j) {
       const int k = (wave + j * NW) * 64 + lane;
@@ -1328,37 +1310,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
         hoff[j] = ok ? (unsigned)((((t.n * a.Hin + 2 * ih) * a.Win + 2 * iw) * a.K + (ch << 3)) * 2) : 0x80000000u;
       else
         hoff[j] = ok ? (unsigned)(((((t.n * a.H + ih) * a.W + iw) << a.lgCin) + (ch << 3)) * 2) : 0x80000000u;
-      if constexpr (PRO) {
-        hval |= ok ? 1u << j : 0u;
-        hcb[j] = ch * 8;
-      }
-    }
-  };
-  float* const sst = reinterpret_cast<float*>(smem + WOFF + 2 * HALO);    // PRO: [scale 256][shift 256]
-  if constexpr (PRO) {
-    for (int i = tid; i < a.Cin; i += NW * 64) {
-      sst[i] = a.psc[i];
-      sst[256 + i] = a.psh[i];
-    }
-  }
-  // PRO: transform this wave's slots of halo chunk c in place (they landed: see above)
-  auto xform = [&](int c) {
-    if constexpr (PRO) {
-      char* const Hs = smem + WOFF + (c & 1) * HALO;
-#pragma unroll
-      for (int j = 0; j < JH; ++j) {
-        if ((hval >> j) & 1u) {
-          uint4* const p = reinterpret_cast<uint4*>(Hs + (wave + j * NW) * 1024 + lane * 16);
-          const float* const sc = sst + c * 32 + hcb[j];
-          Chunk8<bf16> v;
-          v.raw = *p;
-          float f[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) f[q] = fv_act(fmaf(v.get(q), sc[q], sc[256 + q]), a.slope);
-          v.set8(f);
-          *p = v.raw;
-        }
-      }
     }
   };
   auto issue_b = [&](unsigned wbase, int j, int buf) {
@@ -1441,9 +1392,7 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
     // issued after them (chunk 1, first read at unit UPC; stages 1 .. NSB - 2) stay in flight
     // past the prologue barrier and are waited for at the first step barriers; a later tile's
     // prologue was issued before the previous tile's stores, so all is waited for
-    if (PRO) {
-      wait_vm<0>();                        // chunks 0 and 1 are transformed right after the barrier
-    } else {
+    {
       const int nh1 = (JH - 1) + ((JH - 1) * NW + wave < HQ ? 1 : 0);
       int later = nh1;
       for (int i = 1; i < NSB - 1; ++i) later += bcnt(i);
@@ -1454,11 +1403,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
       wait_vm_upto(later);
     }
     __syncthreads();
-    if constexpr (PRO) {
-      xform(0);
-      xform(1);
-      __syncthreads();
-    }
     FV_DIAG_PROLOGUE();
     f32x4 acc[RN][RM];
 #pragma unroll
@@ -1483,7 +1427,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
     }
     load_frags(fa0, fb0, 0, 0);
     int hn = 2, hstep = halo_step(2);
-    int xc = -1, xstep = -1;               // PRO: halo chunk to transform at the end of step xstep
     int bj = 0;
     if constexpr (SCH & 1) {
       if (hi) __builtin_amdgcn_s_setprio(1);
@@ -1516,10 +1459,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
       if (!stag) step_barrier();
       if (hn < nch && j == hstep) {
         issue_halo(hn);
-        if constexpr (PRO) {
-          xc = hn;
-          xstep = j + 1 + (wave >= 4 ? 1 : 0);   // landed by the next step's barrier
-        }
         ++hn;
         hstep = halo_step(hn);
       }
@@ -1531,9 +1470,6 @@ conv3_halo_fwd3(ConvArgs a, unsigned x_bytes, int ntiles) {
       load_frags(fa0, fb0, 2 * j + 2, bn1);
       FV_DIAG_ISSUE_END();
       mfma_all(fa1, fb1);
-      if constexpr (PRO) {
-        if (j == xstep) xform(xc);     // published by the next step's barrier
-      }
       bj = bn1;
     }
     load_frags(fa1, fb1, 2 * nsteps - 1, bj);
@@ -4557,23 +4493,8 @@ bool use_v2(const fv_conv_desc* d) {
   return (long)d->n * hin * win * d->cin * 2 < (1L << 31);
 }
 
-// BN-apply + activation prologue in the halo staging (conv3_halo_fwd3<..., PRO>, the sliding-row
-// weight gradient's PRO variant): the NAC ResBlock convs (256-channel co tiles, <= 256 input
-// channels).  Measured SLOWER than materialising act(BN(x)) with the separate pass (r4, one box,
-// B=32: res fwd 147-155 -> 170-172 us, wgrad 157-162 -> 169 us against the 21.5 us act_fwd pass
-// each saves; step 12.48 -> 12.70 ms), so the host side does not use it by default
-// (ops._NAC_STAGED, FV_NAC_STAGED=1); this reports whether a descriptor is supported.
-static bool pro3_ok(const fv_conv_desc* d) {
-  if (d->dtype != FV_BF16 || d->ksize != 3 || d->upsample || !d->pro_act) return false;
-  if (d->out_nchw_f32 || d->epi_sigmoid || d->ldy % 8 || d->cout % 256) return false;
-  if (d->cin % 64 || d->cin > 256 || d->cin_valid != d->cin || d->w % 64 || d->h % 4) return false;
-  const long P = (long)d->n * d->h * d->w;
-  return P * d->cin * 2 < (1L << 31) && P * d->ldy * 2 < (1L << 31);
-}
-
 // 3x3 halo path (conv3_halo_fwd2 / fwd3): co per block (256 / 128 / 64), 0 when not eligible
 int halo3_bn(const fv_conv_desc* d) {
-  if (d->pro_act) return pro3_ok(d) ? 256 : 0;
   if (!use_v2(d) || d->ksize != 3 || d->upsample || d->w % 64 || d->h % 4) return 0;
   if ((long)d->n * d->h * d->w * d->ldy * 2 >= (1L << 31)) return 0;
   // co % 256: the pipelined pair-of-taps kernel (3 % over conv_fwd_v2's 256 x 256 tile on
@@ -4803,9 +4724,9 @@ bool use_h3w(const fv_conv_desc* d) {
     g_h3w_all = (e && e[0] == '0') ? 0 : 1;
   }
   const bool cin_ok = d->cin == 64 || (g_h3w_all && d->cin % 64 == 0);
-  // the staged BN prologue: the NAC convs, and AFE.down1 (64 input channels: the in_conv BN
-  // applied in its operand staging, fv_conv2d_pro_staged)
-  if (d->pro_act && !pro3_ok(d) && d->cin != 64) return false;
+  // the staged BN prologue: AFE.down1 only (64 input channels: the in_conv BN applied in its
+  // operand staging, fv_conv2d_pro_staged)
+  if (d->pro_act && d->cin != 64) return false;
   return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && cin_ok &&
          d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
 }
@@ -5137,9 +5058,9 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
 static bool use_c64(const fv_conv_desc* fd);
 int fv_conv2d_pro_staged(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK || !d->pro_act) return 0;
-  // the NAC halo convs, or a 64-channel band conv (conv3c64_fwd<true>) whose weight gradient
-  // runs the sliding-row kernel's PRO variant
-  return (pro3_ok(d) || (use_c64(d) && plan_wgrad(d).v2 == 5)) ? 1 : 0;
+  // a 64-channel band conv (conv3c64_fwd<true>) whose weight gradient runs the sliding-row
+  // kernel's PRO variant (the staged NAC ResBlock convs, "option A", were removed in r6)
+  return (use_c64(d) && plan_wgrad(d).v2 == 5) ? 1 : 0;
 }
 
 int fv_conv2d_dgrad_lowres(const fv_conv_desc* d) {
@@ -5406,14 +5327,14 @@ static void launch_h3(int ntiles, hipStream_t s, const ConvArgs& a, unsigned xb)
   const dim3 g(pers ? cap : ntiles), b(64 * WN * WM);
   if constexpr (WN * RN * 16 < 256) {
     if (pers) {
-      if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 2, MODE, true>), g, b, 0, s, a, xb, ntiles);
-      else hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 0, MODE, true>), g, b, 0, s, a, xb, ntiles);
+      if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, 2, MODE, true>), g, b, 0, s, a, xb, ntiles);
+      else hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, 0, MODE, true>), g, b, 0, s, a, xb, ntiles);
       return;
     }
   }
   {
-    if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 2, MODE, false>), g, b, 0, s, a, xb, ntiles);
-    else hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, false, 0, MODE, false>), g, b, 0, s, a, xb, ntiles);
+    if (sch == 2) hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, 2, MODE, false>), g, b, 0, s, a, xb, ntiles);
+    else hipLaunchKernelGGL((conv3_halo_fwd3<WN, WM, RN, RM, NSB, 0, MODE, false>), g, b, 0, s, a, xb, ntiles);
   }
 }
 }  // extern "C++"
@@ -5602,10 +5523,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     // registers (buffer_load_dwordx4 a step ahead, ds_write_b128 after the next barrier) instead
     // of LDS-DMA: res fwd / dgrad 147 / 136 -> 150.5 / 141 us, Generator.in_conv 147-152 ->
     // 160-162 us, step +0.17 ms.)
-    if (d->pro_act) {
-      FV_REQUIRE(bn == 256 && psc && psh, "staged BN prologue: bad arguments");
-      hipLaunchKernelGGL((conv3_halo_fwd3<4, 2, 4, 8, 2, true>), dim3(nblk), dim3(512), 0, s, a, xb, nblk);
-    } else if (bn >= 128 && a.Cin % 64 == 0) {
+    if (bn >= 128 && a.Cin % 64 == 0) {
       if (bn == 256) launch_h3<4, 2, 4, 8, 2, 0>(nblk, s, a, xb);
       else launch_h3<2, 4, 4, 4, 3, 0>(nblk, s, a, xb);
     } else if (bn == 256) {
@@ -5726,17 +5644,6 @@ int fv_conv2d_fwd_sr(const fv_conv_desc* d, const void* x, const void* wk, const
   FV_REQUIRE(x && wk && y && sr && sr->mode == 1, "fwd_sr: null pointer or mode != 1");
   FV_REQUIRE(!d->pro_act && !d->out_nchw_f32 && d->ldy == d->cout, "fwd_sr: plain NHWC output only");
   return conv_run(d, x, wk, bias, nullptr, nullptr, res, y, nullptr, (hipStream_t)stream, sr);
-}
-
-int fv_conv2d_fwd_pro_sr(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
-                         const float* pro_scale, const float* pro_shift, const void* res, void* y,
-                         const fv_store_reduce* sr, void* stream) {
-  int st = check_desc(d);
-  if (st) return st;
-  FV_REQUIRE(x && wk && y && sr && sr->mode == 1, "fwd_pro_sr: null pointer or mode != 1");
-  FV_REQUIRE(!d->pro_act || (pro_scale && pro_shift), "prologue needs scale/shift");
-  FV_REQUIRE(!d->out_nchw_f32 && d->ldy == d->cout, "fwd_pro_sr: plain NHWC output only");
-  return conv_run(d, x, wk, bias, pro_scale, pro_shift, res, y, nullptr, (hipStream_t)stream, sr);
 }
 
 int fv_conv2d_bwd_data_sr(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,

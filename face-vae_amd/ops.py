@@ -934,26 +934,12 @@ def _bnred_of(src):
     return None if src is None or src["nuse"] != 1 else (src["bn"], src["r"], src["y"], src["slope"])
 
 
-# BN-apply + ReLU in the NAC convs' operand staging (DESIGN.md §4 "Round 4, measured": built,
-# slower than the separate act_fwd pass on MI355X, so off unless FV_NAC_STAGED=1; tests flip it)
-_NAC_STAGED = os.environ.get("FV_NAC_STAGED", "0") == "1"
-
-
-def nac_staged(dtype, N, H, W, C, k):
-    """True when the NAC convs of a ResBlock2D of this shape take the BN-apply + ReLU in their
-    operand staging (fv_conv2d_pro_staged: bf16, 256-channel halo kernels): act(BN(x)) is then
-    never written to HBM.  Only with _NAC_STAGED."""
-    if not _NAC_STAGED or dtype != torch.bfloat16 or k != 3:
-        return False
-    return bool(query("fv_conv2d_pro_staged", ctypes.byref(desc(dtype, N, H, W, C, C, C, C, 3, pro=1))))
-
-
 class ResBlockFn(torch.autograd.Function):
     """ResBlock2D: x + NAC(NAC(x)), NAC = BN -> ReLU -> conv3x3 (modules.py:116-130).  The
     BN-apply+ReLU output of each NAC is materialised once (one HBM pass, written with its e4m3
-    copy in fp8 mode); with _NAC_STAGED (bf16, 256-channel halo kernels) each conv instead stages
-    its PRE-BN input and applies BN + ReLU in LDS (fv_conv2d_pro_staged), forward and weight
-    gradient alike -- measured slower, off by default.  The residual add runs in conv2's epilogue."""
+    copy in fp8 mode).  (Applying BN + ReLU in the convs' operand staging instead -- "option A",
+    rounds 4-5 -- measured slower twice and was removed in round 6)  The residual
+    add runs in conv2's epilogue."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, blk):
@@ -972,9 +958,6 @@ class ResBlockFn(torch.autograd.Function):
             r1 = bn_from_records(blk.bn1, rec[0], rec[1], rec[2], N * H * W, C, True, comm)
         else:
             r1 = bn_from_tensor(blk.bn1, xb, training, comm)
-        if mode != FP8 and nac_staged(mode, N, H, W, C, c1.kernel_size):
-            return ResBlockFn._forward_staged(ctx, x, xb, b1, b2, blk, r1, comm, dtype, N, H, W, C)
-        ctx.staged = False
         d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size)
         cs1 = ConvState(c1, d1, dtype, x.device, training, True, fp8=mode == FP8)
         # fp8 convs: the BN pass writes the conv's e4m3 operand beside its bf16 output
@@ -1016,48 +999,7 @@ class ResBlockFn(torch.autograd.Function):
         return out
 
     @staticmethod
-    def _forward_staged(ctx, x, xb, b1, b2, blk, r1, comm, dtype, N, H, W, C):
-        """conv1 reads x, conv2 reads t1 = conv1(.): both pre-BN, with (scale, shift) of bn1 / bn2
-        applied in the staging (conv3_halo_fwd3<..., PRO>)."""
-        training = blk.training
-        c1, c2 = blk.conv1, blk.conv2
-        d1 = desc(dtype, N, H, W, C, C, C, C, c1.kernel_size, pro=1)
-        cs1 = ConvState(c1, d1, dtype, x.device, training, True)
-        t1 = torch.empty_like(xb)
-        part = conv_forward(cs1, xb, b1, pro=(r1.scale, r1.shift), y=t1, stats=training)
-        r2 = bn_from_partials(blk.bn2, part, cs1, True, comm) if training else bn_finalize(blk.bn2, None, 0, False)
-        d2 = desc(dtype, N, H, W, C, C, C, C, c2.kernel_size, pro=1)
-        cs2 = ConvState(c2, d2, dtype, x.device, training, True)
-        out = torch.empty_like(xb)
-        geo = sr_records(d2, False) if training else None
-        pro2 = (r2.scale, r2.shift)
-        if geo is not None:
-            # out = x + conv2(.) with its (sum, sum of squares) reduced in the store pass (the next
-            # ResBlock's bn1 statistics)
-            part = _empty(geo[0] * 2 * C, F32, x.device)
-            sr = L.StoreReduce(1, ptr(part), None, None, None, None, None, 0.0)
-            _timed("fwd", d2, lambda: call("fv_conv2d_fwd_pro_sr", ctypes.byref(d2), ptr(t1), ptr(cs2.wk), ptr(b2),
-                                           ptr(r2.scale), ptr(r2.shift), ptr(xb), ptr(out), ctypes.byref(sr),
-                                           stream()))
-            if CHECK is not None:
-                CHECK("fwd", cs2, x=t1, bias=b2, pro=pro2, res=xb, y=out)
-            blk._fv_out_rec = (part, geo[0], geo[1])
-        else:
-            conv_forward(cs2, t1, b2, pro=pro2, res=xb, y=out)
-            blk._fv_out_rec = None
-        cs1.release()
-        cs2.release()
-        blk._fv_q8_consumer = None
-        ctx.q8_prev = None
-        ctx.staged = True
-        ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm = blk, cs1, cs2, r1, r2, comm
-        ctx.save_for_backward(x, xb, t1)
-        return out
-
-    @staticmethod
     def backward(ctx, dout):
-        if ctx.staged:
-            return ResBlockFn._backward_staged(ctx, dout)
         x, xb, t1, a1, a2 = ctx.saved_tensors
         blk, cs1, cs2, r1, r2, comm = ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm
         C = xb.shape[1]
@@ -1089,21 +1031,6 @@ class ResBlockFn(torch.autograd.Function):
                                              q8=prev[1] if prev is not None else None)
         if prev is not None and q and q[0] is not None:
             prev[0].__dict__["_fv_fp8_pending"] = (weakref.ref(dxb), dxb._version, q[0])
-        dx = from_nhwc(dxb, x)
-        return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None
-
-    @staticmethod
-    def _backward_staged(ctx, dout):
-        """The weight gradients read the pre-BN inputs (t1, x) with the same staged BN-apply;
-        the BN backward passes recompute the ReLU mask from them as always."""
-        x, xb, t1 = ctx.saved_tensors
-        blk, cs1, cs2, r1, r2, comm = ctx.blk, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm
-        C = xb.shape[1]
-        dout = grad_in(dout, xb.dtype)
-        da2, dw2, db2 = conv_backward(cs2, t1, dout, C, pro=(r2.scale, r2.shift))
-        dt1, dg2, dbe2 = bn_act_backward(da2, t1, blk.bn2, r2, 0.0, False, comm)
-        da1, dw1, db1 = conv_backward(cs1, xb, dt1, C, pro=(r1.scale, r1.shift))
-        dxb, dg1, dbe1 = bn_act_backward(da1, xb, blk.bn1, r1, 0.0, False, comm, addend=dout)
         dx = from_nhwc(dxb, x)
         return dx, dw1, db1, dg1, dbe1, dw2, db2, dg2, dbe2, None
 

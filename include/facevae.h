@@ -109,15 +109,13 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
  * stride-2 4x4 conv over dy -- and wt (fv_conv_wt_elems / fv_conv_weight_prep) holds those
  * 4x4 weights; then no fv_upsample2x_bwd follows.  0 otherwise. */
 int fv_conv2d_dgrad_lowres(const fv_conv_desc* d);
-/* 1 when the fast (halo-staged, bf16) kernels run descriptor d WITH its BN-apply prologue
- * (d->pro_act): the ResBlock2D NAC convs (modules.py:13,31-39,119-125: BN -> act -> conv3x3),
- * whose pre-BN input is staged and transformed in LDS, so act(BN(x)) is never materialised
- * (forward: fv_conv2d_fwd / fv_conv2d_fwd_pro_sr; weight gradient: fv_conv2d_bwd_weight with
- * the same scale / shift; the data gradient is w.r.t. act(BN(x)) as before), and the 64-input-
- * channel 3x3 convs (AFE.down1 consuming the in_conv CNA block's pre-BN output:
- * models.py:935-940).  0: other descriptors take the prologue on the generic register-staged
- * kernels (slow).  Measured on MI355X: the NAC variant is slower than
- * materialising act(BN(x)) with fv_bn_act_fwd, so the host side only uses it on request. */
+/* 1 when the fast (bf16) kernels run descriptor d WITH its BN-apply prologue (d->pro_act):
+ * the 64-input-channel 3x3 convs (AFE.down1 consuming the in_conv CNA block's pre-BN output,
+ * models.py:935-940, forward on the band kernel, weight gradient on the sliding-row kernel;
+ * the data gradient is w.r.t. act(BN(x)) as before), so act(BN(x)) is never materialised.
+ * 0: other descriptors take the prologue on the generic register-staged kernels (slow).
+ * Measured on MI355X: neutral against fv_bn_act_fwd + the plain conv, so the
+ * host side only uses it on request (FV_BN_PRO=1). */
 int fv_conv2d_pro_staged(const fv_conv_desc* d);
 
 /* weight gradient w.r.t. the effective (post-SN) weight, split over pixels:
@@ -154,11 +152,6 @@ typedef struct fv_store_reduce {
 int fv_conv2d_sr_records(const fv_conv_desc* d, int dgrad, int* record_pixels);
 int fv_conv2d_fwd_sr(const fv_conv_desc* d, const void* x, const void* wk, const float* bias, const void* res, void* y,
                      const fv_store_reduce* sr, void* stream);
-/* fv_conv2d_fwd_sr with a BN-apply prologue (d->pro_act: the second conv of a ResBlock2D, whose
- * input act(BN2(t)) is formed in the staging) */
-int fv_conv2d_fwd_pro_sr(const fv_conv_desc* d, const void* x, const void* wk, const float* bias,
-                         const float* pro_scale, const float* pro_shift, const void* res, void* y,
-                         const fv_store_reduce* sr, void* stream);
 int fv_conv2d_bwd_data_sr(const fv_conv_desc* d, const void* dy, int ldy_dy, const void* wt, void* dx,
                           const fv_store_reduce* sr, void* stream);
 /* BN backward from store-pass records: dgamma / dbeta (either may be NULL) and k [2][c] over

@@ -179,27 +179,6 @@ def test_bn_eval_mode_matches_oracle():
             assert torch.equal(after[k].cpu(), v.detach().cpu() if v.is_floating_point() else v), k
 
 
-def test_nac_staged_launches():
-    """The staged BN-apply + ReLU of the ResBlock convs (ops._NAC_STAGED; off by default, DESIGN
-    §4 "Round 4, measured"): every launch of the B=32 step with the 12 ResBlock convs on the
-    PRO kernels, gated as the default path (the checker applies BN + ReLU to the pre-BN input
-    in fp32 and rounds it to bf16, as the kernels do)."""
-    prev = ops._NAC_STAGED
-    ops._NAC_STAGED = True
-    try:
-        x, eps = _inputs(32, 256)
-        *_, chk = _gpu_step(fv.FaceVAEConfig(), torch.bfloat16, x, eps, lambda m: LaunchChecker(m, torch.bfloat16))
-    finally:
-        ops._NAC_STAGED = prev
-    print("\n[256x256 B=32 bf16, staged NAC] per-launch deviation\n" + chk.report())
-    res = [r for r in chk.rows if r["layer"].startswith("generator.res.") and r["kind"] in ("fwd", "wgrad", "dgrad")]
-    assert len(res) == 36
-    gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 1e-4,
-            "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}
-    bad = [r for r in chk.rows if not (r["rel_l2"] <= _gate(gate, r, fv.FaceVAEConfig()) and r["worst"] <= 1.0)]
-    assert not bad, bad
-
-
 def _fp8_launch_check(B):
     x, eps = _inputs(B, 256)
     *_, chk = _gpu_step(fv.FaceVAEConfig(), torch.float8_e4m3fn, x, eps,

@@ -30,9 +30,9 @@ import re
 # dispatches per step: the 13 256->256 ones first (12 res + Generator.in_conv, backward order),
 # then AFE.down2's two.
 DOMS = {
-    # (r5 names: conv3_halo_fwd3<4, 2, 4, 8, 2, false, SCH, MODE 0, false>)
-    "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false(, \d, 0, false)?)?>"), 512 * 512),
-    "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false(, \d, 0, false)?)?>"), 512 * 512),
+    # (r5 names: conv3_halo_fwd3<4, 2, 4, 8, 2, false, SCH, MODE 0, false>; r6 dropped the PRO flag)
+    "fwd": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false)?(, \d, 0, false)?>"), 512 * 512),
+    "dgrad": (re.compile(r"conv3_halo_fwd3<4, 2, 4, 8, 2(, false)?(, \d, 0, false)?>"), 512 * 512),
     "wgrad": (re.compile(r"conv3_halo_wgrad2<4(, false)?>"), 256 * 512),
 }
 FWD_PER_STEP = 13

@@ -15,8 +15,14 @@ from collections import defaultdict
 
 from steptrace import load, short
 
+
+def _h3(n, prefix, rest):
+    """conv3_halo_fwd3<prefix, [false, ]rest...>: the r5 template had a PRO flag after NSB"""
+    return n.startswith(f"conv3_halo_fwd3<{prefix}, false, {rest}") or n.startswith(f"conv3_halo_fwd3<{prefix}, {rest}")
+
+
 FAMILIES = [
-    ("res conv fwd/dgrad", lambda n: n.startswith("conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2, 0")),
+    ("res conv fwd/dgrad", lambda n: _h3(n, "4, 2, 4, 8, 2", "2, 0")),
     ("res+down wgrad", lambda n: n.startswith("conv3_halo_wgrad2")),
     ("wgrad slab reduce", lambda n: "wgrad_reduce" in n or "subpix_split_sum" in n or "subpix_fold" in n
      or "w7_reduce" in n),
@@ -26,11 +32,10 @@ FAMILIES = [
     ("1x1 convs", lambda n: n.startswith("conv_fwd_v2<1") or n.startswith("conv_wgrad_v2<1")
      or n.startswith("conv1x1")),
     ("down1 fwd/dgrad", lambda n: n.startswith("conv3c64_fwd") or n.startswith("conv3_halo_fwd3<1, 8")),
-    ("down2 fwd/dgrad", lambda n: n.startswith("conv3_halo_fwd3<2, 4, 4, 4, 3, false, 2, 0")),
+    ("down2 fwd/dgrad", lambda n: _h3(n, "2, 4, 4, 4, 3", "2, 0")),
     ("up family", lambda n: n.startswith("conv3up") or n.startswith("conv3_up_wgrad")
-     or n.startswith("conv3_halo_fwd3<2, 4, 4, 4, 3, false, 2, 2")
-     or n.startswith("conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2, 1")
-     or n.startswith("conv3_halo_fwd3<4, 2, 4, 8, 2, false, 2, 2")),
+     or _h3(n, "2, 4, 4, 4, 3", "2, 2") or _h3(n, "4, 2, 4, 8, 2", "2, 1")
+     or _h3(n, "4, 2, 4, 8, 2", "2, 2")),
 ]
 
 
