@@ -72,7 +72,6 @@ _SIGS = {
     "fv_conv2d_wgrad_reduce": (c_int, [D, P, P, P, P, P]),
     "fv_conv2d_sr_records": (c_int, [D, c_int, POINTER(c_int)]),
     "fv_conv2d_fwd_sr": (c_int, [D, P, P, P, P, P, P, P]),
-    "fv_conv2d_pro_staged": (c_int, [D]),
     "fv_conv2d_bwd_data_sr": (c_int, [D, P, c_int, P, P, P, P]),
     "fv_bn_bwd_from_records": (c_int, [P, c_int, c_int, c_long, c_int, c_long, P, P, P, P, P, P]),
     "fv_convt_supported": (c_int, [D]),

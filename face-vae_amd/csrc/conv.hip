@@ -1861,18 +1861,10 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
 // over 8 iterations = one record of 512 pixels per (wave row, 8 iterations), 16-B bf16 stores
 // (v_permlane16_swap pairs the two 16-channel fragments).  Replaces conv_fwd_v2's per-tap DMA.
 // ----------------------------------------------------------------------------------------
-// PRO ("option B": AFE.in_conv's BN-apply + ReLU in this consumer): x is the
-// PRE-BN in_conv output; each wave transforms the input-row pieces it DMA'd, in LDS, once they
-// landed (its own counted vmcnt) and before the barrier that publishes them --
-// v -> bf16(act(v * scale[c] + shift[c])), act_fwd's arithmetic; out-of-image slots stay 0 --
-// so the separate act_fwd pass over the 256x256x64 tensor (and its output) disappears.
 constexpr int C64_PXB = 160, C64_ROWB = 11 * 1024, C64_NR = 10, C64_G = 8;
-constexpr int C64_XK = 10;             // PRO: k-step at which the next rows' transform starts
-template <bool PRO = false>
 __global__ void __launch_bounds__(512, 1)
 conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
   __shared__ __attribute__((aligned(1024))) char smem[C64_NR * C64_ROWB];
-  __shared__ __attribute__((aligned(16))) float sst[PRO ? 128 : 4];     // PRO: [scale 64][shift 64]
   __shared__ __attribute__((aligned(16))) float sbias[64];              // the block's 64 biases
   // per-lane BN partial sums of the current 8-iteration record group, [wave][16][lane] (kept
   // in LDS: their 16 registers double-buffer the B fragments instead)
@@ -1909,51 +1901,6 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
     dma16s(xr, sbase + row_slot(y) * C64_ROWB + p * 1024, rok ? v : 0x80000000u,
            rok ? (unsigned)((n * a.H + y) * a.W) * 128u : 0u);
   };
-  // PRO: BN-apply + activation of this wave's landed pieces q = wave + 8 (j0 .. j0 + XB - 1)
-  // (< nq) of the rows starting at y0, every LDS read issued before any use.  Pad chunks, halo
-  // columns outside the image and rows outside it keep their DMA zeros.
-  auto xform_batch = [&](int y0, int nq, int j0, auto xb) {
-    if constexpr (PRO) {
-      constexpr int XB = decltype(xb)::value;
-      // an opaque copy of the lane id: otherwise the per-piece addresses / channels (loop
-      // invariants) are hoisted out of the row loop and held in registers the weights need
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-      uint4 raw[XB];
-      unsigned addr[XB];
-      int c0s[XB];
-      bool okp[XB];
-#pragma unroll
-      for (int u = 0; u < XB; ++u) {
-        const int q = wave + 8 * (j0 + u);
-        const int y = y0 + q / 11, p = q % 11;
-        const unsigned v = poff_of(p, ln);
-        okp[u] = q < nq && y >= 0 && y < a.H && v != 0x80000000u;
-        const int ch = (p * 64 + ln) % 10;
-        c0s[u] = (ch < 8 ? ch : 7) * 8;
-        addr[u] = (unsigned)(row_slot(q < nq ? y : y0) * C64_ROWB + p * 1024 + ln * 16);
-        raw[u] = *reinterpret_cast<const uint4*>(smem + addr[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < XB; ++u) {
-        Chunk8<bf16> c;
-        c.raw = raw[u];
-        // 2 channels at a time: (scale, shift) in 4 registers, the result packed at once (8
-        // channels' worth of (scale, shift) spills beside the 144 weight registers)
-        unsigned o[4];
-#pragma unroll
-        for (int hh = 0; hh < 4; ++hh) {
-          const float2 sc = *reinterpret_cast<const float2*>(sst + c0s[u] + 2 * hh);
-          const float2 sh = *reinterpret_cast<const float2*>(sst + 64 + c0s[u] + 2 * hh);
-          const bf16 t[2] = {(bf16)fv_act(c.get(2 * hh) * sc.x + sh.x, a.slope),
-                             (bf16)fv_act(c.get(2 * hh + 1) * sc.y + sh.y, a.slope)};
-          o[hh] = *reinterpret_cast<const unsigned*>(t);
-        }
-        c.raw = make_uint4(o[0], o[1], o[2], o[3]);
-        if (okp[u]) *reinterpret_cast<uint4*>(smem + addr[u]) = c.raw;
-      }
-    }
-  };
 
   // the wave's weights: A fragment (cf, ks) = 16 channels x 32 k, k = tap * 64 + ci
   bf16x8 wf[2][18];
@@ -1966,12 +1913,9 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
 
   // prologue: input rows hb - 1 .. hb + 4 (66 pieces)
   for (int q = wave; q < 66; q += 8) issue_piece(hb - 1, q);
-  // biases (and the PRO scale / shift) in LDS, read back per epilogue: 8 registers fewer beside
-  // the 144 weight registers (loaded after the prologue DMA is on its way)
+  // biases in LDS, read back per epilogue: 8 registers fewer beside the 144 weight registers
+  // (loaded after the prologue DMA is on its way)
   if (tid < 64) sbias[tid] = a.bias ? a.bias[cgrp * 64 + tid] : 0.f;
-  if constexpr (PRO) {
-    if (tid < 128) sst[tid] = tid < 64 ? a.psc[tid] : a.psh[tid - 64];
-  }
   __syncthreads();
 
   float* const sa = sacc + wave * 16 * 64 + lane;         // element e at sa[e * 64]
@@ -1989,14 +1933,6 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
     // output stores (+ 2 record stores), which stay in flight
     if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    if constexpr (PRO) {
-      // the pieces this wave DMA'd for this iteration's new rows (prologue: rows hb - 1 ..
-      // hb + 4; later: rows h0 + 1 .. h0 + 4, issued in the previous iteration)
-      // iteration 0: the prologue rows hb - 1 .. hb + 4; later iterations' rows were transformed
-      // under the previous iteration's MFMAs (below)
-      if (it == 0)
-        for (int j0 = 0; wave + 8 * j0 < 66; j0 += 2) xform_batch(hb - 1, 66, j0, std::integral_constant<int, 2>{});
-    }
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -2026,15 +1962,6 @@ conv3c64_fwd(ConvArgs a, unsigned x_bytes, int nbands) {
       const bf16x8 (&fb)[4] = fbq[ks & 1];
       // the next iteration's rows h0 + 5 .. h0 + 8: pieces wave, wave + 8, ... < 44
       if (ks < 6 && more && wave + 8 * ks < 44) issue_piece(h0 + 5, wave + 8 * ks);
-      if constexpr (PRO) {
-        // ... and their BN-apply + activation once landed, one piece per k-step under this
-        // iteration's MFMAs (they go to ring slots this iteration does not read; the barrier
-        // at the next iteration's top publishes them)
-        if (ks >= C64_XK && ks < C64_XK + 6 && more) {
-          if (ks == C64_XK) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (wave + 8 * (ks - C64_XK) < 44) xform_batch(h0 + 5, 44, ks - C64_XK, std::integral_constant<int, 1>{});
-        }
-      }
 #pragma unroll
       for (int pf = 0; pf < 4; ++pf)
 #pragma unroll
@@ -3187,11 +3114,6 @@ conv_wgrad_v2(Wg2Args a) {
 //   8 waves = 2 (64 co) x 4 (9 of the 36 k-tiles of 16 = (tap, 16 ci)).
 // Output: slab [block][cout][576] (k = tap * 64 + ci: wgrad_reduce_kernel's layout) and the
 // bias slab [block][cout] (sum of dy by an all-ones MFMA operand, k-wave 0).
-// PRO (NAC blocks): x is the PRE-BN tensor; each x row is transformed in LDS after it lands,
-// v -> bf16(act(fma(v, scale, shift))) (act_fwd's arithmetic), out-of-image slots left 0.  The
-// x rows then travel one group earlier (group i = {dy row h0+i, x row h0+i+2}, ring one slot
-// deeper): row h0+i+2 lands by step i's barrier, is transformed in step i and published by
-// step i+1's barrier, where it is first read.
 // ----------------------------------------------------------------------------------------
 struct H3Wg2Args {
   const void* x;
@@ -3201,28 +3123,24 @@ struct H3Wg2Args {
   int H, W, Cout, ldd, nseg, rows, nct;
   int ldx, nci;          // x channel stride (= Cin) and 64-channel input tiles (Cin / 64)
   unsigned xbytes, dybytes;
-  const float* psc;      // PRO: BN scale / shift of the x channels, act slope
-  const float* psh;
-  float slope;
 };
 
 // (measured r5, not kept: one static s_setprio 1 for waves 4-7 instead of the per-half flips,
 // and the second k-half's dy fragments read under the first half's last MFMA group -- res /
 // down2 / down1 143 / 288 / 355 us either way, the prefetch variant spills at 256 VGPRs;
 // profiles/r5/r5c_*)
-template <int AHEAD, bool PRO = false>
+template <int AHEAD>
 __global__ void __launch_bounds__(512, 1)
 conv3_halo_wgrad2(H3Wg2Args a) {
   // AHEAD groups in flight: group i + AHEAD is issued in row step i (HBM latency under load
-  // is several row steps of MFMA work); rings: dy AHEAD + 1 deep, x AHEAD + 2 + XA deep
-  constexpr int XA = PRO ? 2 : 1;                     // group i carries x row h0 + i + XA
+  // is several row steps of MFMA work); rings: dy AHEAD + 1 deep, x AHEAD + 3 deep
+  constexpr int XA = 1;                               // group i carries x row h0 + i + XA
   constexpr int BC = 128, NSD = AHEAD + 1, NSX = AHEAD + 2 + XA;
   constexpr int DYB = 64 * BC * 2;                    // 16 KB, 16 pieces
   constexpr int XQ = (66 * 128 + 1023) / 1024;        // 9 pieces per x row (66 px x 64 ci)
   constexpr int XB = XQ * 1024;
   constexpr int NPC = 16 + XQ;                        // pieces per group (25)
-  constexpr int SSB = PRO ? 2 * 64 * 4 : 0;           // scale / shift of the block's 64 channels
-  __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB + SSB];
+  __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB];
   char* dyr = smem;
   char* xr_ = smem + NSD * DYB;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -3251,7 +3169,6 @@ conv3_halo_wgrad2(H3Wg2Args a) {
   const int npw = wave == 0 ? 4 : 3;                  // pieces of a group this wave issues
   unsigned poff[4];
   int pisx[4];
-  int pci[PRO ? 4 : 1];                               // PRO: the x lane's channel in the tile
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int q = wave + 8 * j;
@@ -3267,7 +3184,6 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       const int ci = ((((b >> 5) ^ tswz<64>(px)) << 4) | (((b >> 4) & 1) << 3));
       const int iw = w0 - 1 + px;
       poff[j] = (px < 66 && iw >= 0 && iw < a.W) ? (unsigned)((iw * a.ldx + ci0 + ci) * 2) : 0x80000000u;
-      if constexpr (PRO) pci[j] = ci;
     } else {
       poff[j] = 0x80000000u;
     }
@@ -3300,46 +3216,12 @@ conv3_halo_wgrad2(H3Wg2Args a) {
     for (int j = 0; j < 4; ++j)
       if (j < npw && pisx[j]) issue_x(y, j);
   };
-  float* const sst = reinterpret_cast<float*>(smem + NSD * DYB + NSX * XB);   // PRO: [scale 64][shift 64]
-  // PRO: transform this wave's slots of x row y (its own DMAs: landed once its vmcnt says so)
-  auto xform_row = [&](int y) {
-    if constexpr (PRO) {
-      if (y < 0 || y >= a.H) return;                  // wave-uniform: an all-zero padding row
-      char* const xs = xr_ + ((y - h0 + 1) % NSX) * XB;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (j < npw && pisx[j] && poff[j] != 0x80000000u) {
-          uint4* const p = reinterpret_cast<uint4*>(xs + (wave + 8 * j - 16) * 1024 + lane * 16);
-          Chunk8<bf16> v;
-          v.raw = *p;
-          float f[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) f[q] = fv_act(fmaf(v.get(q), sst[pci[j] + q], sst[64 + pci[j] + q]), a.slope);
-          v.set8(f);
-          *p = v.raw;
-        }
-      }
-    }
-  };
-  if constexpr (PRO) {
-    if (tid < 64) {
-      sst[tid] = a.psc[ci0 + tid];
-      sst[64 + tid] = a.psh[ci0 + tid];
-    }
-    __syncthreads();
-  }
 
 #pragma unroll
   for (int y = -1; y < XA; ++y) issue_xonly(h0 + y);
 #pragma unroll
   for (int i = 0; i < AHEAD; ++i)
     if (i < nrow) issue_group(i);
-  if constexpr (PRO) {
-    // the prologue rows are this wave's oldest DMAs; transformed here, published by step 0's barrier
-    wait_vm_dyn(min(AHEAD, nrow) * npw);
-#pragma unroll
-    for (int y = -1; y < XA; ++y) xform_row(h0 + y);
-  }
   // the wave's k-wave index as a compile-time constant (its 9 k-tiles, and the bias MFMAs of
   // k-wave 0, then need no registers)
   with_const<0, 4>(wk, [&](auto wkc) {
@@ -3389,7 +3271,6 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (i + AHEAD < nrow) issue_group(i + AHEAD);
-      if constexpr (PRO) xform_row(h0 + i + XA);      // landed with group i; read from step i + 1
       const char* dys = dyr + (i % NSD) * DYB;
       const char* xrow[3];
 #pragma unroll
@@ -4724,9 +4605,8 @@ bool use_h3w(const fv_conv_desc* d) {
     g_h3w_all = (e && e[0] == '0') ? 0 : 1;
   }
   const bool cin_ok = d->cin == 64 || (g_h3w_all && d->cin % 64 == 0);
-  // the staged BN prologue: AFE.down1 only (64 input channels: the in_conv BN applied in its
-  // operand staging, fv_conv2d_pro_staged)
-  if (d->pro_act && d->cin != 64) return false;
+  // (a BN-apply prologue runs the generic kernels: its fast variants, "option B", were removed in r6)
+  if (d->pro_act) return false;
   return d->dtype == FV_BF16 && d->ksize == 3 && !d->upsample && cin_ok &&
          d->cin_valid == d->cin && d->cout % 128 == 0 && d->w % 64 == 0;
 }
@@ -4855,7 +4735,7 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   }
   // 3x3 sliding-row wgrad (v2 == 5, conv3_halo_wgrad2): blocks = (image, 64-column strip,
   // row segment) x co tiles of 128, ~1 block per CU; splits = image x strip x segment
-  if (fits && use_h3w(d)) {             // (with the staged BN prologue too)
+  if (fits && use_h3w(d)) {
     const int strips = d->w / 64;
     p.v2 = 5;
     p.ntc = d->cout / 128;
@@ -5055,14 +4935,6 @@ size_t fv_conv_wt_elems(const fv_conv_desc* d) {
   return rows * kpad_of(d->ksize, cin_t);
 }
 
-static bool use_c64(const fv_conv_desc* fd);
-int fv_conv2d_pro_staged(const fv_conv_desc* d) {
-  if (check_desc(d) != FV_OK || !d->pro_act) return 0;
-  // a 64-channel band conv (conv3c64_fwd<true>) whose weight gradient runs the sliding-row
-  // kernel's PRO variant (the staged NAC ResBlock convs, "option A", were removed in r6)
-  return (use_c64(d) && plan_wgrad(d).v2 == 5) ? 1 : 0;
-}
-
 int fv_conv2d_dgrad_lowres(const fv_conv_desc* d) {
   if (check_desc(d) != FV_OK) return 0;
   return use_dgrad_lowres(d) ? 1 : 0;
@@ -5089,7 +4961,7 @@ static bool use_c74(const fv_conv_desc* fd) {
 // the launch of forward-conv descriptor fd runs conv3c64_fwd (64 input channels, sliding band,
 // weights in registers; plain [co][Kpad] weights)
 static bool use_c64(const fv_conv_desc* fd) {
-  return fd->dtype == FV_BF16 && fd->ksize == 3 && !fd->upsample && fd->cin == 64 &&
+  return fd->dtype == FV_BF16 && fd->ksize == 3 && !fd->upsample && !fd->pro_act && fd->cin == 64 &&
          fd->cin_valid == 64 && fd->cout % 64 == 0 && fd->ldy % 8 == 0 && !fd->epi_sigmoid && !fd->out_nchw_f32 &&
          fd->w % 64 == 0 && fd->h % 32 == 0 && (long)fd->n * fd->h * fd->w * 64 * 2 < (1L << 31) &&
          (long)fd->n * fd->h * fd->w * fd->ldy * 2 < (1L << 31);
@@ -5408,12 +5280,7 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     const int nb = c64_bands(d);
     const int nblk = d->n * (d->w / 64) * (d->cout / 64) * nb;
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * 64 * 2);
-    if (d->pro_act) {
-      FV_REQUIRE(psc && psh, "64-channel band conv: prologue needs scale / shift");
-      hipLaunchKernelGGL(conv3c64_fwd<true>, dim3(nblk), dim3(512), 0, s, a, xb, nb);
-    } else {
-      hipLaunchKernelGGL(conv3c64_fwd<false>, dim3(nblk), dim3(512), 0, s, a, xb, nb);
-    }
+    hipLaunchKernelGGL(conv3c64_fwd, dim3(nblk), dim3(512), 0, s, a, xb, nb);
     return fv_check_launch("conv2d_fwd_c64");
   }
   if (use_c74(d)) {
@@ -5743,11 +5610,7 @@ int fv_conv2d_bwd_weight(const fv_conv_desc* d, const void* x, const float* pro_
     a.ldx = d->cin; a.nci = t.ntk;
     a.xbytes = (unsigned)(P * d->cin * 2);
     a.dybytes = (unsigned)(P * ldy_dy * 2);
-    a.psc = pro_scale; a.psh = pro_shift; a.slope = d->pro_slope;
-    if (d->pro_act)
-      hipLaunchKernelGGL((conv3_halo_wgrad2<4, true>), dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
-    else
-      hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(conv3_halo_wgrad2<4>, dim3(t.ntc * t.ntk * t.nsplit), dim3(512), 0, (hipStream_t)stream, a);
     return fv_check_launch("conv2d_bwd_weight_halo3s");
   }
   if (t.v2 == 6) {

@@ -47,15 +47,6 @@ class AFE(_Block):
         self.C, self.D = C, D
 
     def forward_2d(self, x):
-        if len(self.down) and ops.bn_pro_pair_ok(self.in_conv, self.down[0].layers[0], x):
-            # in_conv's BN-apply + ReLU in down1's operand staging (ops.CNAPairFn)
-            b1, b2 = self.in_conv, self.down[0].layers[0]
-            z = ops.CNAPairFn.apply(x, b1.conv.weight_param(), b1.conv.bias, b1.bn.weight, b1.bn.bias,
-                                    b2.conv.weight_param(), b2.conv.bias, b2.bn.weight, b2.bn.bias, b1, b2)
-            holder = getattr(b2, "_fv_holder", None)
-            if holder is not None and z.requires_grad:
-                z._fv_bnsrc = (holder, z._version)   # read by the consuming conv (ops._claim_bnsrc)
-            return self.mid_conv(self.down[1:](z))
         return self.mid_conv(self.down(self.in_conv(x)))
 
     def forward(self, x):

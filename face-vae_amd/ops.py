@@ -835,90 +835,6 @@ class ConvBNActFn(torch.autograd.Function):
         return dx, dw, db, dg, dbt, None
 
 
-# BN-apply + activation of a CNA block in its consumer conv's operand staging (VERDICT r4 item 5,
-# "option B"): AFE.in_conv -> down1 as one Function, the in_conv BN output act(BN(y1)) never
-# materialised -- down1's forward (conv3c64_fwd<true>) and weight gradient (conv3_halo_wgrad2 PRO)
-# read the pre-BN y1 with (scale, shift).  Bit-identical to the unfused chain, but measured no
-# faster on MI355X (DESIGN.md §4 "Round 5": the in-LDS transform adds ~100 us to down1's forward,
-# the 100 us act_fwd pass it removes), so off unless FV_BN_PRO=1; tests flip it.
-_BN_PRO = os.environ.get("FV_BN_PRO", "0") == "1"
-
-
-def bn_pro_pair_ok(blk1, blk2, x) -> bool:
-    """blk1 (CNA, no pool / upsample) feeding blk2 (CNA 3x3) can run as CNAPairFn: bf16, and the
-    fast kernels take blk2's conv with a BN-apply prologue (fv_conv2d_pro_staged)."""
-    if not _BN_PRO or not x.is_cuda or blk1.compute_dtype() != torch.bfloat16 or blk2.compute_dtype() != torch.bfloat16:
-        return False
-    if blk1.pattern != "CNA" or blk2.pattern != "CNA" or blk1.pool or blk1.upsample or blk2.upsample:
-        return False
-    c1, c2 = blk1.conv, blk2.conv
-    if c1.out_channels != c2.in_channels or c1.out_channels % 8 or c2.out_channels % 8:
-        return False
-    N, _, H, W = x.shape
-    d2 = desc(torch.bfloat16, N, H, W, c2.in_channels, c2.in_channels, c2.out_channels, c2.out_channels,
-              c2.kernel_size, pro=1, slope=blk1.slope)
-    return bool(query("fv_conv2d_pro_staged", ctypes.byref(d2)))
-
-
-class CNAPairFn(torch.autograd.Function):
-    """Two chained CNA blocks, conv1 -> BN1 -> act -> conv2 -> BN2 -> act [-> pool], with BN1's
-    apply + act in conv2's operand staging (forward and weight gradient): y1 = conv1(x) pre-BN
-    is the only intermediate written.  The data gradient of conv2 is w.r.t. act(BN1(y1)) as in
-    the unfused chain, and BN1's backward recomputes the activation mask from y1 as always, so
-    the gradients equal ConvBNActFn twice up to bf16 rounding of the same products
-    (tests/test_bnpro_gpu.py)."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1, g1, be1, w2, b2, g2, be2, blk1, blk2):
-        dtype = storage(blk1.compute_dtype())
-        c1, c2, bn1, bn2 = blk1.conv, blk2.conv, blk1.bn, blk2.bn
-        xb, cin_pad = to_nhwc(x, dtype)
-        N, _, H, W = x.shape
-        training = blk1.training
-        C1, C2 = c1.out_channels, c2.out_channels
-        d1 = desc(dtype, N, H, W, cin_pad, c1.in_channels, C1, C1, c1.kernel_size)
-        cs1 = ConvState(c1, d1, dtype, x.device, training, need_wt=ctx.needs_input_grad[0])
-        y1 = torch.empty((N, C1, H, W), dtype=dtype, device=x.device, memory_format=CL)
-        part = conv_forward(cs1, xb, b1, y=y1, stats=training)
-        comm = blk1.bn_comm()
-        r1 = bn_from_partials(bn1, part, cs1, True, comm) if training else bn_finalize(bn1, None, 0, False)
-        if CHECK is not None:
-            CHECK("bn_stat", bn1, y=y1, r=r1)
-        d2 = desc(dtype, N, H, W, C1, C1, C2, C2, c2.kernel_size, pro=1, slope=blk1.slope)
-        cs2 = ConvState(c2, d2, dtype, x.device, training, need_wt=True)
-        y2 = torch.empty((N, C2, H, W), dtype=dtype, device=x.device, memory_format=CL)
-        part = conv_forward(cs2, y1, b2, pro=(r1.scale, r1.shift), y=y2, stats=training)
-        r2 = bn_from_partials(bn2, part, cs2, True, comm) if training else bn_finalize(bn2, None, 0, False)
-        z = bn_act_forward(y2, r2, blk2.slope, blk2.pool, bn2)
-        cs1.release()
-        cs2.release()
-        ctx.blk1, ctx.blk2, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm = blk1, blk2, cs1, cs2, r1, r2, comm
-        ctx.holder = {"bn": bn2, "r": r2, "y": y2, "slope": blk2.slope, "pool": blk2.pool, "nuse": 0}
-        blk2._fv_holder = ctx.holder if training else None
-        ctx.src = _claim_bnsrc(x, xb)
-        ctx.save_for_backward(x, xb, y1, y2)
-        return z
-
-    @staticmethod
-    def backward(ctx, dz):
-        x, xb, y1, y2 = ctx.saved_tensors
-        blk1, blk2, cs1, cs2, r1, r2, comm = ctx.blk1, ctx.blk2, ctx.cs1, ctx.cs2, ctx.r1, ctx.r2, ctx.comm
-        dz = grad_in(dz, y2.dtype)
-        recs = ctx.holder.get("recs") if ctx.holder["nuse"] == 1 else None
-        dy2, dg2, dbt2 = bn_act_backward(dz, y2, blk2.bn, r2, blk2.slope, blk2.pool, comm, recs=recs)
-        # conv2: weight gradient on the staged act(BN1(y1)); data gradient with BN1's backward sums
-        # reduced in its store pass
-        da1, dw2, db2, recs = conv_backward(cs2, y1, dy2, y2.shape[1], pro=(r1.scale, r1.shift),
-                                            bnred=(blk1.bn, r1, y1, blk1.slope), want_recs=True)
-        dy1, dg1, dbt1 = bn_act_backward(da1, y1, blk1.bn, r1, blk1.slope, False, comm, recs=recs)
-        dxb, dw1, db1, recs_in = conv_backward(cs1, xb, dy1, y1.shape[1], need_dx=ctx.needs_input_grad[0],
-                                               bnred=_bnred_of(ctx.src), want_recs=True)
-        if ctx.src is not None:
-            ctx.src["recs"] = recs_in
-        dx = from_nhwc(dxb, x) if dxb is not None else None
-        return dx, dw1, db1, dg1, dbt1, dw2, db2, dg2, dbt2, None, None
-
-
 def _claim_bnsrc(x, xb):
     """The BN-source holder of x (set by the producing CNA block) when this Function's data
     gradient will be x's whole gradient in the producer's layout; counts the consumers."""

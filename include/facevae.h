@@ -109,14 +109,6 @@ int fv_conv2d_bwd_data(const fv_conv_desc* d, const void* dy, int ldy_dy, const 
  * stride-2 4x4 conv over dy -- and wt (fv_conv_wt_elems / fv_conv_weight_prep) holds those
  * 4x4 weights; then no fv_upsample2x_bwd follows.  0 otherwise. */
 int fv_conv2d_dgrad_lowres(const fv_conv_desc* d);
-/* 1 when the fast (bf16) kernels run descriptor d WITH its BN-apply prologue (d->pro_act):
- * the 64-input-channel 3x3 convs (AFE.down1 consuming the in_conv CNA block's pre-BN output,
- * models.py:935-940, forward on the band kernel, weight gradient on the sliding-row kernel;
- * the data gradient is w.r.t. act(BN(x)) as before), so act(BN(x)) is never materialised.
- * 0: other descriptors take the prologue on the generic register-staged kernels (slow).
- * Measured on MI355X: neutral against fv_bn_act_fwd + the plain conv, so the
- * host side only uses it on request (FV_BN_PRO=1). */
-int fv_conv2d_pro_staged(const fv_conv_desc* d);
 
 /* weight gradient w.r.t. the effective (post-SN) weight, split over pixels:
  * slab [nsplit][rows][Kpad] fp32 and bias slab [nsplit][rows] fp32 (sizes from the queries). */

@@ -206,8 +206,7 @@ class LaunchChecker:
         self.bn_stat(bn, t)
 
     def bn_stat(self, bn, t):
-        """Batch statistics of a training-mode BN (also for a BN whose apply runs in its consumer
-        conv's operand staging, ops.CNAPairFn: that apply is checked by the conv's fwd row)."""
+        """Batch statistics of a training-mode BN."""
         r = t["r"]
         name = self.names.get(id(bn), "?")
         if r.count or r.stats is not None:              # training: batch statistics

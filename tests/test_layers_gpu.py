@@ -76,11 +76,9 @@ def test_every_conv_launch_of_the_timed_step(H, B):
     assert len([k for k in kinds if k[1] == "fwd"]) == 21
     assert len([k for k in kinds if k[1] == "wgrad"]) == 21
     assert len([k for k in kinds if k[1] == "dgrad"]) == 20
-    # 18 BatchNorm layers: batch statistics, forward apply, backward sums and data gradient --
-    # AFE.in_conv's apply runs in down1's operand staging (ops.CNAPairFn; checked by down1's fwd
-    # row, whose reference applies BN + ReLU to the pre-BN input), the other 17 as a pass
+    # 18 BatchNorm layers: batch statistics, forward apply, backward sums and data gradient
     assert len({r["layer"] for r in chk.rows if r["kind"] == "bn_stat"}) == 18
-    assert len({r["layer"] for r in chk.rows if r["kind"] == "bn_fwd"}) == (17 if ops._BN_PRO else 18)
+    assert len({r["layer"] for r in chk.rows if r["kind"] == "bn_fwd"}) == 18
     assert len({r["layer"] for r in chk.rows if r["kind"] == "dgamma"}) == 18
     gate = {"fwd": 5e-3, "dgrad": 5e-3, "wgrad": 1e-4, "bgrad": 1e-4,
             "bn_fwd": 5e-3, "bn_stat": 2e-3, "bn_dx": 5e-3, "dgamma": 1e-3, "dbeta": 1e-2}

@@ -96,9 +96,6 @@ def main():
                     help="load the diagnostic library (build.py --diag) and print the in-kernel clock stamps "
                          "of the halo 3x3 forward after each layer's forward timing")
     ap.add_argument("--lib", default="", help="another build of libfacevae.so (A/B of two builds on one box)")
-    ap.add_argument("--pro", action="store_true",
-                    help="BN-apply + ReLU prologue (pre-BN input) on the layers whose fast kernels stage it "
-                         "(fv_conv2d_pro_staged: the NAC ResBlock convs), fwd and wgrad")
     a = ap.parse_args()
     if a.diag:
         L.LIB_PATH = os.path.join(ROOT, "face-vae_amd", "csrc", "build_diag", "libfacevae_diag.so")
@@ -118,12 +115,6 @@ def main():
         x = torch.randn(B, cp, Hi, Hi, device="cuda").to(dtype).contiguous(memory_format=CL)
         d = ops.desc(dtype, B, H, H, cp, cin, cout, cout, k, ups)
         psc = psh = None
-        if a.pro:
-            dp = ops.desc(dtype, B, H, H, cp, cin, cout, cout, k, ups, pro=1)
-            if L.query("fv_conv2d_pro_staged", ctypes.byref(dp)):
-                d = dp
-                psc = (torch.rand(cp, device="cuda") + 0.5).contiguous()
-                psh = (torch.randn(cp, device="cuda") * 0.1).contiguous()
         w = (torch.randn(cout, cin, k, k, device="cuda") / (cin * k * k) ** 0.5).contiguous()
         wk = torch.empty(L.query("fv_conv_wk_elems", ctypes.byref(d)), dtype=dtype, device="cuda")
         wt = torch.empty(L.query("fv_conv_wt_elems", ctypes.byref(d)), dtype=dtype, device="cuda")
