@@ -3141,8 +3141,6 @@ conv3_halo_wgrad2(H3Wg2Args a) {
   constexpr int XB = XQ * 1024;
   constexpr int NPC = 16 + XQ;                        // pieces per group (25)
   __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB];
-  char* dyr = smem;
-  char* xr_ = smem + NSD * DYB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wave & 1, wk = wave >> 1;
@@ -3196,20 +3194,16 @@ conv3_halo_wgrad2(H3Wg2Args a) {
     dma16s(xr, sbase + NSD * DYB + slot * XB + q * 1024, rok ? poff[j] : 0x80000000u,
            rok ? (unsigned)(((n * a.H + y) * a.W) * a.ldx * 2) : 0u);
   };
+  // pieces q = wave + 8 j: j = 0, 1 are dy pieces (q < 16), j = 2 the x piece wave, j = 3 x
+  // piece 8 for wave 0 only (pisx / npw as compile-time structure: no per-piece branches)
   auto issue_group = [&](int i) {             // dy row h0 + i, x row h0 + i + XA
     const int h = h0 + i;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j < npw) {
-        if (!pisx[j]) {
-          const int q = wave + 8 * j;
-          dma16s(dr, sbase + (i % NSD) * DYB + q * 1024, poff[j],
-                 (unsigned)((((n * a.H + h) * a.W + w0) * a.ldd) * 2));
-        } else {
-          issue_x(h + XA, j);
-        }
-      }
-    }
+    const unsigned dbase = sbase + (i % NSD) * DYB;
+    const unsigned drow = (unsigned)((((n * a.H + h) * a.W + w0) * a.ldd) * 2);
+    dma16s(dr, dbase + wave * 1024, poff[0], drow);
+    dma16s(dr, dbase + (wave + 8) * 1024, poff[1], drow);
+    issue_x(h + XA, 2);
+    if (wave == 0) issue_x(h + XA, 3);
   };
   auto issue_xonly = [&](int y) {             // prologue rows h0 - 1 .. h0 + XA - 1
 #pragma unroll
@@ -3263,28 +3257,49 @@ conv3_halo_wgrad2(H3Wg2Args a) {
       const s16x8 v = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
       return __builtin_bit_cast(bf16x8, v);
     };
+    // ring slots of the step's dy row and x rows h - 1 .. h + 1, advanced with a wrap (scalar):
+    // each read address is then lane constant + slot base (one add per distinct address and
+    // step, the two k-halves by immediate offsets) -- the compiler's strength-reduced
+    // (i + r) % NSX took ~100 vector adds per step (r6)
+    int sd = 0, sx = 0;
     for (int i = 0; i < nrow; ++i) {
-      // group i landed; the younger groups issued so far (up to AHEAD - 1) may stay in flight
-      const int younger = min(AHEAD - 1, nrow - 1 - i);
-      wait_vm_dyn(younger * npw);
+      // group i landed; the younger groups issued so far (up to AHEAD - 1) may stay in flight:
+      // steady state 3 (AHEAD - 1) groups of npw pieces, counted at compile time per npw
+      if (i + AHEAD - 1 < nrow) {
+        if (npw == 4) wait_vm<4 * (AHEAD - 1)>();
+        else wait_vm<3 * (AHEAD - 1)>();
+      } else {
+        wait_vm_dyn((nrow - 1 - i) * npw);
+      }
       wait_lgkm0();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (i + AHEAD < nrow) issue_group(i + AHEAD);
-      const char* dys = dyr + (i % NSD) * DYB;
-      const char* xrow[3];
+      unsigned bd = (unsigned)(sd * DYB), bx[3];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) xrow[r] = xr_ + ((i + r) % NSX) * XB;     // x rows h - 1, h, h + 1
+      for (int r = 0; r < 3; ++r) {
+        const int t = sx + r;
+        bx[r] = (unsigned)(NSD * DYB + (t >= NSX ? t - NSX : t) * XB);
+      }
+      asm volatile("" : "+s"(bd), "+s"(bx[0]), "+s"(bx[1]), "+s"(bx[2]));
+      sd = sd + 1 == NSD ? 0 : sd + 1;
+      sx = sx + 1 == NSX ? 0 : sx + 1;
+      unsigned ad[4][2], ax[9][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ad[q][h] = lcd[q][h] + bd;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) ax[j][h] = lcx[j][h] + bx[((9 * WK + j) >> 2) / 3];
+      }
+      const char* const dys = smem;
       // x fragment of k-tile j of k-half kk (tap row / column constant after unrolling)
-      auto xfrag = [&](int j, int kk) {
-        const int kt = 9 * WK + j, tap = kt >> 2;
-        return frag2(xrow[tap / 3], lcx[j][0], lcx[j][1], kk * 32 * 128);
-      };
+      auto xfrag = [&](int j, int kk) { return frag2(smem, ax[j][0], ax[j][1], kk * 32 * 128); };
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         bf16x8 af[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) af[q] = frag2(dys, lcd[q][0], lcd[q][1], kk * 32 * BC * 2);
+        for (int q = 0; q < 4; ++q) af[q] = frag2(dys, ad[q][0], ad[q][1], kk * 32 * BC * 2);
         // the next x fragment is read before the current one's 4 MFMAs so the LDS latency hides
         // under them
         bf16x8 bcur = xfrag(0, kk);
