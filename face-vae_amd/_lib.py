@@ -232,7 +232,12 @@ def load():
                           "(or __graft_entry__.build()); the FaceVAE path has no CPU fallback")
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
-        f = getattr(lib, name)
+        try:
+            f = getattr(lib, name)
+        except AttributeError:
+            if os.environ.get("FV_LIB_PATH"):   # an A/B build of an older tree lacks newer entries
+                continue
+            raise
         f.restype = res
         f.argtypes = args
     if lib.fv_abi_version() != ABI_VERSION:

@@ -9,6 +9,8 @@
 //   bwd      : g = dout * act'(.)  ->  sums (g, g*yhat)  ->  dx = gamma*invstd*(g - k0 - yhat*k1)
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "common.h"
 
 namespace {
@@ -290,8 +292,29 @@ __global__ void __launch_bounds__(FOLDT) fold16_kernel(FoldArgs a) {
 // records) -> part [chunk][NV][C] (fp64).  4 lanes per record row (16 B each: a whole 64-B
 // channel segment per row), 16 rows per wave load, every load of the chunk in flight at once
 // (the one-launch fold16 over 16-64 blocks was latency-bound: 16 us for 2048 records).
-template <int NV>
-__global__ void __launch_bounds__(256) fold16_part_kernel(FoldArgs a, int rows, double* part) {
+// Level 2 in the same launch (r6): the chunk rows of a 16-channel group are stored
+// write-through (sc1, no L2 write-back), wave 0 -- the only storing wave -- drains them and takes
+// the group's arrival ticket (relaxed agent atomic); the group's last arriver acquires once and
+// sums the chunk rows in chunk order (sc1 loads).  No block waits for another.  The words live
+// in a per-device pool, a rotating slot per launch, reset by the last arriver (graph replay).
+// (A variant where the last C/16 arrivers of the BN backward reduce / tensor statistics passes
+// polled until every block had arrived and then folded 256 KB each measured slower: r6 below.)
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr int TK_SLOTS = 256, TK_WORDS = 128;        // C / 16 <= 128 groups per launch
+__device__ unsigned fv_bn_tickets[TK_SLOTS * TK_WORDS];
+
+__device__ __forceinline__ void st_sc1_f64(double* p, double v) {
+  __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1_f64(const double* p) {
+  return __longlong_as_double(
+      (long long)__hip_atomic_load((gu64*)const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <int NV, int MODE>
+__global__ void __launch_bounds__(256) fold16_part_kernel(FoldArgs a, int rows, double* part, unsigned* tk) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c0 = blockIdx.x * 16, ch = blockIdx.y, q = lane & 3;
   const int r0 = ch * rows, r1 = min(a.nrec, r0 + rows);
@@ -322,14 +345,39 @@ __global__ void __launch_bounds__(256) fold16_part_kernel(FoldArgs a, int rows, 
       if (lane < 4) red[w][v][4 * lane + k] = t;
     }
   __syncthreads();
-  if (tid >= 16) return;
+  if (w != 0) return;
+  if (tid < 16) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      double t = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += red[j][v][tid];
+      st_sc1_f64(part + ((long)ch * NV + v) * a.C + c0 + tid, t);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add((gu32*)(tk + blockIdx.x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, 0, 64);
+  if (t != gridDim.y - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // lane = (chunk lane rl, channel): chunks rl, rl + 4, ... (loads of 4 chunks in flight), then
+  // the xor tree over the 4 chunk lanes
+  const int cl = lane & 15, rl = lane >> 4, nch = gridDim.y;
+  double tot[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) tot[v] = 0.0;
+#pragma unroll 4
+  for (int r = rl; r < nch; r += 4)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) tot[v] += ld_sc1_f64(part + ((long)r * NV + v) * a.C + c0 + cl);
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    double t = 0.0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) t += red[j][v][tid];
-    part[((long)ch * NV + v) * a.C + c0 + tid] = t;
+    tot[v] += __shfl_xor(tot[v], 16, 64);
+    tot[v] += __shfl_xor(tot[v], 32, 64);
   }
+  if (lane < 16) fold_finish<NV, MODE>(a, c0 + lane, tot);
+  if (lane == 0) __hip_atomic_store((gu32*)(tk + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int NV, int MODE>
@@ -360,6 +408,18 @@ __device__ __forceinline__ void fold_finish(const FoldArgs& a, int c, const doub
   }
 }
 
+// the arrival words of one two-level fold launch: a rotating slot of the per-device pool, so
+// launches in flight on different streams never share one (a captured launch keeps its slot;
+// the kernel leaves it zeroed)
+unsigned* ticket_slot() {
+  static unsigned* base[64] = {};
+  static std::atomic<unsigned> next{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev] && hipGetSymbolAddress((void**)&base[dev], HIP_SYMBOL(fv_bn_tickets)) != hipSuccess) return nullptr;
+  return base[dev] + (next.fetch_add(1) % TK_SLOTS) * TK_WORDS;
+}
+
 // scratch: room for max(ceil(nrec / FOLDR), ceil(256 / (C / 16)) + 1) x NV x C doubles (fp32
 // records and rows beyond FOLD2 fold in two launches: chunk partials, then the partial rows)
 template <typename T, int NV, int MODE>
@@ -375,12 +435,9 @@ int launch_fold(const FoldArgs& a, hipStream_t s, const char* what, double* scra
     if (nch > a.nrec / 64) nch = a.nrec / 64;
     const int rows = (a.nrec + nch - 1) / nch;
     nch = (a.nrec + rows - 1) / rows;
-    hipLaunchKernelGGL((fold16_part_kernel<NV>), dim3(ng, nch), dim3(256), 0, s, a, rows, scratch);
-    FoldArgs b = a;
-    b.src = scratch;
-    b.nrec = nch;
-    b.rstride = (long)NV * a.C;
-    hipLaunchKernelGGL((fold1_kernel<double, NV, MODE>), dim3(a.C), dim3(FOLDT), 0, s, b);
+    unsigned* tk = ticket_slot();
+    FV_REQUIRE(tk && ng <= TK_WORDS, "BN fold: no ticket slot");
+    hipLaunchKernelGGL((fold16_part_kernel<NV, MODE>), dim3(ng, nch), dim3(256), 0, s, a, rows, scratch, tk);
     return fv_check_launch(what);
   }
   if (a.nrec <= FOLD2) {

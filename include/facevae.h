@@ -395,6 +395,9 @@ int fv_spectral_norm_fwd_batch(const void* table_dev, int nlayers, const int* nb
 
 /* ---------------------------------------------------------------- batch norm ---- */
 size_t fv_bn_ws_bytes(int c);
+/* Conv-record folds (fv_bn_*_partials, fv_bn_bwd_from_records) run in ONE launch: level 1
+ * chunk partials + level 2 by each 16-channel group's last-arriving block (bn.hip
+ * fold16_part_kernel: sc1 stores, arrival tickets in a per-device pool; bit-reproducible). */
 /* (count, sum, centred-M2) conv partials -> stats [3][c] doubles (count, sum, sumsq) */
 int fv_bn_stats_from_partials(const float* partials, int nblocks, int block_pixels,
                               long total_pixels, int c, double* stats, void* ws, void* stream);
@@ -410,8 +413,7 @@ int fv_bn_finalize(const double* stats, int c, const float* gamma, const float* 
                    long long* num_batches_tracked, float* save_mean, float* save_invstd, float* scale,
                    float* shift, void* stream);
 /* single-process training forms (no SyncBN exchange between the statistics and finalize):
- * statistics + finalize (+ num_batches_tracked += 1) in two launches (one when the conv wrote
- * <= 1024 records) */
+ * statistics + finalize (+ num_batches_tracked += 1) in one launch (two for a tensor) */
 int fv_bn_stats_finalize_partials(const float* partials, int nblocks, int block_pixels, long total_pixels,
                                   int c, const float* gamma, const float* beta, float eps, float momentum,
                                   float* running_mean, float* running_var, long long* num_batches_tracked,
