@@ -8,20 +8,12 @@ loss, and the buffer sync (C3).  The model here is plain torch (CPU); the bucket
 hooks, flat buffers and averaging are the product code.
 """
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 class _Net(torch.nn.Module):
@@ -35,10 +27,10 @@ class _Net(torch.nn.Module):
         return self.b(torch.tanh(self.a(x)))
 
 
-def _worker(rank, world, port, bucket_mb, q, grad_dtype=None):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, store_path, bucket_mb, q, grad_dtype=None):
+    # file rendezvous: no TCP port to race for (a probed free port can be taken before the
+    # ranks bind it when the container is busy)
+    dist.init_process_group("gloo", init_method="file://" + store_path, rank=rank, world_size=world)
     try:
         import fvamd  # noqa: F401
         from facevae_amd import distributed as D
@@ -69,8 +61,10 @@ def _worker(rank, world, port, bucket_mb, q, grad_dtype=None):
 def _run(world, bucket_mb, grad_dtype=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q, grad_dtype)) for r in range(world)]
+    store = tempfile.NamedTemporaryFile(prefix="fv_gloo_", delete=False)
+    store.close()
+    os.unlink(store.name)
+    ps = [ctx.Process(target=_worker, args=(r, world, store.name, bucket_mb, q, grad_dtype)) for r in range(world)]
     for p in ps:
         p.start()
     out = [q.get(timeout=120) for _ in ps]
