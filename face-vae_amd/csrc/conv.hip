@@ -1673,21 +1673,22 @@ conv_halo_fwd(ConvArgs a, unsigned x_bytes) {
 //  * persistent blocks (2 per CU): the 64 x 224 weight image is staged ONCE per block, the
 //    halos of the next two tiles are in flight (3-buffer ring) while the current one computes;
 //  * a minimal epilogue (bias preloaded, NHWC bf16 stores widened to 16 B), so no load in the
-//    loop waits behind the halo DMA; ONE BN (sum, sum^2) record per 256-pixel tile (the 8
-//    waves' partials summed through LDS after the tile's barrier: 4.2 MB of records instead
-//    of 33.5 MB of scattered 32-B stores).
+//    loop waits behind the halo DMA; ONE BN (sum, sum^2) record per BLOCK (r6): every lane
+//    keeps the running sums of its 16 channels over all the block's tiles (plain adds), reduced
+//    across lanes and waves once at the end -- the per-tile record (32 DPP row sums per wave
+//    and tile, an LDS exchange and a record store) made the in_conv forward 27 us slower than
+//    the same kernel without statistics (104 vs 77 us in the replayed step).  Block b owns tiles
+//    b, b + G, ... (C74 tiles per block, c74_grid), so record b covers exactly those pixels.
 // Tile: 4 rows x 64 columns x 64 co; wave w owns pixels [32w, 32w + 32) x all 64 co.
 // ----------------------------------------------------------------------------------------
 constexpr int C74_TR = 4, C74_HW = 71, C74_HR = C74_TR + 6;          // halo row: 64 + 6 + 1 (zero) px
 constexpr int C74_K = 224, C74_WCOL = C74_K / 8;                     // 16-B chunks (k columns) per weight row
 constexpr int C74_WQ = 64 * C74_WCOL / 64;                           // 1-KB weight pieces (28)
 constexpr int C74_HQ = (C74_HR * C74_HW + 63) / 64;                  // 1-KB halo pieces (16 B / px)
-__global__ void __launch_bounds__(512, 4)
+__global__ void __launch_bounds__(512, 2)
 conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
   constexpr int WB = C74_WQ * 1024, HB = C74_HQ * 1024, NHB = 3;   // 3-deep halo ring
-  constexpr int SB = 8 * 2 * 64 * 4;                                 // per-wave BN partials of a tile
-  __shared__ __attribute__((aligned(1024))) char smem[WB + NHB * HB + 2 * SB];
-  float* const sred = reinterpret_cast<float*>(smem + WB + NHB * HB);   // [2 tiles][wave][2][64]
+  __shared__ __attribute__((aligned(1024))) char smem[WB + NHB * HB];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, g = lane >> 4;
@@ -1735,17 +1736,14 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
     const int loc = wave * 32 + m * 16 + li;
     hbase[m] = (loc >> 6) * C74_HW + (loc & 63);
   }
-  int buf = 0, it = 0;
-  for (; tile < ntiles; tile += gridDim.x, ++it) {
-    // BN record of the previous tile: its 8 waves' partials (published by the last barrier),
-    // summed in wave order by 128 threads -> one [2][64] record per tile (256 pixels)
-    if (a.stats && it > 0 && tid < 128) {
-      const float* sp = sred + ((it - 1) & 1) * (SB / 4) + tid;
-      float v = 0.f;
+  // BN running sums of this lane's channels nn * 16 + g * 4 + i over the block's pixels
+  float bs[4][4], bq[4][4];
 #pragma unroll
-      for (int w = 0; w < 8; ++w) v += sp[w * 128];
-      if (tile - (int)gridDim.x < a.nrec) a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
-    }
+  for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs[nn][i] = bq[nn][i] = 0.f;
+  int buf = 0;
+  for (; tile < ntiles; tile += gridDim.x) {
     // the halo two tiles ahead goes into the buffer the previous tile released at its barrier
     const int ahead = tile + 2 * gridDim.x;
     if (ahead < ntiles) issue_halo(ahead, buf == 0 ? 2 : buf - 1);
@@ -1782,22 +1780,14 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[nn][m][i] += bv[nn][i];
     if (a.stats) {
-      float* sw = sred + (it & 1) * (SB / 4) + wave * 128;
 #pragma unroll
-      for (int nn = 0; nn < 4; ++nn) {
-        float sv[4], qv[4];
+      for (int nn = 0; nn < 4; ++nn)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v0 = acc[nn][0][i], v1 = acc[nn][1][i];
-          sv[i] = row16_sum(v0 + v1);
-          qv[i] = row16_sum(v0 * v0 + v1 * v1);
+          bs[nn][i] += v0 + v1;
+          bq[nn][i] += v0 * v0 + v1 * v1;
         }
-        const int ii = li & 3;
-        const float s01 = ii & 1 ? sv[1] : sv[0], s23 = ii & 1 ? sv[3] : sv[2];
-        const float q01 = ii & 1 ? qv[1] : qv[0], q23 = ii & 1 ? qv[3] : qv[2];
-        const float val = li < 4 ? (ii & 2 ? s23 : s01) : (ii & 2 ? q23 : q01);
-        if (li < 8) sw[(li >> 2) * 64 + nn * 16 + g * 4 + ii] = val;
-      }
     }
     // 16-B stores (the guide's T21 widening, 16-lane rows): lane (li, g) holds channels
     // nt * 16 + g * 4 .. + 3 of every n-tile nt; one v_permlane16_swap per dword of an n-tile
@@ -1827,20 +1817,34 @@ conv7c4_fwd(ConvArgs a, unsigned x_bytes, int ntiles) {
     // (raw barrier: __syncthreads() would also drain the stores)
     {
       const int dpieces = ahead < ntiles ? (wave + 8 < C74_HQ ? 2 : 1) : 0;
-      const int recst = (a.stats && it > 0 && wave < 2) ? 1 : 0;
-      wait_vm_dyn(8 + dpieces + recst);
+      wait_vm_dyn(8 + dpieces);
     }
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     buf = buf == 2 ? 0 : buf + 1;
   }
-  if (a.stats && it > 0 && tid < 128) {
-    const float* sp = sred + ((it - 1) & 1) * (SB / 4) + tid;
-    float v = 0.f;
+  if (a.stats) {
+    // the block's record: lane sums over li (row16_sum), then the 8 waves in order through LDS
+    // (the halo ring is free: every wave passed the last tile's barrier)
+    float* sw = reinterpret_cast<float*>(smem + WB);
 #pragma unroll
-    for (int w = 0; w < 8; ++w) v += sp[w * 128];
-    if (tile - (int)gridDim.x < a.nrec) a.stats[(long)(tile - (int)gridDim.x) * 128 + tid] = v;
+    for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float sv = row16_sum(bs[nn][i]), qv = row16_sum(bq[nn][i]);
+        if (li == 0) {
+          sw[wave * 128 + nn * 16 + g * 4 + i] = sv;
+          sw[wave * 128 + 64 + nn * 16 + g * 4 + i] = qv;
+        }
+      }
+    __syncthreads();
+    if (tid < 128 && (int)blockIdx.x < a.nrec) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += sw[w * 128 + tid];
+      a.stats[(long)blockIdx.x * 128 + tid] = v;
+    }
   }
 }
 
@@ -4973,6 +4977,15 @@ static bool use_c74(const fv_conv_desc* fd) {
   return halo_tr(fd) == 4 && fd->cin == 8 && fd->cin_valid <= 4 && fd->cout == 64 && fd->ldy == 64 &&
          !fd->epi_sigmoid && !fd->out_nchw_f32;
 }
+// conv7c4_fwd's persistent grid: G blocks (<= 512, two per CU) of c74_tiles_per_block tiles
+// each (block b: tiles b, b + G, ...); G = the BN record count (one record per block)
+static int c74_tiles_per_block(const fv_conv_desc* d) {
+  const int ntiles = d->n * (d->h / C74_TR) * (d->w / 64);
+  return fv_cdiv(ntiles, 512);
+}
+static int c74_grid(const fv_conv_desc* d) {
+  return fv_cdiv(d->n * (d->h / C74_TR) * (d->w / 64), c74_tiles_per_block(d));
+}
 // the launch of forward-conv descriptor fd runs conv3c64_fwd (64 input channels, sliding band,
 // weights in registers; plain [co][Kpad] weights)
 static bool use_c64(const fv_conv_desc* fd) {
@@ -4999,7 +5012,7 @@ static int stats_record_pixels(const fv_conv_desc* d) {
   if (use_c7n(d)) return 64;
   if (use_upband(d)) return UPB_G * 2 * 32;                  // (block, 4 iterations, phase)
   if (use_subpix_halo(d)) return 128;                         // (tile, wave row, phase): RM * 16                                  // one 64-pixel row segment
-  if (use_c74(d)) return C74_TR * 64;                         // one record per tile
+  if (use_c74(d)) return c74_tiles_per_block(d) * C74_TR * 64;   // one record per block
   if (use_c64(d)) return C64_G * 64;                          // 8 iterations x one wave's row
   if (halo_tr(d)) return plan_tile(d).bm / 8;                 // 8 waves stacked over pixels
   const FwdTile t = plan_tile(d);
@@ -5302,7 +5315,8 @@ static int conv_run(const fv_conv_desc* d, const void* x, const void* wk, const 
     FV_REQUIRE(!res, "packed 7x7 conv: no residual");
     const int ntiles = d->n * (d->h / C74_TR) * (d->w / 64);
     const unsigned xb = (unsigned)((long)d->n * d->h * d->w * d->cin * 2);
-    hipLaunchKernelGGL(conv7c4_fwd, dim3(std::min(ntiles, 512)), dim3(512), 0, s, a, xb, ntiles);
+    FV_REQUIRE(!a.stats || a.nrec == c74_grid(d), "packed 7x7 conv: %d BN records for %d blocks", a.nrec, c74_grid(d));
+    hipLaunchKernelGGL(conv7c4_fwd, dim3(c74_grid(d)), dim3(512), 0, s, a, xb, ntiles);
     return fv_check_launch("conv2d_fwd_c74");
   }
   if (const int tr = halo_tr(d)) {
