@@ -113,12 +113,12 @@ def cpu_baseline(args, cfg, B, gpu_first=None):
                       f"the cgroup quota; os.cpu_count() = {ncpu} is the whole machine)"}, parity
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r5_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r6_pmc.json")
 
 
 def pmc_counters(cfg, B, dtype, fam, avg_ms):
     """Counter figures of the dominant kernel from the committed PMC passes (tools/gpu.sh pmc
-    -> profiles/r5_pmc.json, tools/pmc_collect.py): HBM bytes per launch ((2 x FETCH_SIZE +
+    -> profiles/r6_pmc.json, tools/pmc_collect.py): HBM bytes per launch ((2 x FETCH_SIZE +
     WRITE_SIZE) KiB, the gfx950 correction of MI355X_MICROARCH.md), the MFMA busy fraction
     (SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)) and the effective clock.
     Measured on the default 256x256, B=32 bf16 configuration only; others report null."""
@@ -128,7 +128,7 @@ def pmc_counters(cfg, B, dtype, fam, avg_ms):
     dom = (d.get("dominant") or {}).get(fam)
     if not dom:
         return {}
-    out = {"pmc_source": "profiles/r5_pmc.json (" + dom["kernel"] + ")"}
+    out = {"pmc_source": "profiles/r6_pmc.json (" + dom["kernel"] + ")"}
     if "hbm_bytes_per_launch" in dom:
         t = dom["hbm_bytes_per_launch"]
         act = B * cfg.latent_hw ** 2 * cfg.up_seq[0] * 2          # one bf16 activation of the res stack
