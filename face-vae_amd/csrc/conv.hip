@@ -4726,6 +4726,13 @@ static bool use_upw(const fv_conv_desc* d) {
   return on && d->dtype == FV_BF16 && d->upsample && d->ksize == 3 && !d->pro_act && d->cin % 64 == 0 &&
          d->cin_valid == d->cin && d->cout % 64 == 0 && d->w % 64 == 0 && d->h % 4 == 0;
 }
+// an integer tuning knob from the environment (A/B runs), read per call
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+
 WgPlan plan_wgrad(const fv_conv_desc* d) {
   WgPlan p{};
   const int K = d->ksize * d->ksize * d->cin;
@@ -4737,10 +4744,12 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
                    P * pad_pow2_8(d->cout) * 2 < (1L << 31);
   p.v2 = fits && !d->pro_act;
   // out_conv 7x7 64 -> <= 4 (v2 == 3): blocks = (image, 64-column strip, row segment), about
-  // 4 per CU; slab [block][32 (r, co)][448 (s, ci)]
+  // 2 per CU (r6: 1024 -> 512 blocks halves the 58.7 MB of slabs; out_conv weight gradient
+  // 98.4 -> 90.4 us + reduce 15 -> 10.6 us, step -0.03 ms; 256 blocks: 114 us;
+  // profiles/r6/r6k_ab_wgrad_blocks.log); slab [block][32 (r, co)][448 (s, ci)]
   if (p.v2 && use_c7w(d)) {
     const int strips = d->w / 64;
-    int nseg = fv_cdiv(1024, d->n * strips);
+    int nseg = fv_cdiv(env_int("FV_C7W_BLOCKS", 512), d->n * strips);
     if (nseg > fv_cdiv(d->h, 8)) nseg = fv_cdiv(d->h, 8);
     if (nseg < 1) nseg = 1;
     p.v2 = 3;
@@ -4844,7 +4853,8 @@ WgPlan plan_wgrad(const fv_conv_desc* d) {
   p.ntc = fv_cdiv(d->cout, p.bc);
   p.nsteps = fv_cdiv(P, p.px);
   const int ntile = p.ntk * p.ntc;
-  int ns = p.v2 ? (256 + ntile / 2) / ntile : 768 / ntile;
+  const int wblk = env_int("FV_WG2_BLOCKS", 256);   // (128: 1x1 weight gradients 45 / 33 -> 67 / 40 us)
+  int ns = p.v2 ? (wblk + ntile / 2) / ntile : 768 / ntile;
   if (ns < 1) ns = 1;
   if (ns > p.nsteps) ns = p.nsteps;
   p.sps = fv_cdiv(p.nsteps, ns);
