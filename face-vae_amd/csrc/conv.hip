@@ -6433,17 +6433,31 @@ struct Wg8Args {
 
 __device__ __forceinline__ int swz8x(int px) { return (((px >> 2) & 1) | (((px >> 4) & 1) << 1)) << 1; }   // 64-B rows
 __device__ __forceinline__ int swz8d(int px) { return (((px >> 1) & 3) | (((px >> 4) & 1) << 2)) << 1; }   // 128-B rows
+// 32-B rows (CIB = 32): a half-wave's tr_b8 pixels are two runs of 8, 16 apart, which alias mod
+// 8 pixels (256 B): the block pair flips with pixel bit 4
+__device__ __forceinline__ int swz8x32(int px) { return ((px >> 4) & 1) << 1; }
+template <int CIB>
+__device__ __forceinline__ int swz8xc(int px) {
+  if constexpr (CIB == 64) return swz8x(px);
+  else return swz8x32(px);
+}
 
 __device__ __forceinline__ v2i_t tr8(const char* p) {
   return __builtin_amdgcn_ds_read_tr8_b64_v2i32((FV_LDS v2i_t*)(FV_LDS char*)(p));
 }
 
-template <int AHEAD>
+// CIB (r6): input channels per block.  64: a wave owns 64 co x 18 k-tiles =
+// 288 accumulators, more than the 256 AGPRs, so the compiler rotates accumulator tiles through
+// VGPRs (~860 v_accvgpr moves per 72 MFMAs).  32: the block is 128 co x 9 taps x 32 ci and a
+// wave owns 64 co x 9 k-tiles = 144 accumulators (no rotation), at twice the blocks (dy rows
+// read by twice as many ci tiles, through the XCD's L2) and 13 fragment reads per 9 MFMAs
+// instead of 22 per 18.
+template <int AHEAD, int CIB = 64>
 __global__ void __launch_bounds__(256, 1)
 conv3_wgrad_fp8(Wg8Args a) {
   constexpr int BC = 128, NSD = AHEAD + 1, NSX = 2 * AHEAD + 4;
   constexpr int DYR = 64 * BC, DYB = 2 * DYR;         // 8 KB per dy row, 16 KB per group
-  constexpr int XQ = 5, XB = XQ * 1024;               // x row: 66 px x 64 B = 4224 B -> 5 pieces
+  constexpr int XQ = (66 * CIB + 1023) / 1024, XB = XQ * 1024;   // x row: 66 px x CIB B (5 / 3 pieces)
   constexpr int NPC = 16 + 2 * XQ;                    // pieces per group (26)
   __shared__ __attribute__((aligned(1024))) char smem[NSD * DYB + NSX * XB];
   char* const dyr = smem;
@@ -6460,7 +6474,7 @@ conv3_wgrad_fp8(Wg8Args a) {
   const int tile = blk % ntile, tc = tile % a.nct, tci = tile / a.nct;
   const int split = blk / ntile;
   const int seg = split % a.nseg, strip = (split / a.nseg) % strips, n = split / (a.nseg * strips);
-  const int co0 = tc * BC, w0 = strip * 64, ci0 = tci * 64;
+  const int co0 = tc * BC, w0 = strip * 64, ci0 = tci * CIB;
   const int h0 = seg * a.rows, h1 = min(a.H, h0 + a.rows);
   const int nstep = (h1 - h0) >> 1;                   // row pairs (the host keeps segments even)
   constexpr int NWV = 4, JP = (NPC + NWV - 1) / NWV;  // 4 waves; <= 7 pieces per wave and group
@@ -6482,9 +6496,9 @@ conv3_wgrad_fp8(Wg8Args a) {
       poff[j] = (unsigned)(px * a.Cout + co0 + ((kk ^ (swz8d(px) >> 1)) << 4));
     } else if (q < NPC) {
       const int o = ((q - 16) % XQ) * 1024 + lane * 16;
-      const int px = o >> 6, kk = (o >> 4) & 3;
+      const int px = o / CIB, kk = (o >> 4) & (CIB / 16 - 1);
       const int iw = w0 - 1 + px;
-      if (px < 66 && iw >= 0 && iw < a.W) poff[j] = (unsigned)(iw * a.Cin + ci0 + ((kk ^ (swz8x(px) >> 1)) << 4));
+      if (px < 66 && iw >= 0 && iw < a.W) poff[j] = (unsigned)(iw * a.Cin + ci0 + ((kk ^ (swz8xc<CIB>(px) >> 1)) << 4));
     }
   }
   auto xslot = [&](int y) { return (y - h0 + 1) % NSX; };
@@ -6520,7 +6534,8 @@ conv3_wgrad_fp8(Wg8Args a) {
     if (i < nstep) issue_group(i);
 
   with_const<0, 2>(wk, [&](auto wkc) {
-    constexpr int WK = decltype(wkc)::value, NK = 18;   // k-tiles NK WK .. NK WK + 17 of 36
+    constexpr int KTT = CIB / 16;                       // 16-ci k-tiles per tap
+    constexpr int WK = decltype(wkc)::value, NK = 9 * KTT / 2;   // k-tiles NK WK .. NK WK + NK - 1
     f32x4 acc[4][NK];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -6553,12 +6568,12 @@ conv3_wgrad_fp8(Wg8Args a) {
       }
       // x fragment of k-tile j: tap (r, s), 16-ci block u; rows h - 1 + r (k < 64) and h + r
       auto xfrag = [&](int j) {
-        const int kt = NK * WK + j, tap = kt >> 2, u = kt & 3, r = tap / 3, s3 = tap - (tap / 3) * 3;
+        const int kt = NK * WK + j, tap = kt / KTT, u = kt % KTT, r = tap / 3, s3 = tap - (tap / 3) * 3;
         const char* xa = xr_ + ((2 * i + r) % NSX) * XB;
         const char* xb = xr_ + ((2 * i + 1 + r) % NSX) * XB;
         const int cb = 2 * u + (li & 1);
         const int p0 = plv + s3, p1 = plv + 8 + s3;
-        const int o0 = p0 * 64 + ((cb ^ swz8x(p0)) << 3), o1 = p1 * 64 + ((cb ^ swz8x(p1)) << 3);
+        const int o0 = p0 * CIB + ((cb ^ swz8xc<CIB>(p0)) << 3), o1 = p1 * CIB + ((cb ^ swz8xc<CIB>(p1)) << 3);
         const v2i_t r0 = tr8(xa + o0), r1 = tr8(xa + o1), r2 = tr8(xb + o0), r3 = tr8(xb + o1);
         return v8i{r0[0], r0[1], r1[0], r1[1], r2[0], r2[1], r3[0], r3[1]};
       };
@@ -6582,8 +6597,8 @@ conv3_wgrad_fp8(Wg8Args a) {
     float* sl = a.slab + (long)split * a.Cout * KW;
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
-      const int kt = NK * WK + j, tap = kt >> 2;
-      const int kcol = tap * a.Cin + ci0 + (kt & 3) * 16 + li;
+      const int kt = NK * WK + j, tap = kt / KTT;
+      const int kcol = tap * a.Cin + ci0 + (kt % KTT) * 16 + li;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -6824,10 +6839,18 @@ int fv_conv2d_bwd_weight_fp8(const fv_conv_desc* d, const uint8_t* x8, const flo
   Wg8Args a{};
   a.x8 = x8; a.dy8 = dy8; a.dqx = x_dq; a.dqdy = dy_dq; a.slab = slab; a.bslab = bias_slab;
   a.H = d->h; a.W = d->w; a.Cin = d->cin; a.Cout = d->cout;
-  a.nseg = t.nsteps; a.rows = t.sps; a.nct = t.ntc; a.nci = t.ntk;
+  a.nseg = t.nsteps; a.rows = t.sps; a.nct = t.ntc;
   a.xbytes = (unsigned)(P * d->cin);
   a.dybytes = (unsigned)(P * d->cout);
-  hipLaunchKernelGGL(conv3_wgrad_fp8<3>, dim3(t.ntc * t.ntk * t.nsplit), dim3(256), 0, (hipStream_t)stream, a);
+  // 32-channel input tiles (144 accumulators per wave) unless FV_FP8_WG_CIB=64 (A/B)
+  const char* e = getenv("FV_FP8_WG_CIB");
+  if (e && atoi(e) == 64) {
+    a.nci = d->cin / 64;
+    hipLaunchKernelGGL((conv3_wgrad_fp8<3, 64>), dim3(t.ntc * a.nci * t.nsplit), dim3(256), 0, (hipStream_t)stream, a);
+  } else {
+    a.nci = d->cin / 32;
+    hipLaunchKernelGGL((conv3_wgrad_fp8<3, 32>), dim3(t.ntc * a.nci * t.nsplit), dim3(256), 0, (hipStream_t)stream, a);
+  }
   return fv_check_launch("conv2d_bwd_weight_fp8");
 }
 
