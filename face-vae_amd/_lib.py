@@ -98,6 +98,7 @@ _SIGS = {
     "fv_fp8_site_bytes": (c_size_t, []),
     "fv_quantize_fp8_site": (c_int, [c_int, P, c_long, P, P, c_int, P, P]),
     "fv_conv2d_fwd_fp8_site": (c_int, [D, P, P, P, P, P, P, P, P, P]),
+    "fv_conv2d_fwd_fp8_site_sr": (c_int, [D, P, P, P, P, P, P, P, P, P]),
     "fv_conv2d_bwd_data_fp8_site": (c_int, [D, P, P, P, P, P, P]),
     "fv_fp8_set_deferred_roll": (c_int, [c_int]),
     "fv_fp8_amax": (c_int, [c_int, P, c_long, P, P, P]),

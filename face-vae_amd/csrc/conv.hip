@@ -6624,8 +6624,14 @@ bool fp8_ok(const fv_conv_desc* d) {
 
 int conv_fp8_run(const fv_conv_desc* d, int cin, int cout, const uint8_t* x8, const float* dq_x, const uint8_t* w8,
                  const float* dq_w, const float* bias, const void* res, void* y, float* stats, hipStream_t s,
-                 unsigned* roll = nullptr) {
+                 unsigned* roll = nullptr, float* sprec = nullptr) {
   ConvArgs a{};
+  // store-pass mode 1 (r6): (sum, sum of squares) of the stored, residual-added output in the
+  // staged epilogue's store loop -- the records of fv_conv2d_fwd_sr, same geometry (256-pixel
+  // tiles, one record per wave and tile: the bf16 res tile's count), so in fp8 mode the next
+  // ResBlock's bn1 statistics need no tensor_stats pass either
+  a.spm = sprec ? 1 : 0;
+  a.sprec = sprec;
   a.x = x8; a.w = w8; a.bias = bias; a.res = res; a.y = y; a.stats = stats;
   a.nrec = stats ? fv_conv2d_fp8_stats_blocks(d) : 0;
   a.dq0 = dq_x; a.dq1 = dq_w;
@@ -6797,6 +6803,23 @@ int fv_conv2d_fwd_fp8_site(const fv_conv_desc* d, const uint8_t* x8, void* site,
                       (hipStream_t)stream, g_fp8_defer_roll ? nullptr : sp);
 }
 
+int fv_conv2d_fwd_fp8_site_sr(const fv_conv_desc* d, const uint8_t* x8, void* site, const uint8_t* wk,
+                              const float* w_dq, const float* bias, const void* res, void* y, const fv_store_reduce* sr,
+                              void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fp8_ok(d), "fp8 conv: unsupported descriptor");
+  FV_REQUIRE(x8 && site && wk && w_dq && y && sr && sr->mode == 1 && sr->records, "fwd_fp8_sr: null pointer or mode != 1");
+  // the fp8 tile (128 co x 256 px, 8 waves) writes the records of the bf16 res tile (256 px,
+  // 8 waves): the geometry query must describe exactly that
+  int bp = 0;
+  FV_REQUIRE(sr_geometry(d, &bp) == (int)((long)d->n * d->h * d->w / 256 * 8) && bp == 32,
+             "fwd_fp8_sr: store-pass records unavailable for this shape");
+  unsigned* sp = (unsigned*)site;
+  return conv_fp8_run(d, d->cin, d->cout, x8, (const float*)(sp + 18), wk, w_dq, bias, res, y, nullptr,
+                      (hipStream_t)stream, g_fp8_defer_roll ? nullptr : sp, sr->records);
+}
+
 int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void* site, const uint8_t* wt,
                                 const float* wt_dq, void* dx, void* stream) {
   int st = check_desc(d);
@@ -6849,7 +6872,12 @@ int fv_conv2d_bwd_weight_fp8(const fv_conv_desc* d, const uint8_t* x8, const flo
     hipLaunchKernelGGL((conv3_wgrad_fp8<3, 64>), dim3(t.ntc * a.nci * t.nsplit), dim3(256), 0, (hipStream_t)stream, a);
   } else {
     a.nci = d->cin / 32;
-    hipLaunchKernelGGL((conv3_wgrad_fp8<3, 32>), dim3(t.ntc * a.nci * t.nsplit), dim3(256), 0, (hipStream_t)stream, a);
+    const char* ea = getenv("FV_FP8_WG_AHEAD");   // row-pair groups in flight (A/B)
+    const int ahead = ea ? atoi(ea) : 2;            // (r6: res fp8 wgrad 198.8 -> 191.8 us vs 3, step -0.05 ms)
+    const dim3 grid(t.ntc * a.nci * t.nsplit);
+    if (ahead == 2) hipLaunchKernelGGL((conv3_wgrad_fp8<2, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else if (ahead == 4) hipLaunchKernelGGL((conv3_wgrad_fp8<4, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((conv3_wgrad_fp8<3, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
   }
   return fv_check_launch("conv2d_bwd_weight_fp8");
 }

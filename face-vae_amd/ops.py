@@ -669,6 +669,9 @@ def _q8_ok(site, y, pool, bn=None):
 
 
 _Q8_ONLY = os.environ.get("FV_Q8_ONLY", "1") == "1"   # tests/test_fp8_gpu.py flips it to compare with the bf16-writing passes
+# fp8 ResBlock conv2: store-pass BN statistics of the residual-added output in the e4m3 conv's
+# epilogue (fv_conv2d_fwd_fp8_site_sr) instead of a tensor_stats pass; FV_FP8_SR=0 for A/B
+FP8_SR = os.environ.get("FV_FP8_SR", "1") == "1"
 
 
 def q8_only(cs: ConvState) -> bool:
@@ -887,17 +890,27 @@ class ResBlockFn(torch.autograd.Function):
         a2, q2 = bn_act_forward_q8(t1, r2, 0.0, blk.bn2, fp8_site(c2, "x", x.device) if cs2.fp8 else None,
                                    only8=q8_only(cs2))
         out = torch.empty_like(xb)
-        geo = sr_records(d2, False) if training and not cs2.fp8 else None
+        geo = sr_records(d2, False) if training and (not cs2.fp8 or FP8_SR) else None
         if geo is not None:
             # out = x + conv2(.) with its (sum, sum of squares) reduced in the store pass: the
             # next ResBlock's bn1 statistics without a pass over out (ResBlock2D.forward hands
-            # them on)
+            # them on); in fp8 mode the e4m3 conv's staged epilogue does the same (r6)
             part = _empty(geo[0] * 2 * C, F32, x.device)
             sr = L.StoreReduce(1, ptr(part), None, None, None, None, None, 0.0)
-            _timed("fwd", d2, lambda: call("fv_conv2d_fwd_sr", ctypes.byref(d2), ptr(a2), ptr(cs2.wk), ptr(b2),
-                                           ptr(xb), ptr(out), ctypes.byref(sr), stream()))
-            if CHECK is not None:
-                CHECK("fwd", cs2, x=a2, bias=b2, pro=None, res=xb, y=out)
+            if cs2.fp8:
+                site = fp8_site(c2, "x", x.device)
+                x8, xdq = q2 if q2 is not None else quantize_fp8_site(a2, site)
+                cs2.x8 = (x8, xdq.clone())
+                _timed("fwd", d2, lambda: call("fv_conv2d_fwd_fp8_site_sr", ctypes.byref(d2), ptr(x8), ptr(site[0]),
+                                               ptr(cs2.wk), ptr(cs2.wdq), ptr(b2), ptr(xb), ptr(out),
+                                               ctypes.byref(sr), stream()))
+                if CHECK is not None:
+                    CHECK("fwd", cs2, x=a2, bias=b2, pro=None, res=xb, y=out, q8=(x8, xdq))
+            else:
+                _timed("fwd", d2, lambda: call("fv_conv2d_fwd_sr", ctypes.byref(d2), ptr(a2), ptr(cs2.wk), ptr(b2),
+                                               ptr(xb), ptr(out), ctypes.byref(sr), stream()))
+                if CHECK is not None:
+                    CHECK("fwd", cs2, x=a2, bias=b2, pro=None, res=xb, y=out)
             blk._fv_out_rec = (part, geo[0], geo[1])
         else:
             conv_forward(cs2, a2, b2, res=xb, y=out, x8=q2)

@@ -234,6 +234,12 @@ int fv_quantize_fp8_site(int dtype_in, const void* x, long count, uint8_t* y, vo
 int fv_conv2d_fwd_fp8_site(const fv_conv_desc* d, const uint8_t* x8, void* site, const uint8_t* wk,
                            const float* w_dq, const float* bias, const void* res, void* y, float* stats,
                            void* stream);
+/* fv_conv2d_fwd_fp8_site + the store-pass reduction of fv_conv2d_fwd_sr (mode 1 only: the
+ * (sum, sum of squares) of the stored, residual-added output, in the records
+ * fv_conv2d_sr_records(d, 0, ...) sizes) */
+int fv_conv2d_fwd_fp8_site_sr(const fv_conv_desc* d, const uint8_t* x8, void* site, const uint8_t* wk,
+                              const float* w_dq, const float* bias, const void* res, void* y,
+                              const fv_store_reduce* sr, void* stream);
 int fv_conv2d_bwd_data_fp8_site(const fv_conv_desc* d, const uint8_t* dy8, void* site, const uint8_t* wt,
                                 const float* wt_dq, void* dx, void* stream);
 /* Data-parallel global scaling (BASELINE config C5 at N > 1; the fp8 counterpart of SyncBN's

@@ -270,6 +270,44 @@ def test_resblock_fp8_only8_matches_bf16_copies():
     assert seen_on[-2:] == [True, True] and not any(seen_off)
 
 
+def test_resblock_fp8_store_pass_statistics():
+    """fp8 ResBlock conv2 with the store-pass reduction in the e4m3 conv's epilogue
+    (fv_conv2d_fwd_fp8_site_sr): the output equals the run without it bit for bit, and the
+    records it hands to the next ResBlock's bn1 sum to the statistics of the stored output."""
+    from facevae_amd.modules import ResBlock2D
+    N, C, H, W = 2, 256, 8, 64
+    g = torch.Generator().manual_seed(43)
+    x0 = torch.randn(N, C, H, W, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    torch.manual_seed(9)
+    blk = ResBlock2D(C, True).cuda().train().set_compute_dtype(torch.float8_e4m3fn)
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+
+    def run(sr):
+        blk.load_state_dict(sd)
+        for m in (blk, blk.conv1, blk.conv2):
+            m.__dict__.pop("_fv_fp8_sites", None)
+            m.__dict__.pop("_fv_fp8_pending", None)
+        ops.FP8_SR = sr
+        try:
+            for _ in range(2):                        # step 1 seeds the delayed-scaling sites
+                out = blk(x0.clone())
+            torch.cuda.synchronize()
+            return out.detach().clone(), getattr(out, "_fv_bnrec", None)
+        finally:
+            ops.FP8_SR = True
+
+    o_on, rec = run(True)
+    o_off, rec_off = run(False)
+    assert torch.equal(o_on, o_off)
+    assert rec is not None and rec_off is None
+    part, nrec, bp = rec[0], rec[1], rec[2]
+    assert nrec * bp == N * H * W
+    r = part.view(nrec, 2, C).double().sum(0).cpu()
+    y = o_on.double().permute(1, 0, 2, 3).reshape(C, -1).cpu()
+    assert ((r[0] - y.sum(1)).abs() / y.abs().sum(1)).max() < 1e-5
+    assert ((r[1] - (y * y).sum(1)).abs() / (y * y).sum(1)).max() < 1e-5
+
+
 @pytest.mark.parametrize("two_consumers", [False, True])
 def test_resblock_fp8_handoff_checks_the_gradient_tensor(two_consumers):
     """the next ResBlock's bn1 backward leaves an e4m3 copy of its output for this
