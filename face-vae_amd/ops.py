@@ -829,9 +829,14 @@ class ConvBNActFn(torch.autograd.Function):
         blk, cs, r = ctx.blk, ctx.cs, ctx.r
         dz = grad_in(dz, y.dtype)
         recs = ctx.holder.get("recs") if ctx.holder["nuse"] == 1 else None
-        dy, dg, dbt = bn_act_backward(dz, y, blk.bn, r, blk.slope, blk.pool, ctx.comm, recs=recs)
+        # fp8 conv (Generator.in_conv): the BN backward apply writes the e4m3 copy of dy its data
+        # and weight gradients consume (no quantize pass over dy; r6)
+        q8 = fp8_site(cs.conv, "dy", y.device) if cs.fp8 and not blk.pool else None
+        out = bn_act_backward(dz, y, blk.bn, r, blk.slope, blk.pool, ctx.comm, recs=recs, q8=q8)
+        dy, dg, dbt = out[:3]
         dxb, dw, db, recs_in = conv_backward(cs, xb, dy, y.shape[1], need_dx=ctx.needs_input_grad[0],
-                                             bnred=_bnred_of(ctx.src), want_recs=True)
+                                             bnred=_bnred_of(ctx.src), want_recs=True,
+                                             dy8=out[3] if q8 is not None else None)
         if ctx.src is not None:
             ctx.src["recs"] = recs_in
         dx = from_nhwc(dxb, x) if dxb is not None else None
