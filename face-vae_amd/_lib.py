@@ -107,6 +107,7 @@ _SIGS = {
     "fv_fp8_sites_roll": (c_int, [c_int, P, P, P]),
     "fv_conv2d_wgrad_fp8_supported": (c_int, [D]),
     "fv_conv2d_bwd_weight_fp8": (c_int, [D, P, P, P, P, P, P, P]),
+    "fv_conv2d_wgrad_fp8_reduce": (c_int, [D, P, P, P, P, P]),
     "fv_conv2d_fp8_stats_blocks": (c_int, [D]),
     "fv_conv2d_fp8_stats_block_pixels": (c_int, [D]),
     "fv_fp8_mfma_probe": (c_int, [P, P, P, P]),

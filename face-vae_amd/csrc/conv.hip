@@ -6428,6 +6428,7 @@ struct Wg8Args {
   float* slab;
   float* bslab;
   int H, W, Cin, Cout, nseg, rows, nct, nci;
+  int N, ipb;            // images, images per split (the block walks them in turn, one slab)
   unsigned xbytes, dybytes;
 };
 
@@ -6473,7 +6474,8 @@ conv3_wgrad_fp8(Wg8Args a) {
   const int ntile = a.nct * a.nci;
   const int tile = blk % ntile, tc = tile % a.nct, tci = tile / a.nct;
   const int split = blk / ntile;
-  const int seg = split % a.nseg, strip = (split / a.nseg) % strips, n = split / (a.nseg * strips);
+  const int seg = split % a.nseg, strip = (split / a.nseg) % strips, ng = split / (a.nseg * strips);
+  int n = ng * a.ipb;                                 // the image being walked (issue_* read it)
   const int co0 = tc * BC, w0 = strip * 64, ci0 = tci * CIB;
   const int h0 = seg * a.rows, h1 = min(a.H, h0 + a.rows);
   const int nstep = (h1 - h0) >> 1;                   // row pairs (the host keeps segments even)
@@ -6503,11 +6505,15 @@ conv3_wgrad_fp8(Wg8Args a) {
   }
   auto xslot = [&](int y) { return (y - h0 + 1) % NSX; };
   auto issue_x = [&](int y, int j, int q) {             // x piece (q - 16) % 5 of row y
+    // (the resource is rebuilt from the kernel argument here: called from inside the image
+    // loop the captured one was treated as divergent and put in VGPRs)
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.x8), 0, (int)a.xbytes, 0x00020000);
     const bool rok = y >= 0 && y < a.H;
     dma16s(xr, sbase + NSD * DYB + xslot(y) * XB + ((q - 16) % XQ) * 1024, rok ? poff[j] : 0x80000000u,
            rok ? (unsigned)(((n * a.H + y) * a.W) * a.Cin) : 0u);
   };
   auto issue_group = [&](int i) {
+    const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.dy8), 0, (int)a.dybytes, 0x00020000);
     const int h = h0 + 2 * i;
 #pragma unroll
     for (int j = 0; j < JP; ++j) {
@@ -6523,75 +6529,96 @@ conv3_wgrad_fp8(Wg8Args a) {
       }
     }
   };
-  // prologue x rows h0 - 1 (as row 0 of a group) and h0 (as row 1)
+  // prologue of one image: x rows h0 - 1 (as row 0 of a group) and h0 (as row 1), the first
+  // AHEAD groups
+  auto prologue = [&]() {
 #pragma unroll
-  for (int j = 0; j < JP; ++j) {
-    const int q = wave + NWV * j;
-    if (j < npw && q >= 16) issue_x(h0 - 1 + (q - 16) / XQ, j, q);
-  }
+    for (int j = 0; j < JP; ++j) {
+      const int q = wave + NWV * j;
+      if (j < npw && q >= 16) issue_x(h0 - 1 + (q - 16) / XQ, j, q);
+    }
 #pragma unroll
-  for (int i = 0; i < AHEAD; ++i)
-    if (i < nstep) issue_group(i);
+    for (int i = 0; i < AHEAD; ++i)
+      if (i < nstep) issue_group(i);
+  };
+  prologue();
 
-  with_const<0, 2>(wk, [&](auto wkc) {
-    constexpr int KTT = CIB / 16;                       // 16-ci k-tiles per tap
-    constexpr int WK = decltype(wkc)::value, NK = 9 * KTT / 2;   // k-tiles NK WK .. NK WK + NK - 1
-    f32x4 acc[4][NK];
+  constexpr int KTT = CIB / 16;                         // 16-ci k-tiles per tap
+  constexpr int NK = 9 * KTT / 2;                       // k-tiles NK WK .. NK WK + NK - 1 of a wave
+  f32x4 acc[4][NK];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int j = 0; j < NK; ++j) acc[q][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // bias gradient: k-wave WK sums co tiles 2 WK, 2 WK + 1 of its four (an all-ones e4m3 B operand)
-    f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    const bool do_bias = a.bslab && tci == 0;
-    const int pl = 16 * g + (li >> 1);                  // this lane's pixel row of a tr_b8 block
-    for (int i = 0; i < nstep; ++i) {
-      const int younger = min(AHEAD - 1, nstep - 1 - i);
-      wait_vm_dyn(younger * npw);
+    for (int j = 0; j < NK; ++j) acc[q][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias gradient: k-wave WK sums co tiles 2 WK, 2 WK + 1 of its four (an all-ones e4m3 B operand)
+  f32x4 accb[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const bool do_bias = a.bslab && tci == 0;
+  const int pl = 16 * g + (li >> 1);                    // this lane's pixel row of a tr_b8 block
+  // r6: a split may hold ipb images (B = 64: half the fp32 slabs); each image restarts the
+  // rings once every wave has passed the previous image's last step (all its DMAs waited)
+  for (int im = 0; im < a.ipb; ++im) {
+    if (im > 0) {
+      if (ng * a.ipb + im >= a.N) break;
+      n = ng * a.ipb + im;
       wait_lgkm0();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (i + AHEAD < nstep) issue_group(i + AHEAD);
-      const char* d0 = dyr + (i % NSD) * DYB;
-      const char* d1 = d0 + DYR;
-      // the fragment offsets are recomputed every step (an opaque copy of the pixel row) instead
-      // of being hoisted out of the loop: 26 loop-invariant offsets would spill the accumulators
-      int plv = pl;
-      asm volatile("" : "+v"(plv));
-      v8i af[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int cb = 2 * (wc * 4 + q) + (li & 1);     // 8-byte co block of the 128-co tile
-        const int o0 = plv * BC + ((cb ^ swz8d(plv)) << 3), o1 = (plv + 8) * BC + ((cb ^ swz8d(plv + 8)) << 3);
-        const v2i_t r0 = tr8(d0 + o0), r1 = tr8(d0 + o1), r2 = tr8(d1 + o0), r3 = tr8(d1 + o1);
-        af[q] = v8i{r0[0], r0[1], r1[0], r1[1], r2[0], r2[1], r3[0], r3[1]};
-      }
-      // x fragment of k-tile j: tap (r, s), 16-ci block u; rows h - 1 + r (k < 64) and h + r
-      auto xfrag = [&](int j) {
-        const int kt = NK * WK + j, tap = kt / KTT, u = kt % KTT, r = tap / 3, s3 = tap - (tap / 3) * 3;
-        const char* xa = xr_ + ((2 * i + r) % NSX) * XB;
-        const char* xb = xr_ + ((2 * i + 1 + r) % NSX) * XB;
-        const int cb = 2 * u + (li & 1);
-        const int p0 = plv + s3, p1 = plv + 8 + s3;
-        const int o0 = p0 * CIB + ((cb ^ swz8xc<CIB>(p0)) << 3), o1 = p1 * CIB + ((cb ^ swz8xc<CIB>(p1)) << 3);
-        const v2i_t r0 = tr8(xa + o0), r1 = tr8(xa + o1), r2 = tr8(xb + o0), r3 = tr8(xb + o1);
-        return v8i{r0[0], r0[1], r1[0], r1[1], r2[0], r2[1], r3[0], r3[1]};
-      };
-      v8i bcur = xfrag(0);
-#pragma unroll
-      for (int j = 0; j < NK; ++j) {
-        v8i bnext = bcur;
-        if (j + 1 < NK) bnext = xfrag(j + 1);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q][j] = mma_f8(af[q], bcur, acc[q][j]);
-        bcur = bnext;
-      }
-      if (do_bias) {
-        const v8i ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838};
-        accb[0] = mma_f8(af[2 * WK], ones, accb[0]);
-        accb[1] = mma_f8(af[2 * WK + 1], ones, accb[1]);
-      }
+      prologue();
     }
+    with_const<0, 2>(wk, [&](auto wkc) {
+      constexpr int WK = decltype(wkc)::value;
+      for (int i = 0; i < nstep; ++i) {
+        const int younger = min(AHEAD - 1, nstep - 1 - i);
+        wait_vm_dyn(younger * npw);
+        wait_lgkm0();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (i + AHEAD < nstep) issue_group(i + AHEAD);
+        const char* d0 = dyr + (i % NSD) * DYB;
+        const char* d1 = d0 + DYR;
+        // the fragment offsets are recomputed every step (an opaque copy of the pixel row)
+        // instead of being hoisted out of the loop: 26 loop-invariant offsets would spill the
+        // accumulators
+        int plv = pl;
+        asm volatile("" : "+v"(plv));
+        v8i af[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cb = 2 * (wc * 4 + q) + (li & 1);   // 8-byte co block of the 128-co tile
+          const int o0 = plv * BC + ((cb ^ swz8d(plv)) << 3), o1 = (plv + 8) * BC + ((cb ^ swz8d(plv + 8)) << 3);
+          const v2i_t r0 = tr8(d0 + o0), r1 = tr8(d0 + o1), r2 = tr8(d1 + o0), r3 = tr8(d1 + o1);
+          af[q] = v8i{r0[0], r0[1], r1[0], r1[1], r2[0], r2[1], r3[0], r3[1]};
+        }
+        // x fragment of k-tile j: tap (r, s), 16-ci block u; rows h - 1 + r (k < 64) and h + r
+        auto xfrag = [&](int j) {
+          const int kt = NK * WK + j, tap = kt / KTT, u = kt % KTT, r = tap / 3, s3 = tap - (tap / 3) * 3;
+          const char* xa = xr_ + ((2 * i + r) % NSX) * XB;
+          const char* xb = xr_ + ((2 * i + 1 + r) % NSX) * XB;
+          const int cb = 2 * u + (li & 1);
+          const int p0 = plv + s3, p1 = plv + 8 + s3;
+          const int o0 = p0 * CIB + ((cb ^ swz8xc<CIB>(p0)) << 3), o1 = p1 * CIB + ((cb ^ swz8xc<CIB>(p1)) << 3);
+          const v2i_t r0 = tr8(xa + o0), r1 = tr8(xa + o1), r2 = tr8(xb + o0), r3 = tr8(xb + o1);
+          return v8i{r0[0], r0[1], r1[0], r1[1], r2[0], r2[1], r3[0], r3[1]};
+        };
+        v8i bcur = xfrag(0);
+#pragma unroll
+        for (int j = 0; j < NK; ++j) {
+          v8i bnext = bcur;
+          if (j + 1 < NK) bnext = xfrag(j + 1);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[q][j] = mma_f8(af[q], bcur, acc[q][j]);
+          bcur = bnext;
+        }
+        if (do_bias) {
+          const v8i ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838};
+          accb[0] = mma_f8(af[2 * WK], ones, accb[0]);
+          accb[1] = mma_f8(af[2 * WK + 1], ones, accb[1]);
+        }
+      }
+    });
+  }
+  with_const<0, 2>(wk, [&](auto wkc) {
+    constexpr int WK = decltype(wkc)::value;
     const float dq = a.dqx[0] * a.dqdy[0], dqb = a.dqdy[0];
     const long KW = 9L * a.Cin;
     float* sl = a.slab + (long)split * a.Cout * KW;
@@ -6840,6 +6867,26 @@ int fv_conv2d_bwd_data_fp8(const fv_conv_desc* d, const uint8_t* dy8, const floa
   return conv_fp8_run(d, d->cout, d->cin, dy8, dy_dq, wt, wt_dq, nullptr, nullptr, dx, nullptr, (hipStream_t)stream);
 }
 
+// images per split of the fp8 weight gradient: about 512 blocks of (128 co x 32 ci) tiles x
+// splits (B = 32 res: 1 image; B = 64: 2, half the slabs of the bf16 plan's one image per
+// split); a divisor of N.  FV_FP8_WG_IPB=k forces k (A/B).  The slabs of fv_conv2d_bwd_weight_fp8
+// are then fp8_wg_nsplit(d) (<= the bf16 plan's, so fv_conv2d_wgrad_slab_elems still sizes
+// them) and fv_conv2d_wgrad_fp8_reduce sums exactly those.
+static int fp8_wg_ipb(const fv_conv_desc* d) {
+  const WgPlan t = plan_wgrad(d);
+  const long blocks = (long)t.ntc * (d->cin / 32) * t.nsplit;
+  int ipb = (int)(blocks / 512);
+  if (const char* e = getenv("FV_FP8_WG_IPB")) ipb = atoi(e);
+  if (ipb < 1) ipb = 1;
+  if (ipb > d->n) ipb = d->n;
+  while (d->n % ipb) --ipb;
+  return ipb;
+}
+static int fp8_wg_nsplit(const fv_conv_desc* d) {
+  const WgPlan t = plan_wgrad(d);
+  return t.nsteps * (d->w / 64) * (d->n / fp8_wg_ipb(d));
+}
+
 int fv_conv2d_wgrad_fp8_supported(const fv_conv_desc* d) {
   static int off = -1;          // FV_FP8_WGRAD=0: the bf16 weight gradient in fp8 mode (A/B)
   if (off < 0) {
@@ -6849,6 +6896,25 @@ int fv_conv2d_wgrad_fp8_supported(const fv_conv_desc* d) {
   if (off || check_desc(d) != FV_OK || !fp8_ok(d) || d->cin % 64 || d->cout % 128) return 0;
   const WgPlan t = plan_wgrad(d);
   return t.v2 == 5 && t.ntk == d->cin / 64 && t.sps % 2 == 0 && d->h % t.sps == 0 ? 1 : 0;
+}
+
+// the reduce of fv_conv2d_bwd_weight_fp8's slabs: wgrad_reduce_kernel over fp8_wg_nsplit(d) splits
+int fv_conv2d_wgrad_fp8_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab, float* dw_param,
+                               float* db, void* stream) {
+  int st = check_desc(d);
+  if (st) return st;
+  FV_REQUIRE(fv_conv2d_wgrad_fp8_supported(d), "fp8 weight gradient reduce: unsupported descriptor");
+  FV_REQUIRE(slab && dw_param, "null pointer");
+  FV_REQUIRE(!db || bias_slab, "db needs the bias slab");
+  const WgPlan t = plan_wgrad(d);
+  const int K = d->ksize * d->ksize * d->cin;
+  const long tot = (long)d->cout * K;
+  const int nb_main = fv_cdiv(tot, 64);
+  const int nb_bias = db ? fv_cdiv(d->cout, 64) : 0;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nb_main + nb_bias), dim3(256), 0, (hipStream_t)stream, slab,
+                     bias_slab, dw_param, db, fp8_wg_nsplit(d), t.CW, t.KW, K, d->cout, d->cin_valid,
+                     fv_ilog2(d->cin), d->ksize, nb_main, d->ksize);
+  return fv_check_launch("wgrad_reduce_fp8");
 }
 
 int fv_conv2d_bwd_weight_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_dq, const uint8_t* dy8,
@@ -6865,16 +6931,19 @@ int fv_conv2d_bwd_weight_fp8(const fv_conv_desc* d, const uint8_t* x8, const flo
   a.nseg = t.nsteps; a.rows = t.sps; a.nct = t.ntc;
   a.xbytes = (unsigned)(P * d->cin);
   a.dybytes = (unsigned)(P * d->cout);
+  a.N = d->n;
+  a.ipb = fp8_wg_ipb(d);
+  const int nsplit = fp8_wg_nsplit(d);
   // 32-channel input tiles (144 accumulators per wave) unless FV_FP8_WG_CIB=64 (A/B)
   const char* e = getenv("FV_FP8_WG_CIB");
   if (e && atoi(e) == 64) {
     a.nci = d->cin / 64;
-    hipLaunchKernelGGL((conv3_wgrad_fp8<3, 64>), dim3(t.ntc * a.nci * t.nsplit), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((conv3_wgrad_fp8<3, 64>), dim3(t.ntc * a.nci * nsplit), dim3(256), 0, (hipStream_t)stream, a);
   } else {
     a.nci = d->cin / 32;
     const char* ea = getenv("FV_FP8_WG_AHEAD");   // row-pair groups in flight (A/B)
     const int ahead = ea ? atoi(ea) : 2;            // (r6: res fp8 wgrad 198.8 -> 191.8 us vs 3, step -0.05 ms)
-    const dim3 grid(t.ntc * a.nci * t.nsplit);
+    const dim3 grid(t.ntc * a.nci * nsplit);
     if (ahead == 2) hipLaunchKernelGGL((conv3_wgrad_fp8<2, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else if (ahead == 4) hipLaunchKernelGGL((conv3_wgrad_fp8<4, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else hipLaunchKernelGGL((conv3_wgrad_fp8<3, 32>), grid, dim3(256), 0, (hipStream_t)stream, a);

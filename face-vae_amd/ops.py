@@ -436,7 +436,9 @@ def _wgrad_finish(cs: ConvState, x, dy, ldd, pro, need_db, slab, bslab, q8=None)
     dev = dy.device
     dw = torch.empty_like(cs.w)
     db = torch.empty(d.cout, dtype=F32, device=dev) if need_db else None
-    call("fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab), ptr(bslab), ptr(dw), ptr(db), stream())
+    # the fp8 weight gradient's slabs (images per split of its own) have their own reduce
+    call("fv_conv2d_wgrad_fp8_reduce" if q8 is not None else "fv_conv2d_wgrad_reduce", ctypes.byref(d), ptr(slab),
+         ptr(bslab), ptr(dw), ptr(db), stream())
     if CHECK is not None:
         CHECK("wgrad", cs, x=x, dy=dy, ldd=ldd, dw=dw, db=db, pro=pro, q8=q8)
     if cs.conv.sn and not (_sn_defer_ok(cs) and _sn_defer(cs)):

@@ -257,12 +257,17 @@ int fv_fp8_sites_inflight(int n, const uint64_t* sites, float* amax, void* strea
 int fv_fp8_sites_roll(int n, const uint64_t* sites, const float* amax, void* stream);
 /* fp8 weight gradient of a 3x3 conv (k = (tap, ci), pixel-pair MFMA K = 128) from the e4m3 copies
  * of its input (x8, dequantisation factor x_dq) and output gradient (dy8, dy_dq) -- the operands
- * the fp8 forward and data gradient consumed: slab / bias slab as fv_conv2d_bwd_weight (sizes from
- * fv_conv2d_wgrad_slab_elems, reduced by fv_conv2d_wgrad_reduce).  Supported when
+ * the fp8 forward and data gradient consumed: slab / bias slab sized by fv_conv2d_wgrad_slab_elems,
+ * reduced by fv_conv2d_wgrad_fp8_reduce.  Supported when
  * fv_conv2d_wgrad_fp8_supported(d) (128-multiple channels, the sliding-row plan). */
 int fv_conv2d_wgrad_fp8_supported(const fv_conv_desc* d);
 int fv_conv2d_bwd_weight_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_dq, const uint8_t* dy8,
                              const float* dy_dq, float* slab, float* bias_slab, void* stream);
+/* reduce of fv_conv2d_bwd_weight_fp8's slabs -> dw (param layout) [+ db]: the fp8 weight
+ * gradient splits a batch over fewer slabs than the bf16 plan (images per split chosen for
+ * about 512 blocks), so its slabs are summed by this entry, not fv_conv2d_wgrad_reduce */
+int fv_conv2d_wgrad_fp8_reduce(const fv_conv_desc* d, const float* slab, const float* bias_slab, float* dw_param,
+                               float* db, void* stream);
 /* layout probe: c[16][16] = a[16][128] . b[16][128]^T through one scaled fp8 MFMA tile */
 int fv_fp8_mfma_probe(const uint8_t* a, const uint8_t* b, float* c, void* stream);
 /* test probe: 64 lanes each read 8 bytes by ds_read_b64_tr_b8 at LDS byte offset lane_addr[lane]

@@ -479,7 +479,7 @@ def test_conv_fp8_wgrad(kind, N):
            dydq.data_ptr(), slab.data_ptr(), bslab.data_ptr(), L.stream())
     dw = torch.empty(cout, cin, 3, 3, device="cuda")
     db = torch.empty(cout, device="cuda")
-    L.call("fv_conv2d_wgrad_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(), dw.data_ptr(),
+    L.call("fv_conv2d_wgrad_fp8_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(), dw.data_ptr(),
            db.data_ptr(), L.stream())
     torch.cuda.synchronize()
     xq = deq(x8, xdq, (N, H, W, cin)).permute(0, 3, 1, 2).double().cpu()

@@ -28,7 +28,7 @@ def run_wg(d, x8, xdq, dy8, dydq):
            slab.data_ptr(), bslab.data_ptr(), L.stream())
     dw = torch.empty(d.cout, d.cin, 3, 3, device="cuda")
     db = torch.empty(d.cout, device="cuda")
-    L.call("fv_conv2d_wgrad_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(), dw.data_ptr(), db.data_ptr(),
+    L.call("fv_conv2d_wgrad_fp8_reduce", ctypes.byref(d), slab.data_ptr(), bslab.data_ptr(), dw.data_ptr(), db.data_ptr(),
            L.stream())
     torch.cuda.synchronize()
     return dw, db
