@@ -229,7 +229,8 @@ __global__ void __launch_bounds__(256) gs_scan_blocks(int* __restrict__ cnt, lon
 }
 
 // one block: bsum[0, nb) -> exclusive prefix sums, 1024 at a time with a carry
-__global__ void __launch_bounds__(256) gs_scan_totals(int* __restrict__ bsum, int nb) {
+__global__ void __launch_bounds__(256) gs_scan_totals(int* __restrict__ bsum, int nb, int* __restrict__ lst) {
+  if (threadIdx.x == 0) lst[0] = 0, lst[1] = 0;
   int carry = 0;
   for (int base = 0; base < nb; base += GS_SCAN) {
     const int i0 = base + threadIdx.x * 4;
@@ -267,46 +268,108 @@ __global__ void __launch_bounds__(256) gs_bucket_fill(const float* __restrict__ 
 }
 
 // The fill places a bucket's records in atomicAdd-rank order, which changes run to run; the
-// gather sums them in bucket order.  One thread per bucket sorts it by voxel index, so the
-// input gradient is bit-reproducible: insertion sort for the common few records, heapsort
-// (O(n log n), in place) when a degenerate grid piles many voxels onto one cell.
-__device__ __forceinline__ void gs_sift(GsRec* a, int i, int n) {
-  const GsRec x = a[i];
-  while (true) {
-    int c = 2 * i + 1;
-    if (c >= n) break;
-    if (c + 1 < n && a[c + 1].v > a[c].v) ++c;
-    if (a[c].v <= x.v) break;
-    a[i] = a[c];
-    i = c;
-  }
-  a[i] = x;
+// gather sums them in bucket order, so every bucket is put in voxel-index order and the input
+// gradient is bit-reproducible.  No lane sorts more than GS_INS records alone: one thread per
+// bucket insertion-sorts the common few and appends the larger buckets' keys to two lists
+// (wave-aggregated), which gs_bucket_sort_coop works through with whole workgroups -- a bitonic
+// sort in LDS up to GS_MID records, and above that (a degenerate or collapsed motion grid piling
+// voxels onto one cell) a stable compaction: the workgroup streams keyrank in voxel order and
+// re-emits the bucket's records in that order, O(nvox / 1024) block steps per big bucket instead
+// of one lane's O(n log n) walk through global memory.
+constexpr int GS_INS = 16, GS_MID = 2048, GS_COOP_BLOCKS = 256;
+
+__device__ __forceinline__ void gs_append(bool p, int* ctr, int* list, int val) {
+  const unsigned long long m = __ballot(p);
+  if (!m) return;
+  const int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(ctr, __popcll(m));
+  base = __shfl(base, leader, 64);
+  if (p) list[base + __popcll(m & ((1ull << lane) - 1))] = val;
 }
+
+// lst[0] / lst[1]: counts of the mid / big lists (zeroed by gs_scan_totals), midk / bigk: keys
 __global__ void __launch_bounds__(256) gs_bucket_sort(GsRec* __restrict__ rec, const int* __restrict__ off,
-                                                      const int* __restrict__ boff, long nkey) {
+                                                      const int* __restrict__ boff, long nkey, int* __restrict__ lst,
+                                                      int* __restrict__ midk, int* __restrict__ bigk) {
   const long key = (long)blockIdx.x * 256 + threadIdx.x;
-  if (key >= nkey - 1) return;
-  const int b = gs_offset(off, boff, (int)key), n = gs_offset(off, boff, (int)key + 1) - b;
-  if (n < 2) return;
-  GsRec* a = rec + b;
-  if (n <= 16) {
-    for (int i = 1; i < n; ++i) {
-      const GsRec x = a[i];
-      int j = i - 1;
-      while (j >= 0 && a[j].v > x.v) {
-        a[j + 1] = a[j];
-        --j;
-      }
-      a[j + 1] = x;
-    }
-    return;
+  int b = 0, n = 0;
+  if (key < nkey - 1) {
+    b = gs_offset(off, boff, (int)key);
+    n = gs_offset(off, boff, (int)key + 1) - b;
   }
-  for (int i = n / 2 - 1; i >= 0; --i) gs_sift(a, i, n);
-  for (int e = n - 1; e > 0; --e) {
-    const GsRec t = a[0];
-    a[0] = a[e];
-    a[e] = t;
-    gs_sift(a, 0, e);
+  gs_append(n > GS_INS && n <= GS_MID, lst, midk, (int)key);
+  gs_append(n > GS_MID, lst + 1, bigk, (int)key);
+  if (n < 2 || n > GS_INS) return;
+  GsRec* a = rec + b;
+  for (int i = 1; i < n; ++i) {
+    const GsRec x = a[i];
+    int j = i - 1;
+    while (j >= 0 && a[j].v > x.v) {
+      a[j + 1] = a[j];
+      --j;
+    }
+    a[j + 1] = x;
+  }
+}
+
+// persistent over the two lists (GS_COOP_BLOCKS workgroups; every block exits once both are done)
+__global__ void __launch_bounds__(256) gs_bucket_sort_coop(const float* __restrict__ grid,
+                                                           const int2* __restrict__ keyrank, GsRec* __restrict__ rec,
+                                                           const int* __restrict__ off, const int* __restrict__ boff,
+                                                           const int* __restrict__ lst, const int* __restrict__ midk,
+                                                           const int* __restrict__ bigk, long nvox, int Di, int Hi,
+                                                           int Wi) {
+  __shared__ GsRec s[GS_MID];
+  const int tid = threadIdx.x;
+  const int nmid = lst[0], nbig = lst[1];
+  for (int i = blockIdx.x; i < nmid; i += gridDim.x) {
+    const int key = midk[i];
+    const int b = gs_offset(off, boff, key), n = gs_offset(off, boff, key + 1) - b;
+    int P = 32;
+    while (P < n) P <<= 1;
+    for (int j = tid; j < P; j += 256) {
+      if (j < n) s[j] = rec[b + j];
+      else s[j].v = 0x7fffffff;
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int t = tid; t < P / 2; t += 256) {
+          const int lo = 2 * t - (t & (j - 1)), hi = lo + j;
+          const GsRec x = s[lo], y = s[hi];
+          if ((x.v > y.v) == ((lo & k) == 0)) s[lo] = y, s[hi] = x;
+        }
+        __syncthreads();
+      }
+    for (int j = tid; j < n; j += 256) rec[b + j] = s[j];
+    __syncthreads();
+  }
+  for (int i = blockIdx.x; i < nbig; i += gridDim.x) {
+    const int key = bigk[i];
+    GsRec* a = rec + gs_offset(off, boff, key);
+    int run = 0;
+    for (long v0 = 0; v0 < nvox; v0 += 1024) {
+      int m[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long v = v0 + tid * 4 + j;
+        m[j] = v < nvox && keyrank[v].x == key;
+      }
+      int total;
+      int e = gs_block_scan(m, &total) + run;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (m[j]) {
+          const long v = v0 + tid * 4 + j;
+          int x0, y0, z0;
+          GsRec r;
+          gs_base(grid, v, Di, Hi, Wi, x0, y0, z0, r.tx, r.ty, r.tz);
+          r.v = (int)v;
+          a[e++] = r;
+        }
+      run += total;
+    }
   }
 }
 
@@ -364,7 +427,7 @@ __global__ void __launch_bounds__(256) gs_gather_input(const GsRec* __restrict__
 }
 
 struct GsWs {
-  int *cnt, *bsum;
+  int *cnt, *bsum, *lst, *midk, *bigk;   // lst: the two list counts of gs_bucket_sort
   int2* keyrank;
   GsRec* rec;
   long nkey, nblk, nvox;
@@ -382,6 +445,9 @@ static GsWs gs_ws_layout(void* base, int B, int Di, int Hi, int Wi, int Do, int 
   w.bsum = (int*)(p + o), o += up(w.nblk * 4);
   w.keyrank = (int2*)(p + o), o += up(w.nvox * 8);
   w.rec = (GsRec*)(p + o), o += up(w.nvox * sizeof(GsRec));
+  w.lst = (int*)(p + o), o += up(2 * 4);
+  w.midk = (int*)(p + o), o += up((w.nvox / (GS_INS + 1) + 1) * 4);
+  w.bigk = (int*)(p + o), o += up((w.nvox / (GS_MID + 1) + 1) * 4);
   w.bytes = o;
   return w;
 }
@@ -691,10 +757,13 @@ int fv_grid_sample3d_bwd_input(int dtype, const float* grid, const void* gout, i
   hipLaunchKernelGGL(gs_bucket_count, dim3(fv_cdiv(w.nvox, 256)), dim3(256), 0, s, grid, w.nvox, (long)Do * Ho * Wo, Di,
                      Hi, Wi, group, w.cnt, w.keyrank);
   hipLaunchKernelGGL(gs_scan_blocks, dim3((unsigned)w.nblk), dim3(256), 0, s, w.cnt, w.nkey, w.bsum);
-  hipLaunchKernelGGL(gs_scan_totals, dim3(1), dim3(256), 0, s, w.bsum, (int)w.nblk);
+  hipLaunchKernelGGL(gs_scan_totals, dim3(1), dim3(256), 0, s, w.bsum, (int)w.nblk, w.lst);
   hipLaunchKernelGGL(gs_bucket_fill, dim3(fv_cdiv(w.nvox, 256)), dim3(256), 0, s, grid, w.keyrank, w.cnt, w.bsum,
                      w.nvox, Di, Hi, Wi, w.rec);
-  hipLaunchKernelGGL(gs_bucket_sort, dim3(fv_cdiv(w.nkey - 1, 256)), dim3(256), 0, s, w.rec, w.cnt, w.bsum, w.nkey);
+  hipLaunchKernelGGL(gs_bucket_sort, dim3(fv_cdiv(w.nkey - 1, 256)), dim3(256), 0, s, w.rec, w.cnt, w.bsum, w.nkey,
+                     w.lst, w.midk, w.bigk);
+  hipLaunchKernelGGL(gs_bucket_sort_coop, dim3(GS_COOP_BLOCKS), dim3(256), 0, s, grid, w.keyrank, w.rec, w.cnt, w.bsum,
+                     w.lst, w.midk, w.bigk, w.nvox, Di, Hi, Wi);
 #define GS_GATHER(T, V)                                                                                          \
   hipLaunchKernelGGL((gs_gather_input<T, V>), dim3(fv_cdiv(ncell * (C / V), 256)), dim3(256), 0, s, w.rec, w.cnt, \
                      w.bsum, (const T*)gout, ncell, Di, Hi, Wi, C, (T*)gin)

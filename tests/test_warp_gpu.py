@@ -200,8 +200,9 @@ def test_grid_sample3d_warp_shape_vs_torch(dtype):
 @pytest.mark.parametrize("collapse", [False, True])
 def test_grid_sample3d_input_gradient_is_deterministic(collapse):
     """The bucketed gather's buckets are sorted by voxel index (warp.hip gs_bucket_sort), so the
-    input gradient is bit-identical run to run; `collapse` squeezes every sample into a corner
-    cell (buckets of thousands of voxels: the heapsort path) -- still vs F.grid_sample."""
+    input gradient is bit-identical run to run; `collapse` squeezes every sample into two corner
+    cells (buckets of 17..2048 voxels: the workgroup bitonic sort of gs_bucket_sort_coop) --
+    still vs F.grid_sample."""
     g = torch.Generator().manual_seed(11)
     N, C, Di, Hi, Wi, Do, Ho, Wo = 2, 32, 4, 8, 16, 8, 16, 16
     inp = torch.randn(N, C, Di, Hi, Wi, generator=g)
@@ -220,3 +221,42 @@ def test_grid_sample3d_input_gradient_is_deterministic(collapse):
     ir = inp.clone().requires_grad_(True)
     F.grid_sample(ir, grid, align_corners=True).backward(gout)
     assert rel(grads[0], ir.grad) < 1e-5
+
+
+@pytest.mark.parametrize("mode", ["constant", "half"])
+def test_grid_sample3d_input_gradient_degenerate_grid(mode):
+    """A degenerate motion grid: every voxel ("constant") or the front half of the volume
+    ("half") samples one point, so one bucket per image holds 32-64 K voxels (more than
+    GS_MID: gs_bucket_sort_coop's stable compaction, not one lane's sort).  Bit-identical run to
+    run, within 1e-4 of a float64 F.grid_sample (65 K-term sums per cell), and bounded in time:
+    the warm backward finishes in well under a second (one lane sorting the bucket took
+    seconds)."""
+    g = torch.Generator().manual_seed(5)
+    N, C, Di, Hi, Wi, Do, Ho, Wo = 2, 32, 8, 16, 16, 16, 64, 64
+    inp = torch.randn(N, C, Di, Hi, Wi, generator=g)
+    grid = (torch.rand(N, Do, Ho, Wo, 3, generator=g) - 0.5) * 2.0
+    pt = torch.tensor([0.1, -0.2, 0.3])
+    if mode == "constant":
+        grid[:] = pt
+    else:
+        grid[:, : Do // 2] = pt
+    gout = torch.randn(N, C, Do, Ho, Wo, generator=g)
+    gd, god = grid.cuda(), gout.cuda()
+    grads, times = [], []
+    for _ in range(3):
+        xi = inp.cuda().contiguous(memory_format=CL3).requires_grad_(True)
+        out = warp.GridSample3dFn.apply(xi, gd, 1, torch.float32)
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        out.backward(god)
+        t1.record()
+        torch.cuda.synchronize()
+        times.append(t0.elapsed_time(t1))
+        grads.append(xi.grad.cpu())
+    print(f"\ndegenerate grid ({mode}): backward {min(times[1:]):.2f} ms")
+    assert all(torch.equal(grads[0], t) for t in grads[1:])
+    ir = inp.double().requires_grad_(True)
+    F.grid_sample(ir, grid.double(), align_corners=True).backward(gout.double())
+    assert rel(grads[0], ir.grad) < 1e-4
+    assert min(times[1:]) < 500.0, times
