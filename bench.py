@@ -174,16 +174,19 @@ def main():
     eps = torch.randn(B, cfg.latent, cfg.latent_hw, cfg.latent_hw,
                       generator=torch.Generator().manual_seed(1235 + rank)).cuda()
 
+    # d(w_R R + w_K K) seeded straight into the two loss terms (no ones-fill, add or scalar
+    # multiplies in the backward); the weighted sum is formed only for the returned value
+    w_seed = (torch.tensor(cfg.w_R, device="cuda"), torch.tensor(cfg.w_K, device="cuda"))
+
     def step(keep=None):
         opt.zero_grad(set_to_none=True)
         y, mu, logstd = net(x, eps)
         R, K = rec((x, y)), kl((mu, logstd))
-        loss = cfg.w_R * R + cfg.w_K * K
-        loss.backward()
+        torch.autograd.backward([R, K], list(w_seed))
         opt.step()
         if keep is not None:
             keep.extend([y.detach(), R.detach(), K.detach()])
-        return loss
+        return R.detach(), K.detach()
 
     # dominant kernel family: the ResBlock 3x3 256->256 convs at the latent resolution
     res_c = cfg.up_seq[0]
@@ -235,6 +238,7 @@ def main():
         tt = torch.tensor([t], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = tt.item()
+    loss = cfg.w_R * loss[0] + cfg.w_K * loss[1]          # the weighted sum (trainer.py:250-251)
     assert torch.isfinite(loss).item()
 
     ms = t / args.steps * 1e3

@@ -95,14 +95,23 @@ class FaceVAETrainer:
         for opt in self.g_optimizers.values():
             opt.zero_grad(set_to_none=True)
         y, mu, logstd = self.net(x, eps)
-        losses = {"R": self.weights["R"] * self.recon((x, y)),
-                  "K": self.weights["K"] * self.kl((mu, logstd))}
-        loss = sum(losses.values())
-        loss.backward()
+        R, K = self.recon((x, y)), self.kl((mu, logstd))
+        losses = {"R": self.weights["R"] * R.detach(), "K": self.weights["K"] * K.detach()}
+        # backward of sum(w * loss): the weights seed the two terms directly (no ones-fill, add
+        # or scalar multiplies in the captured backward)
+        torch.autograd.backward([R, K], list(self._loss_seeds(x.device)))
         for opt in self.g_optimizers.values():
             opt.step()
         losses["y"] = y
         return losses
+
+    def _loss_seeds(self, device):
+        key = (device, float(self.weights["R"]), float(self.weights["K"]))
+        seeds = getattr(self, "_seeds", None)
+        if seeds is None or seeds[0] != key:
+            seeds = (key, torch.tensor(key[1], device=device), torch.tensor(key[2], device=device))
+            self._seeds = seeds
+        return seeds[1:]
 
     def sample_eps(self, x: torch.Tensor) -> torch.Tensor:
         B = x.shape[0]
