@@ -155,6 +155,47 @@ def test_trainer_graph_mode_matches_eager():
     assert trs[1]._sg is not None            # the graph of the first shape survived the eager step
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainer_loss_weights_seed_backward(graph):
+    """FaceVAETrainer seeds the backward of R and K with their weights (no ones-fill / add /
+    scalar multiplies in the step): with the reference's commented weights (w_R = 10, w_K = 0.2,
+    trainer.py:250-251) three steps give the parameters and losses of the plain
+    (w_R R + w_K K).backward() step on the same model -- bit-identical eager, within the
+    graph-vs-eager Adam bar when graph-replayed."""
+    import dataclasses
+    g = torch.load(os.path.join(GOLD, "toy_step.pt"), weights_only=True)
+    cfg = dataclasses.replace(fv.FaceVAEConfig.toy(), w_R=10.0, w_K=0.2)
+    torch.manual_seed(0)
+    tr = fv.FaceVAETrainer(None, None, [], cfg.lr, cfg=cfg, compute_dtype=torch.float32, graph=graph)
+    tr.model.load_state_dict(g["init"])
+    torch.manual_seed(0)
+    m = fv.FaceVAE(cfg).cuda().set_compute_dtype(torch.float32)
+    m.load_state_dict(g["init"])
+    opts = [fv.Adam(mm.parameters(), lr=cfg.lr, betas=cfg.betas) for mm in (m.afe, m.generator)]
+    rec, kl = fv.ReconLoss(), fv.KLDivergenceLoss()
+    gen = torch.Generator().manual_seed(3)
+    for i in range(3):
+        x = torch.rand(2, 3, 64, 64, generator=gen).cuda()
+        eps = torch.randn(2, cfg.latent, cfg.latent_hw, cfg.latent_hw, generator=gen).cuda()
+        out = tr.train_step(x, eps)
+        for o in opts:
+            o.zero_grad(set_to_none=True)
+        y, mu, ls = m(x, eps)
+        R, K = rec((x, y)), kl((mu, ls))
+        (cfg.w_R * R + cfg.w_K * K).backward()
+        for o in opts:
+            o.step()
+        torch.cuda.synchronize()
+        # eager: bit-identical; graph: the replayed Adam's device-side bias correction differs
+        # from the eager one in the last bits (test_trainer_graph_mode_matches_eager's bar)
+        tol = 1e-6 if graph else 0.0
+        for a, b in ((out["R"].item(), (cfg.w_R * R).item()), (out["K"].item(), (cfg.w_K * K).item())):
+            assert abs(a - b) <= tol * abs(b), (i, a, b)
+        pa = dict(tr.model.named_parameters())
+        for k, p in m.named_parameters():
+            assert (rel(pa[k], p) < 1e-6) if graph else torch.equal(pa[k], p), (i, k)
+
+
 def test_sn_bwd_batch_bit_identical(monkeypatch):
     """Spectral-norm backward terms batched at the end of backward (ops._SN_BATCH) against the
     per-conv launches: the same partial sums in the same order, bit-identical parameters."""
