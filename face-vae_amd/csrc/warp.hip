@@ -396,7 +396,41 @@ __global__ void __launch_bounds__(256) gs_gather_input(const GsRec* __restrict__
     const int dx = k & 1, dy = (k >> 1) & 1, dz = k >> 2;
     const int key = gs_key(bi, z - dz, y - dy, x - dx, Di, Hi, Wi);
     const int e = gs_offset(off, boff, key + 1);
-    for (int r = gs_offset(off, boff, key); r < e; ++r) {
+    int r = gs_offset(off, boff, key);
+    // long buckets (a collapsed motion grid piles many voxels onto one cell): four records'
+    // loads in flight per step instead of one dependent pair, still summed in record order
+    for (; e - r >= 8; r += 4) {
+      GsRec R4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) R4[u] = rec[r + u];
+      if constexpr (V % 8 == 0) {
+        Chunk8<T> c4[4][V / 8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int h = 0; h < V / 8; ++h) c4[u][h].load(gout + (long)R4[u].v * C + q * V + 8 * h);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const GsRec& R = R4[u];
+          const float w = (dx ? R.tx : 1.f - R.tx) * (dy ? R.ty : 1.f - R.ty) * (dz ? R.tz : 1.f - R.tz);
+#pragma unroll
+          for (int h = 0; h < V / 8; ++h)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[8 * h + j] += w * c4[u][h].get(j);
+        }
+      } else {
+        float g4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g4[u] = ld(gout + (long)R4[u].v * C + q * V);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const GsRec& R = R4[u];
+          const float w = (dx ? R.tx : 1.f - R.tx) * (dy ? R.ty : 1.f - R.ty) * (dz ? R.tz : 1.f - R.tz);
+          acc[0] += w * g4[u];
+        }
+      }
+    }
+    for (; r < e; ++r) {
       const GsRec R = rec[r];
       const float w = (dx ? R.tx : 1.f - R.tx) * (dy ? R.ty : 1.f - R.ty) * (dz ? R.tz : 1.f - R.tz);
       const T* g = gout + (long)R.v * C + q * V;
