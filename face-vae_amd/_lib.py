@@ -197,6 +197,7 @@ _SIGS = {
     "fv_conv_weight_prep_batchable": (c_int, [D]),
     "fv_spectral_norm_bwd_multi": (c_int, [c_int, P, P, P]),
     "fv_conv_weight_prep_multi": (c_int, [c_int, P, P, P, P, P, P]),
+    "fv_conv_weight_prep_fp8_multi": (c_int, [c_int, P, P, P, P, P, P, P, P]),
     "fv_comm_unique_id": (c_int, [P]),
     "fv_comm_init": (c_int, [P, c_int, c_int, c_int, POINTER(c_void_p)]),
     "fv_comm_allreduce": (c_int, [c_void_p, P, c_size_t, c_int, c_int, P]),

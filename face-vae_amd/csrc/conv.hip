@@ -6019,10 +6019,11 @@ namespace {
 
 constexpr int FP8_NPART = 1024;   // amax partials (blocks of the amax pass)
 
+// block bid of nblk: max |x| over its grid-stride share -> part[bid]
 template <typename T>
-__global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, long n, float* part) {
+__device__ __forceinline__ void amax_body(const T* __restrict__ x, long n, float* part, int bid, int nblk) {
   float m = 0.f;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i * 8 < n; i += (long)gridDim.x * 256) {
+  for (long i = bid * 256L + threadIdx.x; i * 8 < n; i += (long)nblk * 256) {
     const long e = i * 8;
     if (e + 8 <= n) {
       Chunk8<T> c;
@@ -6037,7 +6038,12 @@ __global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, long
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (threadIdx.x == 0) part[bid] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, long n, float* part) {
+  amax_body<T>(x, n, part, blockIdx.x, gridDim.x);
 }
 
 // every block reduces the partials itself (1024 floats from L2), block 0 publishes dq
@@ -6172,15 +6178,15 @@ __global__ void __launch_bounds__(256) quantize_fp8_delayed_kernel(const T* __re
 // fp8 weights: wk [rows][9 cin] (k = tap * cin + ci) and / or the transposed, flipped wt
 // [rows_t][9 cout] (k = tap' * cout + co), both scaled by s = pow2 scale of amax(|w| / sigma);
 // dq[0] = 1 / s.  The amax partials of |w| come from amax_kernel<float> over w_param.
-__global__ void __launch_bounds__(256) weight_prep_fp8_kernel(const float* __restrict__ wp, const float* sigma,
-                                                              const float* part, int np, uint8_t* wk, int rows,
-                                                              uint8_t* wt, int rows_t, int cout, int cin, float* dq) {
+__device__ __forceinline__ void weight_prep_fp8_body(const float* __restrict__ wp, const float* sigma,
+                                                     const float* part, int np, uint8_t* wk, int rows, uint8_t* wt,
+                                                     int rows_t, int cout, int cin, float* dq, int bid, int nblk) {
   __shared__ float sh[4];
   const float inv = sigma ? 1.f / sigma[0] : 1.f;
   const float s = pow2_scale_of(amax_of_parts(part, np, sh) * inv);
-  if (blockIdx.x == 0 && threadIdx.x == 0) dq[0] = 1.f / s;
+  if (bid == 0 && threadIdx.x == 0) dq[0] = 1.f / s;
   const long nk = wk ? (long)rows * 9 * cin : 0, nt = wt ? (long)rows_t * 9 * cout : 0;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < nk + nt; e += (long)gridDim.x * 256) {
+  for (long e = bid * 256L + threadIdx.x; e < nk + nt; e += (long)nblk * 256) {
     float v = 0.f;
     uint8_t* dst;
     if (e < nk) {
@@ -6198,6 +6204,38 @@ __global__ void __launch_bounds__(256) weight_prep_fp8_kernel(const float* __res
     const int q = __builtin_amdgcn_cvt_pk_fp8_f32(v * inv * s, 0.f, 0, false);
     *dst = (uint8_t)(q & 0xff);
   }
+}
+
+__global__ void __launch_bounds__(256) weight_prep_fp8_kernel(const float* __restrict__ wp, const float* sigma,
+                                                              const float* part, int np, uint8_t* wk, int rows,
+                                                              uint8_t* wt, int rows_t, int cout, int cin, float* dq) {
+  weight_prep_fp8_body(wp, sigma, part, np, wk, rows, wt, rows_t, cout, cin, dq, blockIdx.x, gridDim.x);
+}
+
+// the e4m3 weights of many convs in two launches (fv_conv_weight_prep_fp8_multi): blockIdx.y
+// selects the conv, its amax partials live at ws + y * stride
+struct W8Job {
+  const float* w;
+  const float* sigma;
+  uint8_t *wk, *wt;
+  float* dq;
+  long nw;
+  int cout, cin, nb, nb2;
+};
+struct W8Multi {
+  int n, stride;
+  W8Job j[FV_WPREP_MAX];
+};
+__global__ void __launch_bounds__(256) amax_multi_kernel(W8Multi m, float* ws) {
+  const W8Job& j = m.j[blockIdx.y];
+  if ((int)blockIdx.x >= j.nb) return;
+  amax_body<float>(j.w, j.nw, ws + (long)blockIdx.y * m.stride, blockIdx.x, j.nb);
+}
+__global__ void __launch_bounds__(256) weight_prep_fp8_multi_kernel(W8Multi m, const float* ws) {
+  const W8Job& j = m.j[blockIdx.y];
+  if ((int)blockIdx.x >= j.nb2) return;
+  weight_prep_fp8_body(j.w, j.sigma, ws + (long)blockIdx.y * m.stride, j.nb, j.wk, j.cout, j.wt, j.cin, j.cout, j.cin,
+                       j.dq, blockIdx.x, j.nb2);
 }
 
 typedef int v8i __attribute__((ext_vector_type(8)));
@@ -6806,6 +6844,37 @@ int fv_conv_weight_prep_fp8(const fv_conv_desc* d, const float* w_param, const f
   hipLaunchKernelGGL(weight_prep_fp8_kernel, dim3(nb2), dim3(256), 0, s, w_param, sigma, (const float*)ws, nb, wk,
                      d->cout, wt, d->cin, d->cout, d->cin, dq);
   return fv_check_launch("weight_prep_fp8");
+}
+
+int fv_conv_weight_prep_fp8_multi(int n, const fv_conv_desc* descs, const float* const* w_params,
+                                  const float* const* sigmas, uint8_t* const* wks, uint8_t* const* wts,
+                                  float* const* dqs, void* ws, void* stream) {
+  FV_REQUIRE(n >= 1 && n <= FV_WPREP_MAX && descs && w_params && sigmas && wks && wts && dqs && ws,
+             "weight_prep_fp8_multi: bad args");
+  W8Multi m{};
+  m.n = n;
+  m.stride = FP8_NPART;
+  int nb_max = 1, nb2_max = 1;
+  for (int i = 0; i < n; ++i) {
+    const fv_conv_desc* d = &descs[i];
+    int st = check_desc(d);
+    if (st) return st;
+    FV_REQUIRE(fp8_ok(d), "weight_prep_fp8_multi: conv %d: unsupported descriptor", i);
+    FV_REQUIRE(w_params[i] && (wks[i] || wts[i]) && dqs[i], "weight_prep_fp8_multi: null pointer (conv %d)", i);
+    W8Job& j = m.j[i];
+    j.w = w_params[i], j.sigma = sigmas[i], j.wk = wks[i], j.wt = wts[i], j.dq = dqs[i];
+    j.nw = (long)d->cout * d->cin * 9;
+    j.cout = d->cout, j.cin = d->cin;
+    // the per-conv entry's grids (fv_conv_weight_prep_fp8): the same partials, the same bits
+    j.nb = (int)std::min<long>(FP8_NPART, std::max<long>(1, (j.nw / 8 + 255) / 256));
+    j.nb2 = (int)std::min<long>(2048, fv_cdiv((wks[i] ? j.nw : 0) + (wts[i] ? j.nw : 0), 256));
+    nb_max = std::max(nb_max, j.nb);
+    nb2_max = std::max(nb2_max, j.nb2);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(amax_multi_kernel, dim3(nb_max, n), dim3(256), 0, s, m, (float*)ws);
+  hipLaunchKernelGGL(weight_prep_fp8_multi_kernel, dim3(nb2_max, n), dim3(256), 0, s, m, (const float*)ws);
+  return fv_check_launch("weight_prep_fp8_multi");
 }
 
 int fv_conv2d_fwd_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_dq, const uint8_t* wk,

@@ -239,6 +239,9 @@ class SNBatch:
 
 
 WPREP_MAX = 24
+# fp8 weight quantization batched by WPrepBatch (tests flip it off to compare with the per-conv
+# fv_conv_weight_prep_fp8 launches)
+_WPREP_FP8_BATCH = os.environ.get("FV_WPREP8_BATCH", "1") != "0"
 
 
 class WPrepBatch:
@@ -252,6 +255,8 @@ class WPrepBatch:
         self.convs = list(convs)
 
     def run(self, device):
+        if _WPREP_FP8_BATCH:
+            self._run_fp8(device)
         groups = {}
         for c in self.convs:
             key = getattr(c, "_fv_desc", None)
@@ -286,6 +291,41 @@ class WPrepBatch:
                 for c, key, k, t in bufs:
                     c._fv_prep = (key[0], k, t)
 
+    def _run_fp8(self, device):
+        """The e4m3 weights (+ scales) of the convs whose last forward ran fp8, in two launches
+        (fv_conv_weight_prep_fp8_multi; 2 x 14 launches per fp8 FaceVAE step before)."""
+        items = []
+        for c in self.convs:
+            key = getattr(c, "_fv_desc8", None)
+            if key is None:
+                continue
+            sigma = None
+            if c.sn:
+                pre = getattr(c, "_sn_pre", None)
+                if pre is None:
+                    continue
+                sigma = pre[0]
+            items.append((c, L.ConvDesc.from_buffer_copy(key[0]), key, sigma))
+        for i0 in range(0, len(items), WPREP_MAX):
+            chunk = items[i0:i0 + WPREP_MAX]
+            n = len(chunk)
+            descs = (L.ConvDesc * n)(*[d for _, d, _, _ in chunk])
+            wp, sg, wk, wt, dq = ((ctypes.c_void_p * n)() for _ in range(5))
+            bufs = []
+            for i, (c, d, key, sigma) in enumerate(chunk):
+                k = _empty(query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), torch.uint8, device)
+                t = _empty(query("fv_conv_fp8_wt_bytes", ctypes.byref(d)), torch.uint8, device) if key[1] else None
+                q = _empty(1, F32, device)
+                wp[i], sg[i], wk[i], wt[i], dq[i] = c.weight_param().data_ptr(), ptr(sigma), k.data_ptr(), ptr(t), \
+                    q.data_ptr()
+                bufs.append((c, key, k, t, q))
+            ws = _empty(n * query("fv_fp8_ws_bytes") // 4, F32, device)
+            call("fv_conv_weight_prep_fp8_multi", n, ctypes.addressof(descs), ctypes.addressof(wp),
+                 ctypes.addressof(sg), ctypes.addressof(wk), ctypes.addressof(wt), ctypes.addressof(dq), ptr(ws),
+                 stream())
+            for c, key, k, t, q in bufs:
+                c._fv_prep8 = (key[0], k, t, q)
+
 
 class ConvState:
     """Per-forward state of one conv: descriptor, prepared weights, SN snapshot.  With fp8
@@ -312,6 +352,13 @@ class ConvState:
         self.fp8 = bool(fp8) and bool(query("fv_conv2d_fp8_supported", ctypes.byref(d)))
         if self.fp8:
             conv._fv_desc = conv._fv_prep = None
+            key = (bytes(d), bool(need_wt))
+            pre = getattr(conv, "_fv_prep8", None)
+            conv._fv_prep8 = None
+            conv._fv_desc8 = key               # what the next forward's WPrepBatch quantizes
+            if pre is not None and pre[0] == key[0] and (pre[2] is not None or not need_wt):
+                self.wk, self.wt, self.wdq = pre[1], (pre[2] if need_wt else None), pre[3]
+                return
             self.wk = _empty(query("fv_conv_fp8_wk_bytes", ctypes.byref(d)), torch.uint8, device)
             self.wt = _empty(query("fv_conv_fp8_wt_bytes", ctypes.byref(d)), torch.uint8, device) if need_wt else None
             self.wdq = _empty(1, F32, device)
@@ -319,6 +366,7 @@ class ConvState:
             call("fv_conv_weight_prep_fp8", ctypes.byref(d), ptr(w), ptr(self.sigma), ptr(self.wk), ptr(self.wt),
                  ptr(self.wdq), ptr(ws), stream())
             return
+        conv._fv_desc8 = conv._fv_prep8 = None
         key = (bytes(d), bool(need_wt))
         pre = getattr(conv, "_fv_prep", None)
         conv._fv_prep = None

@@ -212,6 +212,13 @@ size_t fv_conv_fp8_wt_bytes(const fv_conv_desc* d);
  * transposed, flipped wt [cin][9 cout] (k = tap * channels + c), one scale: dq[0] */
 int fv_conv_weight_prep_fp8(const fv_conv_desc* d, const float* w_param, const float* sigma,
                             uint8_t* wk, uint8_t* wt, float* dq, void* ws, void* stream);
+/* fv_conv_weight_prep_fp8 for n <= FV_WPREP_MAX convs in two launches (the per-step weight
+ * quantization of an fp8 model): arrays of n descriptors / pointers as fv_conv_weight_prep_multi
+ * (wts[i] may be NULL), dqs[i] one float each; ws = n * fv_fp8_ws_bytes() bytes.  Bit-identical
+ * to n fv_conv_weight_prep_fp8 calls. */
+int fv_conv_weight_prep_fp8_multi(int n, const fv_conv_desc* descs, const float* const* w_params,
+                                  const float* const* sigmas, uint8_t* const* wks, uint8_t* const* wts,
+                                  float* const* dqs, void* ws, void* stream);
 int fv_conv2d_fwd_fp8(const fv_conv_desc* d, const uint8_t* x8, const float* x_dq, const uint8_t* wk,
                       const float* w_dq, const float* bias, const void* res, void* y, float* stats,
                       void* stream);

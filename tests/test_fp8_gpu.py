@@ -492,3 +492,49 @@ def test_conv_fp8_wgrad(kind, N):
     print(f"\n[fp8 wgrad {kind} N={N}] worst |d| / (2^-10 sum|terms|): weight {ew:.4f} bias {eb:.4f}; "
           f"rel-L2 weight {rel(dw, rw):.2e} bias {rel(db, rb):.2e}")
     assert ew <= 1.0 and eb <= 1.0
+
+
+def test_fp8_weight_prep_batched_bit_identical(monkeypatch):
+    """The per-step e4m3 weight quantization of every fp8 conv batched into two launches
+    (ops.WPrepBatch -> fv_conv_weight_prep_fp8_multi) against the per-conv
+    fv_conv_weight_prep_fp8 launches: three fp8 training steps of the FaceVAE at 256², B=2 give
+    bit-identical parameters, losses and output."""
+    cfg = fv.FaceVAEConfig()
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(2, 3, cfg.H, cfg.H, generator=g).cuda()
+    eps = torch.randn(2, cfg.latent, cfg.latent_hw, cfg.latent_hw, generator=g).cuda()
+    torch.manual_seed(0)
+    init = {k: v.clone() for k, v in fv.FaceVAE(cfg).state_dict().items()}
+    res, counts = [], []
+    names = []
+    orig_call = ops.call
+
+    def spy(name, *a):
+        names.append(name)
+        return orig_call(name, *a)
+
+    monkeypatch.setattr(ops, "call", spy)
+    for batch in (False, True):
+        monkeypatch.setattr(ops, "_WPREP_FP8_BATCH", batch)
+        names.clear()
+        m = fv.FaceVAE(cfg).cuda().train().set_compute_dtype(torch.float8_e4m3fn)
+        m.load_state_dict(init)
+        opt = fv.Adam(m.parameters(), lr=cfg.lr, betas=cfg.betas)
+        for _ in range(3):
+            opt.zero_grad(set_to_none=True)
+            y, mu, ls = m(x, eps)
+            R, K = fv.ReconLoss()((x, y)), fv.KLDivergenceLoss()((mu, ls))
+            (R + K).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        counts.append((names.count("fv_conv_weight_prep_fp8"), names.count("fv_conv_weight_prep_fp8_multi")))
+        res.append((y.detach().float().cpu(), R.item(), K.item(),
+                    {k: p.detach().cpu().clone() for k, p in m.named_parameters()}))
+    # per-conv quantization in every step without batching; with it only in the first step (no
+    # forward has recorded the descriptors yet), then one two-launch call per step
+    (n1_off, nm_off), (n1_on, nm_on) = counts
+    assert n1_off > 0 and nm_off == 0 and n1_on * 3 == n1_off and nm_on == 2, counts
+    (y0, r0, k0, p0), (y1, r1, k1, p1) = res
+    assert torch.equal(y0, y1) and r0 == r1 and k0 == k1
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
