@@ -49,7 +49,7 @@ def fp8_site(conv, which: str, device):
     sites = conv.__dict__.setdefault("_fv_fp8_sites", {})
     st = sites.get(which)
     if st is None or st[0].device != device:
-        st = [torch.zeros(query("fv_fp8_site_bytes") // 4, dtype=torch.int32, device=device), False]
+        st = [torch.zeros(query("fv_fp8_site_bytes") // 4, dtype=torch.int32, device=device), False, []]
         sites[which] = st
     return st
 
@@ -59,11 +59,41 @@ def fp8_site(conv, which: str, device):
 FP8_GLOBAL = None
 
 
+def _dq_snapshot(site):
+    """A forward's e4m3 operand keeps a VIEW of its site's dq word for the weight gradient (no
+    copy per forward: 14 copy launches per fp8 step).  Before the site is quantized again while
+    such a view is still held -- a second forward through the conv before its backward, or an
+    eval forward in between -- the holder gets its own copy of the value."""
+    if site is None or len(site) < 3:
+        return
+    for ref in site[2]:
+        cs = ref()
+        q = getattr(cs, "x8", None) if cs is not None else None
+        if q is not None and q[1].data_ptr() == site[0].data_ptr() + 18 * 4:
+            cs.x8 = (q[0], q[1].clone())
+    site[2].clear()
+
+
+_DQ_VIEW = os.environ.get("FV_DQ_VIEW", "1") == "1"     # 0: copy the dq at every forward (A/B)
+
+
+def _hold_x8(cs, x8, xdq, site):
+    """cs.x8 = (x8, xdq) for the fp8 weight gradient; a dq that is the site's word is tracked
+    (_dq_snapshot copies it only if the site is re-quantized before cs's backward)."""
+    if not _DQ_VIEW:
+        cs.x8 = (x8, xdq.clone())
+        return
+    cs.x8 = (x8, xdq)
+    if len(site) > 2 and xdq.data_ptr() == site[0].data_ptr() + 18 * 4:
+        site[2].append(weakref.ref(cs))
+
+
 def quantize_fp8_site(t: torch.Tensor, site):
     """(uint8 e4m3 copy of t quantized with the site's delayed scale, dq view [1] fp32); the
     first call of a site quantizes exactly and seeds its history -- under data parallelism
     with the exact amax all-reduced (MAX) across ranks, so every rank starts from the same
     scale (the single process on the global batch)."""
+    _dq_snapshot(site)
     y = _empty(t.numel(), torch.uint8, t.device)
     ws = _empty(query("fv_fp8_ws_bytes") // 4, F32, t.device)
     seeded = int(site[1])
@@ -402,10 +432,10 @@ def conv_forward(cs: ConvState, x, bias, pro=None, res=None, y=None, stats=False
     if cs.fp8:
         site = fp8_site(cs.conv, "x", x.device)
         x8, xdq = x8 if x8 is not None else quantize_fp8_site(x, site)
-        # the e4m3 operand stays for the fp8 weight gradient with a COPY of its dq: the site's
-        # word 18 is rewritten by the site's next quantization (a second forward through this
-        # conv, or an eval forward, before this backward)
-        cs.x8 = (x8, xdq.clone())
+        # the e4m3 operand stays for the fp8 weight gradient; its dq is the site's word 18,
+        # which the site's next quantization rewrites (a second forward through this conv, or
+        # an eval forward, before this backward): _dq_snapshot copies it then
+        _hold_x8(cs, x8, xdq, site)
         _timed("fwd", d, lambda: call("fv_conv2d_fwd_fp8_site", ctypes.byref(d), ptr(x8), ptr(site[0]), ptr(cs.wk),
                                       ptr(cs.wdq), ptr(bias), ptr(res), ptr(y), ptr(part), stream()))
         if CHECK is not None:
@@ -739,6 +769,7 @@ def bn_act_forward_q8(y, r: BNResult, slope, bn, site, only8=False):
     the e4m3 copy alone -- `out` is then a 0-element placeholder of the right dtype / device."""
     if not _q8_ok(site, y, False):
         return bn_act_forward(y, r, slope, False, bn), None
+    _dq_snapshot(site)
     N, C, H, W = y.shape
     n = N * C * H * W
     if only8:
@@ -955,7 +986,7 @@ class ResBlockFn(torch.autograd.Function):
             if cs2.fp8:
                 site = fp8_site(c2, "x", x.device)
                 x8, xdq = q2 if q2 is not None else quantize_fp8_site(a2, site)
-                cs2.x8 = (x8, xdq.clone())
+                _hold_x8(cs2, x8, xdq, site)
                 _timed("fwd", d2, lambda: call("fv_conv2d_fwd_fp8_site_sr", ctypes.byref(d2), ptr(x8), ptr(site[0]),
                                                ptr(cs2.wk), ptr(cs2.wdq), ptr(b2), ptr(xb), ptr(out),
                                                ctypes.byref(sr), stream()))

@@ -538,3 +538,51 @@ def test_fp8_weight_prep_batched_bit_identical(monkeypatch):
     assert torch.equal(y0, y1) and r0 == r1 and k0 == k1
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
+
+
+def test_fp8_dq_view_survives_a_second_forward():
+    """The fp8 weight gradient reads the forward's x scale (dq) as a view of the conv's
+    delayed-scaling site (no copy per forward).  A second forward through the same block before
+    the first one's backward re-quantizes the site with another scale (4x larger input): the
+    first backward must still see ITS dq (ops._dq_snapshot copies it just before the site is
+    re-quantized), so every gradient equals the run without the second forward, bit for bit."""
+    from facevae_amd.modules import ResBlock2D
+    N, C, H, W = 2, 256, 8, 64
+    g = torch.Generator().manual_seed(47)
+    x0 = torch.randn(N, C, H, W, generator=g).cuda().to(torch.bfloat16).contiguous(memory_format=CL)
+    g1 = torch.randn(N, C, H, W, generator=g).cuda()
+    torch.manual_seed(11)
+    blk = ResBlock2D(C, False).cuda().train().set_compute_dtype(torch.float8_e4m3fn)
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+
+    def site_dq():
+        return blk.conv1.__dict__["_fv_fp8_sites"]["x"][0][18:19].view(torch.float32)
+
+    def run(second):
+        blk.load_state_dict(sd)
+        for m in blk.modules():
+            m.__dict__.pop("_fv_fp8_sites", None)
+        x = x0.clone().requires_grad_(True)
+        blk(x).float().mul(g1).sum().backward()     # step 1 seeds the sites
+        for p in blk.parameters():
+            p.grad = None
+        x = x0.clone().requires_grad_(True)
+        out = blk(x)
+        dq_first = site_dq().clone()
+        if second:
+            # a spike survives BN's normalisation: the x sites' amax grows, and the second of
+            # these forwards quantizes with the grown (delayed) scale
+            x2 = x0.clone()
+            x2[:, :, 0, 0] = 50.0
+            for _ in range(2):
+                blk(x2)
+            assert not torch.equal(site_dq(), dq_first), "the test needs the site's dq to change"
+        (out.float() * g1).sum().backward()
+        torch.cuda.synchronize()
+        return x.grad.clone(), [p.grad.clone() for p in blk.parameters()]
+
+    dx_a, gr_a = run(False)
+    dx_b, gr_b = run(True)
+    assert torch.equal(dx_a, dx_b)
+    for a, b in zip(gr_a, gr_b):
+        assert torch.equal(a, b)
