@@ -1199,12 +1199,7 @@ class KLFn(torch.autograd.Function):
         ctx.holder = None
         if pre is not None and pre[0] is logstd and mu._version == pre[2] and logstd._version == pre[3]:
             ctx.holder = pre[4]                    # value reduced by the reparameterisation pass,
-            # gradient folded into its backward; the first KL of this pair returns the reduced
-            # value itself (no copy launch), a second one a copy
-            if not pre[4].get("kl_returned"):
-                pre[4]["kl_returned"] = True
-                return pre[1]
-            return pre[1].clone()
+            return pre[1].clone()                  # gradient folded into its backward
         if mu.dtype not in (F32, torch.bfloat16):
             mu, logstd = mu.float(), logstd.float()
         mu, logstd = _same_layout(mu, logstd)
