@@ -139,10 +139,12 @@ def test_b32_step_matches_oracle(oracle_b32, dtype):
         # layers of the Generator trunk is ill-conditioned -- even between two fp32
         # computations (fp32 mode above vs the fp32 CPU oracle) the deviation grows from 1e-6 at
         # out_conv to 4e-3 at Generator.in_conv, and the bf16 storage noise grows the same way,
-        # ~60x larger (5e-3 at out_conv to ~0.25 at Generator.in_conv).
+        # ~60x larger (5e-3 at out_conv to ~0.25 at Generator.in_conv).  The kernels are
+        # deterministic, so these numbers repeat on every box (r6: image 4.56e-3, median grad
+        # 8.8e-2, worst 0.247, BN running stats 2.2e-3); the gates sit ~1.4-2x above them.
         gs = sorted(gdev.values())
-        assert dev["image"] < 2e-2 and dev["R"] < 1e-3 and dev["K"] < 1e-3
-        assert gs[len(gs) // 2] < 0.2 and gs[-1] < 0.5 and max(bn.values()) < 2e-2
+        assert dev["image"] < 1e-2 and dev["R"] < 1e-3 and dev["K"] < 1e-3
+        assert gs[len(gs) // 2] < 0.12 and gs[-1] < 0.35 and max(bn.values()) < 5e-3
 
 
 def test_bn_eval_mode_matches_oracle():
