@@ -212,11 +212,13 @@ def test_fp8_every_conv_launch_and_step_deviation(oracle_b32):
     Generator.in_conv, AFE.down2) run forward and data gradient on e4m3 operands -- each such launch is
     checked against torch fp32 on the same dequantized operands (fwd8 / dgrad8 rows), every
     other launch as in bf16 mode; the step's deviation from the fp32 oracle is reported
-    (e4m3: 3 mantissa bits, ~2.6e-2 rel-L2 per conv output) and loosely gated."""
+    (e4m3: 3 mantissa bits, ~2.6e-2 rel-L2 per conv output) and gated ~1.5x above the measured,
+    deterministic values (r6: image 3.96e-2, R 3.0e-5, K 1.3e-4; the losses at the north_star
+    1e-3 bar)."""
     x, eps, oo, og, osd = oracle_b32
     _fp8_launch_check(32)
     init, y, R, K, grads, state, _ = _gpu_step(fv.FaceVAEConfig(), torch.float8_e4m3fn, x, eps)
     dev = {"image": rel(y, oo["y"]), "R": abs(R - oo["R"].item()) / oo["R"].item(),
            "K": abs(K - oo["K"].item()) / abs(oo["K"].item())}
     print(f"[fp8] 256x256 B=32 one step vs oracle: {dev}")
-    assert dev["image"] < 0.1 and dev["R"] < 2e-2 and dev["K"] < 1e-2
+    assert dev["image"] < 0.06 and dev["R"] < 1e-3 and dev["K"] < 1e-3
