@@ -167,14 +167,16 @@ def test_full256_step_matches_oracle(full_oracle, dtype):
     if dtype == torch.float32:
         assert dev["image"] < 1e-3 and dev["R"] < 1e-3 and dev["K"] < 1e-3
     else:
-        assert dev["image"] < 5e-2 and dev["R"] < 1e-2 and dev["K"] < 1e-2
+        # deterministic kernels: r6 measured image 5.7e-3 / 5.5e-3 (256 / 512), R <= 2.0e-4,
+        # K <= 8.5e-5 on every box -- the losses hold the north_star 1e-3 bar in bf16 too
+        assert dev["image"] < 1e-2 and dev["R"] < 1e-3 and dev["K"] < 1e-3
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_full512_step_matches_oracle(dtype):
     """BASELINE config C4 (512x512 high-res VAE): every spatial extent doubles (latent 128x128,
     AFE.in_conv / UpBlock2 at 512x512), so each kernel runs at shapes the 256 case never
-    reaches.  One step at B=1 vs the CPU oracle (fp32 mode 1e-3; bf16 reported, loose bound),
+    reaches.  One step at B=1 vs the CPU oracle (fp32 mode 1e-3; bf16 image 1e-2, losses 1e-3),
     plus the step-2 losses (after Adam on the GPU vs Adam on the oracle)."""
     torch.set_num_threads(min(16, os.cpu_count() or 1))
     ocfg = O.OracleConfig(H=512)
@@ -207,7 +209,9 @@ def test_full512_step_matches_oracle(dtype):
     if dtype == torch.float32:
         assert dev["image"] < 1e-3 and dev["R"] < 1e-3 and dev["K"] < 1e-3
     else:
-        assert dev["image"] < 5e-2 and dev["R"] < 1e-2 and dev["K"] < 1e-2
+        # deterministic kernels: r6 measured image 5.7e-3 / 5.5e-3 (256 / 512), R <= 2.0e-4,
+        # K <= 8.5e-5 on every box -- the losses hold the north_star 1e-3 bar in bf16 too
+        assert dev["image"] < 1e-2 and dev["R"] < 1e-3 and dev["K"] < 1e-3
 
 
 def test_trainer_surface(tmp_path):
